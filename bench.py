@@ -1,0 +1,191 @@
+"""Benchmark: task assignment decisions/s of the HIP push balancer.
+
+Workload (BASELINE.json configs[2], the headline): one tick over
+1M pending tasks x 64K workers, Zipf(1.5) loads capped at 32, 5 % of workers
+past the heartbeat timeout (evicted, their in-flight tasks redistributed
+first).  A step = one full tick (events -> purge -> orphans -> water-filling
+dispatch -> next state) over that synthetic state, resident in HBM; the tick
+is functional (reads the committed state, writes outputs and the next state
+to separate buffers), so K steps recompute the same tick without cached work.
+
+Prints one JSON line (rank 0).  Multi-GPU: see DESIGN.md §6.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "distributed-faas_amd"))
+
+import numpy as np  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def tick_bytes(W, Q, F, O, N, E=0):
+    """SURVEY.md §8(d) algorithmic bytes of one tick."""
+    return 16 * W + 8 * W + 4 * (N - O) + 4 * F + 8 * O + 17 * E
+
+
+def emit_bytes(W, Q, F, O, N, Qn_out):
+    """Algorithmic bytes of k_emit: assignment log writes (4 B/task), the
+    c-array and queue reads (4+4 B per LRU position), free_processes
+    read-modify-write (8 B per queued worker), next queue (4 B/entry),
+    in-flight log re-read for orphan compaction (4 B/entry) and orphan ids
+    (8 B each)."""
+    return 4 * N + 8 * Q + 8 * Q + 4 * Qn_out + 4 * F + 8 * O
+
+
+def cpu_baseline(st, T, budget_s=10.0):
+    """The oracle (C restatement of the reference loop, 1 core) on a bounded
+    prefix of the same tick: the loop as written (O(W) purge per iteration)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from oracle import Oracle
+    W = len(st["reg"])
+    cap = len(st["log"]) * 2 + T + 16
+    # calibrate the prefix length on a short run, then time ~budget_s
+    o = Oracle(W, cap, purge_mode=0)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    t0 = time.perf_counter()
+    o.tick(1000.0, 10.0, [], [], [], [], [], T, dispatch_limit=200)
+    dt = time.perf_counter() - t0
+    n = int(max(200, min(T, 200 * budget_s / max(dt, 1e-6))))
+    o = Oracle(W, cap, purge_mode=0)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    t0 = time.perf_counter()
+    out = o.tick(1000.0, 10.0, [], [], [], [], [], T, dispatch_limit=n)
+    dt = time.perf_counter() - t0
+    rate = len(out["assign"]) / dt
+    # purge-once variant (same results, no redundant O(W) purges): full tick
+    o = Oracle(W, cap, purge_mode=1)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    t0 = time.perf_counter()
+    full = o.tick(1000.0, 10.0, [], [], [], [], [], T)
+    dt1 = time.perf_counter() - t0
+    return dict(value=rate, unit="assignments/s", cores=1, kind="port",
+                sample="first %d dispatches of the configs[2] tick, loop as written (O(W) purge per "
+                       "iteration), oracle/push_oracle.c; host nproc=%d" % (len(out["assign"]), os.cpu_count()),
+                purge_once_value=len(full["assign"]) / dt1,
+                purge_once_sample="whole tick (%d dispatches), purge skipped when provably idempotent"
+                                  % len(full["assign"]))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--workers", type=int, default=65536)
+    ap.add_argument("--tasks", type=int, default=1_000_000)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=10.0)
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+
+    from faasbal import GpuBalancer, synth
+
+    W, T = args.workers, args.tasks
+    # weak scaling: every rank runs the configs[2] tick on its own shard of
+    # the pool (seeded per rank); see DESIGN.md §6 for the sharded global path.
+    st = synth.zipf_state(W=W, seed=rank)
+    cap = 2 * len(st["log"]) + T + 16
+    g = GpuBalancer(W, cap, max_events=1, device=local if world > 1 else 0)
+    g.load(st)
+    g.launch(1000.0, 10.0, n_pending=T)
+    res = g.wait()
+    n_assigned = int(res["n_assigned"])
+    O = int(res["n_orphans"])
+    F = len(st["log"])
+    Q = len(st["queue"])
+
+    def barrier():
+        if dist is not None:
+            import torch
+            t = torch.zeros(1, device="cuda")
+            dist.all_reduce(t)
+            torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        g.launch(1000.0, 10.0, n_pending=T)
+    g.sync()
+    # timed region: K back-to-back ticks on the device stream
+    barrier()
+    g.sync()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        g.launch(1000.0, 10.0, n_pending=T)
+    g.sync()
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist is not None:
+        import torch
+        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    # per-kernel device time with HIP events on the balancer's stream (same K)
+    g.timing_enable(True)
+    for _ in range(args.steps):
+        g.launch(1000.0, 10.0, n_pending=T)
+    kt = g.timing_read()
+    g.timing_enable(False)
+    g.wait()
+
+    kern = {k: (ms / n, n) for k, (ms, n) in kt.items()}
+    dom = max(kern, key=lambda k: kern[k][0])
+    dom_ms = kern[dom][0]
+    tick_dev_ms = sum(v[0] for v in kern.values())
+    if dom == "emit":
+        dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]))
+    else:
+        dom_bytes = tick_bytes(W, Q, F, O, n_assigned)
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
+    B = tick_bytes(W, Q, F, O, n_assigned)
+    value = n_assigned * args.steps * world / dt
+    line = {
+        "metric": "task assignment decisions/s (1M tasks x 64K workers, Zipf loads + 5% heartbeat timeouts)",
+        "value": value,
+        "unit": "assignments/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": dt * 1e3 / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (faasbal.synth.zipf_state, seed=rank)",
+        "config": {"workload": "configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
+                               "5%% dead -> %d orphans redistributed" % (T, W, O),
+                   "tasks_per_tick": T, "workers": W, "in_flight": F, "queue": Q,
+                   "assigned_per_tick": n_assigned, "evicted": int(res["n_evicted"]),
+                   "fill_level": int(res["fill_level"]), "parallelism": "dp%d" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes": dom_bytes,
+                     "kernel_avg_ms": dom_ms},
+        "tick": {"algorithmic_bytes": B, "device_ms": tick_dev_ms,
+                 "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,
+                 "kernels_avg_ms": {k: v[0] for k, v in kern.items()}},
+    }
+    if rank == 0 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(st, T, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

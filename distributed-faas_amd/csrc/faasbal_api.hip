@@ -1,0 +1,730 @@
+// faasbal_api.hip -- C ABI of libfaasbal.so (include/faasbal.h).
+//
+// Host orchestration of one tick on the context's HIP stream.  No CPU
+// fallback exists: every decision is computed by the kernels in
+// faasbal_kernels.hip; the host only validates arguments, stages event
+// arrays (pinned) and reads back a few scalars.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "faasbal.h"
+#include "faasbal_kernels.h"
+
+using namespace fb;
+
+namespace {
+
+struct TimedLaunch {
+    const char *name;
+    hipEvent_t a, b;
+};
+
+}  // namespace
+
+struct fb_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    int32_t W_cap = 0, E_cap = 0;
+    int64_t log_cap = 0;
+    // committed state
+    int32_t W = 0;
+    int cur = 0;  // index of the committed dense buffers
+    int32_t *free_[2] = {nullptr, nullptr};
+    uint8_t *inq[2] = {nullptr, nullptr};
+    int32_t *queue[2] = {nullptr, nullptr};
+    uint8_t *reg = nullptr;
+    double *hb = nullptr;
+    uint32_t *epoch = nullptr;
+    int32_t *log_slot = nullptr;
+    int64_t Qn = 0, head = 0;
+    uint32_t tick = 1;
+    // per-tick sparse post-message records
+    uint32_t *touched = nullptr;
+    uint8_t *post_reg = nullptr, *post_flags = nullptr, *st = nullptr;
+    int32_t *post_free = nullptr;
+    double *post_hb = nullptr;
+    uint32_t *post_epoch = nullptr;
+    // events
+    uint8_t *ev_kind = nullptr, *ev_status = nullptr;
+    int32_t *ev_val = nullptr, *ev_slot = nullptr;
+    double *ev_ts = nullptr;
+    int64_t *ev_seq = nullptr;
+    uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
+    uint32_t *rs_hist = nullptr;
+    int32_t *front_list = nullptr, *back_list = nullptr;
+    void *h_stage = nullptr;
+    // scan / plan / emit
+    int32_t *c_arr = nullptr, *qbmax = nullptr;
+    uint32_t *fcnt = nullptr, *wcnt = nullptr;
+    int64_t *fpre = nullptr, *wpre = nullptr;
+    uint32_t *qcnt = nullptr;
+    int64_t *qpre = nullptr, *A = nullptr;
+    size_t table_cap = 0;  // entries of qcnt / qpre
+    int R_cap = 0;         // entries of A
+    int64_t *orphans = nullptr;
+    int32_t *evicted = nullptr;
+    DevParams *P = nullptr, *hP = nullptr;
+    // last launch
+    bool launched = false, waited = false;
+    double l_now = 0, l_tte = 0;
+    int32_t l_E = 0;
+    int64_t l_T = 0, l_head = 0, l_Qn = 0;
+    int l_R = 64;
+    int32_t maxc_hint = 1;
+    int reruns = 0;
+    fb_tick_result last{};
+    // timing
+    bool timing = false;
+    std::vector<TimedLaunch> tl;
+    std::vector<hipEvent_t> ev_pool;
+    std::string err;
+};
+
+namespace {
+
+int fail(fb_ctx *c, int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    if (c) c->err = buf;
+    return code;
+}
+
+#define HIPCHK(ctx, expr)                                                                         \
+    do {                                                                                          \
+        hipError_t e_ = (expr);                                                                   \
+        if (e_ != hipSuccess)                                                                     \
+            return fail((ctx), FB_EHIP, "%s failed: %s (%s:%d)", #expr, hipGetErrorString(e_),    \
+                        __FILE__, __LINE__);                                                      \
+    } while (0)
+
+inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
+
+template <typename T>
+int dalloc(fb_ctx *c, T **p, size_t n) {
+    if (n == 0) n = 1;
+    hipError_t e = hipMalloc((void **)p, n * sizeof(T));
+    if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(%zu B) failed: %s", n * sizeof(T), hipGetErrorString(e));
+    return FB_OK;
+}
+
+hipEvent_t pool_event(fb_ctx *c) {
+    if (!c->ev_pool.empty()) {
+        hipEvent_t e = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    hipEventCreate(&e);
+    return e;
+}
+
+struct Timer {
+    fb_ctx *c;
+    const char *name;
+    hipEvent_t a = nullptr;
+    Timer(fb_ctx *c_, const char *n) : c(c_), name(n) {
+        if (c->timing) {
+            a = pool_event(c);
+            hipEventRecord(a, c->stream);
+        }
+    }
+    ~Timer() {
+        if (c->timing) {
+            hipEvent_t b = pool_event(c);
+            hipEventRecord(b, c->stream);
+            c->tl.push_back({name, a, b});
+        }
+    }
+};
+
+int ensure_table(fb_ctx *c, int R, int nbq) {
+    size_t need = (size_t)R * (size_t)nbq;
+    if (need > c->table_cap) {
+        size_t cap = std::max(need, c->table_cap * 2);
+        if (cap > ((size_t)1 << 31))
+            return fail(c, FB_ERANGE, "round table of %zu entries (R=%d rows x %d blocks) exceeds the limit", need, R, nbq);
+        hipFree(c->qcnt);
+        hipFree(c->qpre);
+        c->qcnt = nullptr;
+        c->qpre = nullptr;
+        int rc;
+        if ((rc = dalloc(c, &c->qcnt, cap)) || (rc = dalloc(c, &c->qpre, cap))) return rc;
+        c->table_cap = cap;
+    }
+    if (R > c->R_cap) {
+        hipFree(c->A);
+        c->A = nullptr;
+        int rc;
+        if ((rc = dalloc(c, &c->A, (size_t)R))) return rc;
+        c->R_cap = R;
+    }
+    return FB_OK;
+}
+
+int choose_R(int32_t maxc) { return std::max(64, round_up(std::max(maxc, 1), 64)); }
+
+// Enqueue every kernel of the tick described by c->l_* (events already on device).
+int enqueue_tick(fb_ctx *c) {
+    const int E = c->l_E;
+    const int W = c->W;
+    const int R = c->l_R;
+    const int64_t head = c->l_head, Qn = c->l_Qn;
+    const int64_t Qlog = Qn + 2 * (int64_t)E;
+    const int nbw = (int)cdiv(W, kBS);
+    const int nbf = (int)cdiv(head, kFTile);
+    const int nbq = (int)std::max<int64_t>(1, cdiv(Qlog, kBS));
+    int rc;
+    if ((rc = ensure_table(c, R, nbq))) return rc;
+    const int cur = c->cur, nxt = 1 - cur;
+    HIPCHK(c, hipMemsetAsync(c->P, 0, sizeof(DevParams), c->stream));
+    if (E > 0) {
+        HIPCHK(c, hipMemsetAsync(c->front_list, 0xFF, sizeof(int32_t) * E, c->stream));
+        HIPCHK(c, hipMemsetAsync(c->back_list, 0xFF, sizeof(int32_t) * E, c->stream));
+        // stable radix sort of events by slot
+        int bits = 1;
+        while ((1ll << bits) < (int64_t)W) ++bits;
+        const int passes = (bits + 7) / 8;
+        const int nb = (int)cdiv(E, kRsTile);
+        const uint32_t *kin = (const uint32_t *)c->ev_slot, *vin = nullptr;
+        for (int ps = 0; ps < passes; ++ps) {
+            Timer t(c, "rs_sort");
+            uint32_t *kout = c->keys[ps & 1], *vout = c->vals[ps & 1];
+            launch_rs_hist(kin, E, 8 * ps, c->rs_hist, nb, c->stream);
+            launch_scan_1wg(c->rs_hist, 256 * nb, c->stream);
+            launch_rs_scatter(kin, vin, kout, vout, E, 8 * ps, c->rs_hist, nb, ps == 0 ? 1 : 0, c->stream);
+            kin = kout;
+            vin = vout;
+        }
+        EvArgs a{};
+        a.E = E;
+        a.tick = c->tick;
+        a.tte = c->l_tte;
+        a.head_in = head;
+        a.skeys = kin;
+        a.svals = vin;
+        a.ev_kind = c->ev_kind;
+        a.ev_val = c->ev_val;
+        a.ev_ts = c->ev_ts;
+        a.ev_seq = c->ev_seq;
+        a.ev_status = c->ev_status;
+        a.reg = c->reg;
+        a.free_in = c->free_[cur];
+        a.hb = c->hb;
+        a.epoch = c->epoch;
+        a.inq_in = c->inq[cur];
+        a.log_slot = c->log_slot;
+        a.post_reg = c->post_reg;
+        a.post_free = c->post_free;
+        a.post_hb = c->post_hb;
+        a.post_epoch = c->post_epoch;
+        a.post_flags = c->post_flags;
+        a.touched = c->touched;
+        a.front_list = c->front_list;
+        a.back_list = c->back_list;
+        Timer t(c, "ev_apply");
+        launch_ev_apply(a, c->stream);
+    }
+    if (nbw > 0) {
+        SlotArgs a{};
+        a.W = W;
+        a.tick = c->tick;
+        a.now = c->l_now;
+        a.tte = c->l_tte;
+        a.touched = c->touched;
+        a.reg = c->reg;
+        a.hb = c->hb;
+        a.free_in = c->free_[cur];
+        a.post_reg = c->post_reg;
+        a.post_hb = c->post_hb;
+        a.post_free = c->post_free;
+        a.post_flags = c->post_flags;
+        a.st = c->st;
+        a.free_out = c->free_[nxt];
+        a.inq_out = c->inq[nxt];
+        a.wcnt = c->wcnt;
+        Timer t(c, "slots");
+        launch_slots(a, nbw, c->stream);
+    }
+    {
+        ScanArgs a{};
+        a.nbf = nbf;
+        a.nbq = nbq;
+        a.R = R;
+        a.E = E;
+        a.tick = c->tick;
+        a.Qn = Qn;
+        a.Qlog = Qlog;
+        a.head_in = head;
+        a.log_lo = 0;
+        a.log_slot = c->log_slot;
+        a.st = c->st;
+        a.epoch = c->epoch;
+        a.touched = c->touched;
+        a.post_flags = c->post_flags;
+        a.front_list = c->front_list;
+        a.queue_in = c->queue[cur];
+        a.back_list = c->back_list;
+        a.free_out = c->free_[nxt];
+        a.c_arr = c->c_arr;
+        a.fcnt = c->fcnt;
+        a.qcnt = c->qcnt;
+        a.qbmax = c->qbmax;
+        a.P = c->P;
+        Timer t(c, "scan");
+        launch_scan(a, nbf + nbq, c->stream);
+    }
+    {
+        PlanArgs a{};
+        a.nbf = nbf;
+        a.nbw = nbw;
+        a.nbq = nbq;
+        a.R = R;
+        a.fcnt = c->fcnt;
+        a.wcnt = c->wcnt;
+        a.qcnt = c->qcnt;
+        a.qbmax = c->qbmax;
+        a.fpre = c->fpre;
+        a.wpre = c->wpre;
+        a.qpre = c->qpre;
+        a.A = c->A;
+        a.P = c->P;
+        Timer t(c, "plan");
+        launch_plan(a, 2 + R, c->stream);
+    }
+    {
+        EmitArgs a{};
+        a.nbq = nbq;
+        a.nbf = nbf;
+        a.W = W;
+        a.R = R;
+        a.E = E;
+        a.Qn = Qn;
+        a.Qlog = Qlog;
+        a.head_in = head;
+        a.log_lo = 0;
+        a.T = c->l_T;
+        a.log_cap = c->log_cap;
+        a.c_arr = c->c_arr;
+        a.front_list = c->front_list;
+        a.queue_in = c->queue[cur];
+        a.back_list = c->back_list;
+        a.qpre = c->qpre;
+        a.A = c->A;
+        a.fpre = c->fpre;
+        a.wpre = c->wpre;
+        a.qbmax = c->qbmax;
+        a.st = c->st;
+        a.epoch = c->epoch;
+        a.log_slot_ro = c->log_slot;
+        a.log_slot = c->log_slot;
+        a.free_out = c->free_[nxt];
+        a.queue_out = c->queue[nxt];
+        a.inq_out = c->inq[nxt];
+        a.orphans = c->orphans;
+        a.evicted = c->evicted;
+        a.P = c->P;
+        Timer t(c, "emit");
+        launch_emit(a, nbq + nbf + nbw, c->stream);
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(c->hP, c->P, sizeof(DevParams), hipMemcpyDeviceToHost, c->stream));
+    return FB_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char *fb_last_error(const fb_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_events, int device) {
+    if (!out) return FB_EINVAL;
+    *out = nullptr;
+    if (max_workers < 1 || max_log < 1 || max_events < 0 || max_log >= ((int64_t)1 << 31) ||
+        max_workers >= (1 << 30) || max_events >= (1 << 28))
+        return FB_EINVAL;
+    fb_ctx *c = new fb_ctx();
+    c->device = device;
+    c->W_cap = max_workers;
+    c->E_cap = std::max(max_events, 1);
+    c->log_cap = max_log;
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return FB_EHIP;
+    }
+    const size_t W = (size_t)max_workers, E = (size_t)c->E_cap, F = (size_t)max_log;
+    const size_t Qlog = W + 2 * E;
+    int rc = 0;
+    for (int i = 0; i < 2 && !rc; ++i) {
+        rc = dalloc(c, &c->free_[i], W);
+        if (!rc) rc = dalloc(c, &c->inq[i], W);
+        if (!rc) rc = dalloc(c, &c->queue[i], W);
+    }
+    if (!rc) rc = dalloc(c, &c->reg, W);
+    if (!rc) rc = dalloc(c, &c->hb, W);
+    if (!rc) rc = dalloc(c, &c->epoch, W);
+    if (!rc) rc = dalloc(c, &c->log_slot, F);
+    if (!rc) rc = dalloc(c, &c->touched, W);
+    if (!rc) rc = dalloc(c, &c->post_reg, W);
+    if (!rc) rc = dalloc(c, &c->post_flags, W);
+    if (!rc) rc = dalloc(c, &c->st, W);
+    if (!rc) rc = dalloc(c, &c->post_free, W);
+    if (!rc) rc = dalloc(c, &c->post_hb, W);
+    if (!rc) rc = dalloc(c, &c->post_epoch, W);
+    if (!rc) rc = dalloc(c, &c->ev_kind, E);
+    if (!rc) rc = dalloc(c, &c->ev_status, E);
+    if (!rc) rc = dalloc(c, &c->ev_val, E);
+    if (!rc) rc = dalloc(c, &c->ev_slot, E);
+    if (!rc) rc = dalloc(c, &c->ev_ts, E);
+    if (!rc) rc = dalloc(c, &c->ev_seq, E);
+    for (int i = 0; i < 2 && !rc; ++i) {
+        rc = dalloc(c, &c->keys[i], E);
+        if (!rc) rc = dalloc(c, &c->vals[i], E);
+    }
+    if (!rc) rc = dalloc(c, &c->rs_hist, 256 * (size_t)cdiv(E, kRsTile));
+    if (!rc) rc = dalloc(c, &c->front_list, E);
+    if (!rc) rc = dalloc(c, &c->back_list, E);
+    if (!rc) rc = dalloc(c, &c->c_arr, Qlog);
+    if (!rc) rc = dalloc(c, &c->qbmax, (size_t)cdiv(Qlog, kBS));
+    if (!rc) rc = dalloc(c, &c->fcnt, (size_t)cdiv(F, kFTile));
+    if (!rc) rc = dalloc(c, &c->fpre, (size_t)cdiv(F, kFTile));
+    if (!rc) rc = dalloc(c, &c->wcnt, (size_t)cdiv(W, kBS));
+    if (!rc) rc = dalloc(c, &c->wpre, (size_t)cdiv(W, kBS));
+    if (!rc) rc = dalloc(c, &c->orphans, F);
+    if (!rc) rc = dalloc(c, &c->evicted, W);
+    if (!rc) rc = dalloc(c, &c->P, 1);
+    if (!rc && hipHostMalloc((void **)&c->hP, sizeof(DevParams), hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
+    if (!rc && hipHostMalloc(&c->h_stage, E * 32, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
+    if (!rc) rc = ensure_table(c, 64, (int)cdiv(Qlog, kBS));
+    if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
+    if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
+    if (rc) {
+        fb_destroy(c);
+        return rc;
+    }
+    *out = c;
+    return FB_OK;
+}
+
+int fb_destroy(fb_ctx *c) {
+    if (!c) return FB_OK;
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    void *bufs[] = {c->free_[0], c->free_[1], c->inq[0], c->inq[1], c->queue[0], c->queue[1], c->reg, c->hb,
+                    c->epoch, c->log_slot, c->touched, c->post_reg, c->post_flags, c->st, c->post_free,
+                    c->post_hb, c->post_epoch, c->ev_kind, c->ev_status, c->ev_val, c->ev_slot, c->ev_ts, c->ev_seq,
+                    c->keys[0], c->keys[1], c->vals[0], c->vals[1], c->rs_hist, c->front_list, c->back_list,
+                    c->c_arr, c->qbmax, c->fcnt, c->fpre, c->wcnt, c->wpre, c->qcnt, c->qpre, c->A,
+                    c->orphans, c->evicted, c->P};
+    for (void *p : bufs)
+        if (p) hipFree(p);
+    if (c->hP) hipHostFree(c->hP);
+    if (c->h_stage) hipHostFree(c->h_stage);
+    for (auto &t : c->tl) {
+        hipEventDestroy(t.a);
+        hipEventDestroy(t.b);
+    }
+    for (auto e : c->ev_pool) hipEventDestroy(e);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+    return FB_OK;
+}
+
+int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const int32_t *free_processes,
+                  const double *last_heartbeat, const uint32_t *epoch, const int32_t *queue, int64_t queue_len,
+                  const int32_t *log_slot, int64_t log_len) {
+    if (!c) return FB_EINVAL;
+    if (n_workers < 0 || n_workers > c->W_cap) return fail(c, FB_EINVAL, "n_workers %d outside [0, %d]", n_workers, c->W_cap);
+    if (log_len < 0 || log_len > c->log_cap) return fail(c, FB_EINVAL, "log_len %lld exceeds capacity", (long long)log_len);
+    if (queue_len < 0 || queue_len > n_workers) return fail(c, FB_EINVAL, "queue_len %lld", (long long)queue_len);
+    const size_t W = (size_t)n_workers;
+    std::vector<uint8_t> inq(W ? W : 1, 0);
+    int32_t maxc = 1;
+    for (int64_t i = 0; i < queue_len; ++i) {
+        const int32_t s = queue[i];
+        if (s < 0 || s >= n_workers || !registered[s] || inq[s])
+            return fail(c, FB_EINVAL, "queue[%lld] = %d is out of range, unregistered or duplicated", (long long)i, s);
+        inq[s] = 1;
+        maxc = std::max(maxc, free_processes[s]);
+    }
+    for (int64_t i = 0; i < log_len; ++i)
+        if (log_slot[i] < -1 || log_slot[i] >= n_workers)
+            return fail(c, FB_EINVAL, "log_slot[%lld] = %d out of range", (long long)i, log_slot[i]);
+    std::vector<uint8_t> reg(W ? W : 1, 0);
+    for (size_t s = 0; s < W; ++s) reg[s] = registered[s] ? 1 : 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->cur = 0;
+    if (W) {
+        HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->free_[0], free_processes, W * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->hb, last_heartbeat, W * 8, hipMemcpyHostToDevice));
+        if (epoch) HIPCHK(c, hipMemcpy(c->epoch, epoch, W * 4, hipMemcpyHostToDevice));
+        else HIPCHK(c, hipMemset(c->epoch, 0, W * 4));
+        HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
+    }
+    if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
+    if (log_len) HIPCHK(c, hipMemcpy(c->log_slot, log_slot, (size_t)log_len * 4, hipMemcpyHostToDevice));
+    c->W = n_workers;
+    c->Qn = queue_len;
+    c->head = log_len;
+    c->tick += 1;
+    c->maxc_hint = maxc;
+    c->launched = c->waited = false;
+    return FB_OK;
+}
+
+int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, double *last_heartbeat, uint32_t *epoch,
+                  int32_t *queue, int64_t *queue_len, int32_t *log_slot, int64_t *log_len) {
+    if (!c) return FB_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t W = (size_t)c->W;
+    if (W) {
+        if (registered) HIPCHK(c, hipMemcpy(registered, c->reg, W, hipMemcpyDeviceToHost));
+        if (free_processes) HIPCHK(c, hipMemcpy(free_processes, c->free_[c->cur], W * 4, hipMemcpyDeviceToHost));
+        if (last_heartbeat) HIPCHK(c, hipMemcpy(last_heartbeat, c->hb, W * 8, hipMemcpyDeviceToHost));
+        if (epoch) HIPCHK(c, hipMemcpy(epoch, c->epoch, W * 4, hipMemcpyDeviceToHost));
+    }
+    if (queue && c->Qn) HIPCHK(c, hipMemcpy(queue, c->queue[c->cur], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
+    if (queue_len) *queue_len = c->Qn;
+    if (log_slot && c->head) HIPCHK(c, hipMemcpy(log_slot, c->log_slot, (size_t)c->head * 4, hipMemcpyDeviceToHost));
+    if (log_len) *log_len = c->head;
+    return FB_OK;
+}
+
+int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+                   const int32_t *val, const double *ts, const int64_t *seq, int64_t n_pending) {
+    if (!c) return FB_EINVAL;
+    if (n_events < 0 || n_events > c->E_cap) return fail(c, FB_EINVAL, "n_events %d outside [0, %d]", n_events, c->E_cap);
+    if (n_pending < 0) return fail(c, FB_EINVAL, "n_pending < 0");
+    if (n_events && (!kind || !slot || !val || !ts))
+        return fail(c, FB_EINVAL, "event arrays must be non-NULL");
+    const int E = n_events;
+    int32_t vmax = 0;
+    for (int i = 0; i < E; ++i) {
+        if (slot[i] < 0 || slot[i] >= c->W) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %d)", i, slot[i], c->W);
+        if (kind[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, kind[i]);
+        if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
+            return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
+        if (kind[i] == FB_EV_REGISTER || kind[i] == FB_EV_RECONNECT) vmax = std::max(vmax, val[i]);
+    }
+    HIPCHK(c, hipSetDevice(c->device));
+    if (E) {
+        // stage into pinned memory, then one async copy per array
+        char *h = (char *)c->h_stage;
+        const size_t ecap = (size_t)c->E_cap;
+        uint8_t *hk = (uint8_t *)h;
+        int32_t *hs = (int32_t *)(h + ecap);
+        int32_t *hv = (int32_t *)(h + ecap * 5);
+        double *ht = (double *)(h + ecap * 9);
+        int64_t *hq = (int64_t *)(h + ecap * 17);
+        HIPCHK(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
+        memcpy(hk, kind, E);
+        memcpy(hs, slot, (size_t)E * 4);
+        memcpy(hv, val, (size_t)E * 4);
+        memcpy(ht, ts, (size_t)E * 8);
+        if (seq) memcpy(hq, seq, (size_t)E * 8);
+        else for (int i = 0; i < E; ++i) hq[i] = -1;
+        HIPCHK(c, hipMemcpyAsync(c->ev_kind, hk, E, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_slot, hs, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_val, hv, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_ts, ht, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_seq, hq, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
+    }
+    c->l_now = now;
+    c->l_tte = tte;
+    c->l_E = E;
+    c->l_T = n_pending;
+    c->l_head = c->head;
+    c->l_Qn = c->Qn;
+    c->l_R = choose_R(std::max(c->maxc_hint, vmax));
+    c->reruns = 0;
+    c->launched = true;
+    c->waited = false;
+    return enqueue_tick(c);
+}
+
+int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
+    if (!c) return FB_EINVAL;
+    if (!c->launched) return fail(c, FB_ESTATE, "fb_tick_wait without fb_tick_launch");
+    HIPCHK(c, hipSetDevice(c->device));
+    for (;;) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->hP->status == 0) break;
+        if (c->hP->status == 2)
+            return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
+                        (long long)c->l_head, (long long)c->log_cap);
+        // the queue holds free counts beyond the round table: widen and rerun
+        const int R = choose_R(c->hP->maxc);
+        if (R <= c->l_R || c->reruns > 4)
+            return fail(c, FB_ERANGE, "fill level beyond the round table (maxc %d, R %d)", c->hP->maxc, c->l_R);
+        c->l_R = R;
+        c->reruns++;
+        int rc = enqueue_tick(c);
+        if (rc) return rc;
+    }
+    const DevParams &p = *c->hP;
+    fb_tick_result r{};
+    r.n_assigned = p.N_eff;
+    r.n_orphans = p.O;
+    r.queue_len = (int64_t)p.new_qlen;
+    r.log_head = c->l_head + p.N_eff;
+    r.n_evicted = (int32_t)p.n_evicted;
+    r.fill_level = p.L;
+    r.max_free = p.maxc;
+    r.reruns = c->reruns;
+    c->last = r;
+    c->waited = true;
+    if (res) *res = r;
+    return FB_OK;
+}
+
+int fb_tick_commit(fb_ctx *c) {
+    if (!c) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "fb_tick_commit without a waited tick");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (c->W > 0) {
+        CommitArgs a{};
+        a.W = c->W;
+        a.tick = c->tick;
+        a.st = c->st;
+        a.touched = c->touched;
+        a.post_hb = c->post_hb;
+        a.post_epoch = c->post_epoch;
+        a.reg = c->reg;
+        a.hb = c->hb;
+        a.epoch = c->epoch;
+        Timer t(c, "commit");
+        launch_commit(a, (int)cdiv(c->W, kBS), c->stream);
+        HIPCHK(c, hipGetLastError());
+    }
+    c->cur = 1 - c->cur;
+    c->head = c->last.log_head;
+    c->Qn = c->last.queue_len;
+    c->maxc_hint = std::max(1, c->last.max_free);
+    c->tick += 1;
+    c->launched = c->waited = false;
+    return FB_OK;
+}
+
+int fb_get_assignments(fb_ctx *c, int64_t first, int64_t n, int32_t *dst) {
+    if (!c || !dst) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (first < 0 || n < 0 || first + n > c->last.n_assigned) return fail(c, FB_EINVAL, "assignment range");
+    if (n) HIPCHK(c, hipMemcpy(dst, c->log_slot + c->l_head + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return FB_OK;
+}
+
+int fb_get_orphans(fb_ctx *c, int64_t n, int64_t *dst) {
+    if (!c || !dst) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (n < 0 || n > c->last.n_orphans) return fail(c, FB_EINVAL, "orphan count");
+    if (n) HIPCHK(c, hipMemcpy(dst, c->orphans, (size_t)n * 8, hipMemcpyDeviceToHost));
+    return FB_OK;
+}
+
+int fb_get_evicted(fb_ctx *c, int32_t n, int32_t *dst) {
+    if (!c || !dst) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (n < 0 || n > c->last.n_evicted) return fail(c, FB_EINVAL, "evicted count");
+    if (n) HIPCHK(c, hipMemcpy(dst, c->evicted, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return FB_OK;
+}
+
+int fb_get_event_status(fb_ctx *c, int32_t n, uint8_t *dst) {
+    if (!c || !dst) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (n < 0 || n > c->l_E) return fail(c, FB_EINVAL, "event count");
+    if (n) HIPCHK(c, hipMemcpy(dst, c->ev_status, (size_t)n, hipMemcpyDeviceToHost));
+    return FB_OK;
+}
+
+int fb_tick(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+            const int32_t *val, const double *ts, const int64_t *seq, int64_t n_pending, fb_tick_result *res,
+            uint8_t *ev_status, int32_t *assign, int64_t *orphans, int32_t *evicted) {
+    int rc = fb_tick_launch(c, now, tte, n_events, kind, slot, val, ts, seq, n_pending);
+    if (rc) return rc;
+    fb_tick_result r;
+    if ((rc = fb_tick_wait(c, &r))) return rc;
+    if (ev_status && (rc = fb_get_event_status(c, n_events, ev_status))) return rc;
+    if (assign && (rc = fb_get_assignments(c, 0, r.n_assigned, assign))) return rc;
+    if (orphans && (rc = fb_get_orphans(c, r.n_orphans, orphans))) return rc;
+    if (evicted && (rc = fb_get_evicted(c, r.n_evicted, evicted))) return rc;
+    if (res) *res = r;
+    return fb_tick_commit(c);
+}
+
+int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
+    if (!c || !v) return FB_EINVAL;
+    v->free_processes = c->free_[c->cur];
+    v->last_heartbeat = c->hb;
+    v->registered = c->reg;
+    v->queue = c->queue[c->cur];
+    v->log_slot = c->log_slot;
+    v->orphans = c->orphans;
+    v->evicted = c->evicted;
+    v->n_workers = c->W;
+    v->queue_len = c->Qn;
+    v->log_head = c->head;
+    return FB_OK;
+}
+
+int fb_timing_enable(fb_ctx *c, int enable) {
+    if (!c) return FB_EINVAL;
+    c->timing = enable != 0;
+    return FB_OK;
+}
+
+int fb_timing_read(fb_ctx *c, int32_t max_kernels, const char **names, double *total_ms, int64_t *launches,
+                   int32_t *n_kernels) {
+    if (!c) return FB_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<const char *> nm;
+    std::vector<double> ms;
+    std::vector<int64_t> cnt;
+    for (auto &t : c->tl) {
+        float f = 0;
+        HIPCHK(c, hipEventElapsedTime(&f, t.a, t.b));
+        size_t k = 0;
+        while (k < nm.size() && strcmp(nm[k], t.name)) ++k;
+        if (k == nm.size()) {
+            nm.push_back(t.name);
+            ms.push_back(0);
+            cnt.push_back(0);
+        }
+        ms[k] += f;
+        cnt[k] += 1;
+        c->ev_pool.push_back(t.a);
+        c->ev_pool.push_back(t.b);
+    }
+    c->tl.clear();
+    const int n = (int)std::min<size_t>(nm.size(), (size_t)std::max(max_kernels, 0));
+    for (int i = 0; i < n; ++i) {
+        if (names) names[i] = nm[i];
+        if (total_ms) total_ms[i] = ms[i];
+        if (launches) launches[i] = cnt[i];
+    }
+    if (n_kernels) *n_kernels = n;
+    return FB_OK;
+}
+
+int fb_sync(fb_ctx *c) {
+    if (!c) return FB_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,87 @@
+"""ctypes binding of libfaasbal.so (C ABI in include/faasbal.h).
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible,
+loading fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libfaasbal.so")
+
+FB_OK, FB_EINVAL, FB_ENOMEM, FB_EHIP, FB_ERANGE, FB_ENOSPC, FB_ESTATE = 0, -1, -2, -3, -4, -5, -6
+ERRNAMES = {FB_EINVAL: "FB_EINVAL", FB_ENOMEM: "FB_ENOMEM", FB_EHIP: "FB_EHIP", FB_ERANGE: "FB_ERANGE",
+            FB_ENOSPC: "FB_ENOSPC", FB_ESTATE: "FB_ESTATE"}
+
+# Every symbol include/faasbal.h declares (checked by tests/test_abi.py).
+EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read_state", "fb_tick_launch",
+           "fb_tick_wait", "fb_tick_commit", "fb_get_assignments", "fb_get_orphans", "fb_get_evicted",
+           "fb_get_event_status", "fb_tick", "fb_device_view_get", "fb_timing_enable", "fb_timing_read",
+           "fb_sync")
+
+
+class TickResult(C.Structure):
+    _fields_ = [("n_assigned", C.c_int64), ("n_orphans", C.c_int64), ("queue_len", C.c_int64),
+                ("log_head", C.c_int64), ("n_evicted", C.c_int32), ("fill_level", C.c_int32),
+                ("max_free", C.c_int32), ("reruns", C.c_int32)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class DeviceView(C.Structure):
+    _fields_ = [("free_processes", C.c_void_p), ("last_heartbeat", C.c_void_p), ("registered", C.c_void_p),
+                ("queue", C.c_void_p), ("log_slot", C.c_void_p), ("orphans", C.c_void_p),
+                ("evicted", C.c_void_p), ("n_workers", C.c_int32), ("queue_len", C.c_int64),
+                ("log_head", C.c_int64)]
+
+
+class FaasbalError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("%s: %s" % (ERRNAMES.get(code, code), msg))
+        self.code = code
+
+
+_LIB = None
+_P = C.c_void_p
+
+
+def load(path=LIB_PATH):
+    """Load and prototype libfaasbal.so.  Raises if it has not been built."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(path):
+        raise ImportError("libfaasbal.so not found at %s: run `python -c 'import __graft_entry__ as g; "
+                          "g.build()'` (hipcc --offload-arch=gfx950)" % path)
+    lib = C.CDLL(path)
+    i32, i64, dbl = C.c_int32, C.c_int64, C.c_double
+    proto = {
+        "fb_create": (C.c_int, [C.POINTER(_P), i32, i64, i32, C.c_int]),
+        "fb_destroy": (C.c_int, [_P]),
+        "fb_last_error": (C.c_char_p, [_P]),
+        "fb_load_state": (C.c_int, [_P, i32, _P, _P, _P, _P, _P, i64, _P, i64]),
+        "fb_read_state": (C.c_int, [_P, _P, _P, _P, _P, _P, _P, _P, _P]),
+        "fb_tick_launch": (C.c_int, [_P, dbl, dbl, i32, _P, _P, _P, _P, _P, i64]),
+        "fb_tick_wait": (C.c_int, [_P, C.POINTER(TickResult)]),
+        "fb_tick_commit": (C.c_int, [_P]),
+        "fb_get_assignments": (C.c_int, [_P, i64, i64, _P]),
+        "fb_get_orphans": (C.c_int, [_P, i64, _P]),
+        "fb_get_evicted": (C.c_int, [_P, i32, _P]),
+        "fb_get_event_status": (C.c_int, [_P, i32, _P]),
+        "fb_tick": (C.c_int, [_P, dbl, dbl, i32, _P, _P, _P, _P, _P, i64, C.POINTER(TickResult),
+                              _P, _P, _P, _P]),
+        "fb_device_view_get": (C.c_int, [_P, C.POINTER(DeviceView)]),
+        "fb_timing_enable": (C.c_int, [_P, C.c_int]),
+        "fb_timing_read": (C.c_int, [_P, i32, C.POINTER(C.c_char_p), C.POINTER(dbl), C.POINTER(i64),
+                                     C.POINTER(i32)]),
+        "fb_sync": (C.c_int, [_P]),
+    }
+    for name, (res, args) in proto.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _LIB = lib
+    return lib

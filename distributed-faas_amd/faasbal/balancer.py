@@ -1,0 +1,178 @@
+"""GpuBalancer: Python handle on one libfaasbal context (one GPU, one stream).
+
+One ``tick`` replaces, for a batch of inbound messages and pending tasks, the
+work that ``PushDispatcher.start_heartbeat`` (reference
+``task_dispatcher.py:324-419``) does message by message: the inbound branches
+(:343-387), ``purge_workers`` (:241-249, called at :390) and the LRU dispatch
+block (:393-419), plus redistribution of the dead workers' in-flight tasks.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import FaasbalError, TickResult
+
+_NONE = None
+
+
+def _p(a):
+    return a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None
+
+
+def _arr(a, dt):
+    return np.ascontiguousarray(a, dtype=dt)
+
+
+class GpuBalancer:
+    """Device-resident worker table + LRU queue + in-flight log on one GPU."""
+
+    def __init__(self, max_workers, max_log, max_events=65536, device=0):
+        self.lib = _lib.load()
+        self.h = C.c_void_p()
+        rc = self.lib.fb_create(C.byref(self.h), int(max_workers), int(max_log), int(max_events), int(device))
+        if rc != 0:
+            raise FaasbalError(rc, "fb_create(max_workers=%d, max_log=%d, max_events=%d, device=%d) failed"
+                               % (max_workers, max_log, max_events, device))
+        self.max_workers = int(max_workers)
+        self.max_log = int(max_log)
+        self.max_events = int(max_events)
+        self.n_workers = 0
+        self._E = 0
+
+    # ------------------------------------------------------------------ misc
+    def _chk(self, rc):
+        if rc != 0:
+            msg = self.lib.fb_last_error(self.h)
+            raise FaasbalError(rc, msg.decode() if msg else "")
+
+    def close(self):
+        if getattr(self, "h", None) and self.h.value:
+            self.lib.fb_destroy(self.h)
+            self.h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ----------------------------------------------------------------- state
+    def load_state(self, reg, free, hb, epoch=None, queue=(), log=()):
+        reg = _arr(reg, np.uint8)
+        W = len(reg)
+        free = _arr(free, np.int32)
+        hb = _arr(hb, np.float64)
+        epoch = _arr(np.zeros(W, np.uint32) if epoch is None else epoch, np.uint32)
+        queue = _arr(queue, np.int32)
+        log = _arr(log, np.int32)
+        assert len(free) == W and len(hb) == W and len(epoch) == W
+        self._chk(self.lib.fb_load_state(self.h, W, _p(reg), _p(free), _p(hb), _p(epoch), _p(queue),
+                                         len(queue), _p(log), len(log)))
+        self.n_workers = W
+
+    def load(self, st):
+        """Load a dict as produced by faasbal.synth (reg/free/hb/epoch/queue/log)."""
+        self.load_state(st["reg"], st["free"], st["hb"], st.get("epoch"), st["queue"], st["log"])
+
+    def read_state(self, with_log=True):
+        W = self.n_workers
+        reg = np.zeros(max(W, 1), np.uint8)
+        free = np.zeros(max(W, 1), np.int32)
+        hb = np.zeros(max(W, 1), np.float64)
+        epoch = np.zeros(max(W, 1), np.uint32)
+        queue = np.zeros(max(W, 1), np.int32)
+        qlen = C.c_int64()
+        loglen = C.c_int64()
+        self._chk(self.lib.fb_read_state(self.h, None, None, None, None, None, C.byref(qlen), None,
+                                         C.byref(loglen)))
+        log = np.zeros(max(loglen.value, 1), np.int32) if with_log else None
+        self._chk(self.lib.fb_read_state(self.h, _p(reg), _p(free), _p(hb), _p(epoch), _p(queue),
+                                         C.byref(qlen), _p(log) if with_log else None, C.byref(loglen)))
+        out = dict(reg=reg[:W], free=free[:W], hb=hb[:W], epoch=epoch[:W], queue=queue[: qlen.value],
+                   head=loglen.value)
+        if with_log:
+            out["log"] = log[: loglen.value]
+        return out
+
+    # ----------------------------------------------------------------- ticks
+    def launch(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0):
+        k = _arr(ev_kind, np.uint8)
+        s = _arr(ev_slot, np.int32)
+        v = _arr(ev_val, np.int32)
+        t = _arr(ev_ts, np.float64)
+        q = None if ev_seq is None else _arr(ev_seq, np.int64)
+        E = len(k)
+        if not (len(s) == E and len(v) == E and len(t) == E and (q is None or len(q) == E)):
+            raise ValueError("event arrays differ in length")
+        self._E = E
+        self._keep = (k, s, v, t, q)
+        self._chk(self.lib.fb_tick_launch(self.h, float(now), float(tte), E, _p(k), _p(s), _p(v), _p(t),
+                                          _p(q), int(n_pending)))
+
+    def wait(self):
+        r = TickResult()
+        self._chk(self.lib.fb_tick_wait(self.h, C.byref(r)))
+        self.last = r.as_dict()
+        return self.last
+
+    def commit(self):
+        self._chk(self.lib.fb_tick_commit(self.h))
+
+    def assignments(self, first=0, n=None):
+        n = self.last["n_assigned"] - first if n is None else n
+        out = np.zeros(max(n, 1), np.int32)
+        self._chk(self.lib.fb_get_assignments(self.h, int(first), int(n), _p(out)))
+        return out[:n]
+
+    def orphans(self):
+        n = self.last["n_orphans"]
+        out = np.zeros(max(n, 1), np.int64)
+        self._chk(self.lib.fb_get_orphans(self.h, int(n), _p(out)))
+        return out[:n]
+
+    def evicted(self):
+        n = self.last["n_evicted"]
+        out = np.zeros(max(n, 1), np.int32)
+        self._chk(self.lib.fb_get_evicted(self.h, int(n), _p(out)))
+        return out[:n]
+
+    def event_status(self):
+        out = np.zeros(max(self._E, 1), np.uint8)
+        self._chk(self.lib.fb_get_event_status(self.h, int(self._E), _p(out)))
+        return out[: self._E]
+
+    def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
+             commit=True, outputs=True):
+        """One full tick.  Returns dict(result, reconnect, assign, orphans, evicted)."""
+        self.launch(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
+        res = self.wait()
+        out = dict(result=res)
+        if outputs:
+            out.update(reconnect=self.event_status(), assign=self.assignments(), orphans=self.orphans(),
+                       evicted=self.evicted())
+        if commit:
+            self.commit()
+        return out
+
+    # ---------------------------------------------------------------- timing
+    def sync(self):
+        self._chk(self.lib.fb_sync(self.h))
+
+    def timing_enable(self, on=True):
+        self._chk(self.lib.fb_timing_enable(self.h, 1 if on else 0))
+
+    def timing_read(self, max_kernels=32):
+        names = (C.c_char_p * max_kernels)()
+        ms = (C.c_double * max_kernels)()
+        cnt = (C.c_int64 * max_kernels)()
+        n = C.c_int32()
+        self._chk(self.lib.fb_timing_read(self.h, max_kernels, names, ms, cnt, C.byref(n)))
+        return {names[i].decode(): (ms[i], cnt[i]) for i in range(n.value)}
+
+    def device_view(self):
+        v = _lib.DeviceView()
+        self._chk(self.lib.fb_device_view_get(self.h, C.byref(v)))
+        return v

@@ -1,0 +1,34 @@
+"""Build libfaasbal.so in-tree for gfx950 (hipcc cross-compiles without a GPU)."""
+from __future__ import annotations
+
+import os
+import subprocess
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.dirname(HERE)
+REPO = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+SOURCES = ["faasbal_kernels.hip", "faasbal_api.hip"]
+OUT = os.path.join(HERE, "libfaasbal.so")
+ARCH = os.environ.get("FAASBAL_ARCH", "gfx950")
+
+
+def build_lib(verbose=False):
+    srcs = [os.path.join(CSRC, s) for s in SOURCES]
+    hdrs = [os.path.join(CSRC, "faasbal_kernels.h"), os.path.join(REPO, "include", "faasbal.h")]
+    if os.path.exists(OUT):
+        t = os.path.getmtime(OUT)
+        if all(os.path.getmtime(p) < t for p in srcs + hdrs):
+            return OUT
+    cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
+           "-Wno-unused-result", "-Wno-unused-value",
+           "-I" + os.path.join(REPO, "include"), "-I" + CSRC, *srcs, "-o", OUT + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build_lib(verbose=True))

@@ -1,0 +1,136 @@
+/*
+ * faasbal.h -- C ABI of the MI355X push balancer (libfaasbal.so).
+ *
+ * Drop-in boundary for the heartbeat push dispatcher of Distributed-FaaS.
+ * The reference has no FFI; its seam is the method level of PushDispatcher
+ * (reference task_dispatcher.py).  Each entry point below names the reference
+ * code it replaces.  Plain pointers and sizes only; no torch types.
+ *
+ * One tick = inbound events -> heartbeat purge -> orphan redistribution ->
+ * LRU water-filling dispatch.  All calls for one context must
+ * come from one thread (the reference loop is single-threaded).  Errors are
+ * negative return codes; fb_last_error() gives the message.  No exception
+ * crosses the ABI.
+ */
+#ifndef FAASBAL_H
+#define FAASBAL_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define FB_OK 0
+#define FB_EINVAL (-1)  /* bad argument or inconsistent state                 */
+#define FB_ENOMEM (-2)  /* device or host allocation failed                  */
+#define FB_EHIP (-3)    /* HIP runtime error                                  */
+#define FB_ERANGE (-4)  /* free counts beyond the supported round range       */
+#define FB_ENOSPC (-5)  /* in-flight log full                                 */
+#define FB_ESTATE (-6)  /* call out of order (e.g. wait without launch)       */
+
+/* Inbound message kinds (task_dispatcher.py:347-387). */
+#define FB_EV_REGISTER 0   /* {"type":"register","data":{"num_processes":n}}   */
+#define FB_EV_RECONNECT 1  /* {"type":"reconnect","data":{"free_processes":n}} */
+#define FB_EV_HEARTBEAT 2  /* {"type":"heartbeat"}                              */
+#define FB_EV_RESULT 3     /* {"type":"result", ...}; seq = task's log sequence */
+#define FB_EV_OTHER 4      /* any other type: ignored for known workers         */
+
+/* Per-event status written by a tick. */
+#define FB_EVS_APPLIED 0
+#define FB_EVS_RECONNECT 1 /* sender unknown: reply {"type":"reconnect"}, payload dropped (:356-358) */
+
+typedef struct fb_ctx fb_ctx;
+
+typedef struct fb_tick_result {
+    int64_t n_assigned;  /* tasks dispatched this tick: orphans first, then pending       */
+    int64_t n_orphans;   /* in-flight tasks of dead registrations, redistributed first    */
+    int64_t queue_len;   /* LRU queue (free_workers) length after the tick                */
+    int64_t log_head;    /* log length after the tick: task k got sequence log_head_in+k  */
+    int32_t n_evicted;   /* worker records deleted by the tick (purge_workers, :241-249)  */
+    int32_t fill_level;  /* water-filling rounds completed (L)                            */
+    int32_t max_free;    /* largest effective free count in the queue this tick           */
+    int32_t reruns;      /* internal reruns with a wider round table                      */
+} fb_tick_result;
+
+/* Device pointers of the context's state (for zero-copy consumers, e.g.
+ * torch tensors built from data_ptr).  Valid until the next fb_tick_commit. */
+typedef struct fb_device_view {
+    int32_t *free_processes; /* [n_workers]  PushWorker.free_processes (:205)  */
+    double *last_heartbeat;  /* [n_workers]  PushWorker.last_heartbeat (:206)  */
+    uint8_t *registered;     /* [n_workers]  slot present in self.workers      */
+    int32_t *queue;          /* [queue_len]  free_workers in LRU order (:327)  */
+    int32_t *log_slot;       /* [log_head]   worker slot per task sequence     */
+    int64_t *orphans;        /* last tick's redistributed sequence numbers     */
+    int32_t *evicted;        /* last tick's evicted slots                      */
+    int32_t n_workers;
+    int64_t queue_len, log_head;
+} fb_device_view;
+
+/* Context: owns every device buffer.  device = HIP device ordinal. */
+int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_events, int device);
+int fb_destroy(fb_ctx *ctx);
+const char *fb_last_error(const fb_ctx *ctx);
+
+/* Install a worker-table state (replaces building self.workers and the
+ * free_workers OrderedDict by hand, task_dispatcher.py:194, :327).
+ * queue: slots in LRU order (front first), each registered, no duplicates.
+ * log_slot: worker slot per in-flight task sequence number (-1 = completed). */
+int fb_load_state(fb_ctx *ctx, int32_t n_workers, const uint8_t *registered,
+                  const int32_t *free_processes, const double *last_heartbeat,
+                  const uint32_t *epoch, const int32_t *queue, int64_t queue_len,
+                  const int32_t *log_slot, int64_t log_len);
+
+/* Read the committed state back (any pointer may be NULL). */
+int fb_read_state(fb_ctx *ctx, uint8_t *registered, int32_t *free_processes,
+                  double *last_heartbeat, uint32_t *epoch, int32_t *queue, int64_t *queue_len,
+                  int32_t *log_slot, int64_t *log_len);
+
+/* Enqueue one tick on the context's stream (no host sync).
+ * Replaces, per tick: the inbound branches (task_dispatcher.py:343-387), the
+ * purge (:241-249, called at :390) and the dispatch block (:393-419), plus the
+ * build-defined redistribution.  Events are host arrays in arrival order with
+ * non-decreasing ts <= now; seq is the log sequence of a result's task or -1.
+ * n_pending = tasks waiting in pub/sub (carried-over ones first).
+ * Reads the committed state, writes the tick's outputs and the next state into
+ * separate buffers: launching again without fb_tick_commit recomputes the same
+ * tick (used by the benchmark). */
+int fb_tick_launch(fb_ctx *ctx, double now, double tte, int32_t n_events, const uint8_t *kind,
+                   const int32_t *slot, const int32_t *val, const double *ts, const int64_t *seq,
+                   int64_t n_pending);
+
+/* Wait for the last launched tick; fills *res.  Transparently reruns the tick
+ * with a wider round table when free counts exceeded the launch's estimate. */
+int fb_tick_wait(fb_ctx *ctx, fb_tick_result *res);
+
+/* Make the waited tick's post-state the committed state. */
+int fb_tick_commit(fb_ctx *ctx);
+
+/* Copy outputs of the waited tick to host memory. */
+int fb_get_assignments(fb_ctx *ctx, int64_t first, int64_t n, int32_t *dst); /* slot per task k */
+int fb_get_orphans(fb_ctx *ctx, int64_t n, int64_t *dst);   /* old sequence numbers, ascending */
+int fb_get_evicted(fb_ctx *ctx, int32_t n, int32_t *dst);   /* slots, ascending                */
+int fb_get_event_status(fb_ctx *ctx, int32_t n, uint8_t *dst); /* FB_EVS_* per event          */
+
+/* launch + wait + copies + commit.  Output arrays may be NULL. */
+int fb_tick(fb_ctx *ctx, double now, double tte, int32_t n_events, const uint8_t *kind,
+            const int32_t *slot, const int32_t *val, const double *ts, const int64_t *seq,
+            int64_t n_pending, fb_tick_result *res, uint8_t *ev_status, int32_t *assign,
+            int64_t *orphans, int32_t *evicted);
+
+int fb_device_view_get(fb_ctx *ctx, fb_device_view *view);
+
+/* Per-kernel device timing with HIP events on the context stream.
+ * enable=1 starts accumulating; fb_timing_read syncs and returns, per kernel
+ * name (static strings), total milliseconds and launch counts. */
+int fb_timing_enable(fb_ctx *ctx, int enable);
+int fb_timing_read(fb_ctx *ctx, int32_t max_kernels, const char **names, double *total_ms,
+                   int64_t *launches, int32_t *n_kernels);
+
+/* Synchronise the context stream (for wall-clock benchmarking). */
+int fb_sync(fb_ctx *ctx);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FAASBAL_H */

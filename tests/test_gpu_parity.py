@@ -1,0 +1,225 @@
+"""HIP balancer (through the C ABI) vs the oracle and the reference goldens.
+
+Bit-exact on every output: per-event reconnect flags, task -> slot
+assignments, orphan sequence numbers, evicted slots and the post-tick state
+(registered, free_processes, last_heartbeat, LRU queue order, in-flight log).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from faasbal import GpuBalancer, FaasbalError, synth
+from oracle import Oracle, fixture_expect, fixture_ticks
+
+pytestmark = pytest.mark.gpu
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+
+
+def _state(scen):
+    return dict(reg=scen["init_reg"], free=scen["init_free"], hb=scen["init_hb"], epoch=scen["init_epoch"],
+                queue=scen["init_queue"], log=scen["init_log"])
+
+
+def _pair(st, log_cap, max_events=4096):
+    W = len(st["reg"])
+    g = GpuBalancer(W, log_cap, max_events=max_events)
+    g.load(st)
+    o = Oracle(W, log_cap)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    return g, o
+
+
+def _cmp_out(a, b, t):
+    for k in ("reconnect", "assign", "orphans", "evicted"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg="tick %d: %s" % (t, k))
+
+
+def _cmp_state(g, o, t):
+    sg, so = g.read_state(), o.export()
+    np.testing.assert_array_equal(sg["reg"], so["reg"], err_msg="tick %d reg" % t)
+    reg = so["reg"].astype(bool)
+    np.testing.assert_array_equal(sg["free"][reg], so["free"][reg], err_msg="tick %d free" % t)
+    np.testing.assert_array_equal(sg["hb"][reg], so["hb"][reg], err_msg="tick %d hb" % t)
+    np.testing.assert_array_equal(sg["queue"], so["queue"], err_msg="tick %d queue" % t)
+    np.testing.assert_array_equal(sg["log"], so["log"], err_msg="tick %d log" % t)
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_golden_replay(path):
+    z = np.load(path)
+    W = int(z["W"])
+    cap = len(z["init_log"]) + len(z["exp_assign"]) + 16
+    g = GpuBalancer(W, cap, max_events=max(1, int(np.diff(z["ev_off"]).max(initial=0))))
+    g.load_state(z["init_reg"], z["init_free"], z["init_hb"], z["init_epoch"], z["init_queue"], z["init_log"])
+    carried = 0
+    for t, tk in enumerate(fixture_ticks(z)):
+        exp = fixture_expect(z, t)
+        n = carried + tk["n_new"]
+        out = g.tick(tk["now"], float(z["tte"]), tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"],
+                     tk["ev_seq"], n)
+        _cmp_out(out, exp, t)
+        st = g.read_state(with_log=False)
+        np.testing.assert_array_equal(st["queue"], exp["post_queue"], err_msg="tick %d queue" % t)
+        np.testing.assert_array_equal(st["reg"], exp["post_reg"], err_msg="tick %d reg" % t)
+        reg = exp["post_reg"].astype(bool)
+        np.testing.assert_array_equal(st["free"][reg], exp["post_free"][reg])
+        np.testing.assert_array_equal(st["hb"][reg], exp["post_hb"][reg])
+        carried = n + len(out["orphans"]) - len(out["assign"])
+
+
+@pytest.mark.parametrize("seed", range(40))
+def test_random_multitick_vs_oracle(seed):
+    W = [5, 37, 300, 1000][seed % 4]
+    scen = synth.random_scenario(1000 + seed, W=W, n_ticks=6, max_events=[20, 200, 2000][seed % 3],
+                                 max_new=[50, 400, 3000][(seed // 3) % 3])
+    g, o = _pair(_state(scen), len(scen["init_log"]) + 40000)
+    carried = 0
+    for t, tk in enumerate(scen["ticks"]):
+        # resolve result events to in-flight sequence numbers of the sender
+        log = o.export()["log"]
+        seq = np.full(len(tk["ev_kind"]), -1, np.int64)
+        for i in np.nonzero(tk["ev_kind"] == synth.EV_RESULT)[0]:
+            mine = np.nonzero(log == tk["ev_slot"][i])[0]
+            if len(mine) and tk["ev_pick"][i] % 5 != 4:
+                seq[i] = mine[tk["ev_pick"][i] % len(mine)]
+        n = carried + tk["n_new"]
+        args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp_out(a, b, t)
+        _cmp_state(g, o, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def _one_tick_full(st, T, now=1000.0, tte=10.0):
+    cap = len(st["log"]) + T + len(st["log"]) + 16
+    g, o = _pair(st, cap)
+    a = g.tick(now, tte, n_pending=T)
+    b = o.tick(now, tte, [], [], [], [], [], T)
+    return g, o, a, b
+
+
+def test_config2_full_size():
+    """BASELINE configs[1]: 100K tasks x 1K workers, uniform loads."""
+    st = synth.uniform_state(W=1000, seed=0)
+    g, o, a, b = _one_tick_full(st, 100_000)
+    assert a["result"]["n_assigned"] == 100_000
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+
+
+def test_config3_full_size():
+    """BASELINE configs[2] (the headline): 1M tasks x 64K workers, Zipf loads,
+    5 % heartbeat timeouts, in-flight tasks of dead workers redistributed."""
+    st = synth.zipf_state(W=65536, seed=0)
+    g, o, a, b = _one_tick_full(st, 1_000_000)
+    r = a["result"]
+    assert r["n_orphans"] > 0 and r["n_evicted"] > 0
+    assert r["n_assigned"] == 1_000_000 + r["n_orphans"]
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+    # size-independent properties
+    alive = np.asarray(o.export()["reg"], bool)
+    assert alive[a["assign"]].all()
+    assert not alive[a["evicted"]].any()
+
+
+def test_config4_single_gpu_full_size():
+    """BASELINE configs[3] workload on one GPU: 16M tasks x 1M workers."""
+    st = synth.zipf_state(W=1 << 20, seed=1)
+    g, o, a, b = _one_tick_full(st, 16_000_000)
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+
+
+def test_churn_stream_vs_oracle():
+    """Config-5 shape (64K workers, reduced rate): joins, expiries and results each tick."""
+    st = synth.zipf_state(W=65536, seed=3)
+    ticks = synth.churn_ticks(st, n_ticks=4, seed=2, tasks_per_tick=65536, join_frac=0.001,
+                              expire_frac=0.001, results_per_tick=8192)
+    g, o = _pair(st, len(st["log"]) + 4 * 65536 + 200_000, max_events=20000)
+    carried = 0
+    for t, tk in enumerate(ticks):
+        log = o.export()["log"]
+        order = np.argsort(log, kind="stable")
+        sl = log[order]
+        seq = np.full(len(tk["ev_kind"]), -1, np.int64)
+        for i in np.nonzero(tk["ev_kind"] == synth.EV_RESULT)[0]:
+            s = tk["ev_slot"][i]
+            lo, hi = np.searchsorted(sl, s), np.searchsorted(sl, s, side="right")
+            if hi > lo:
+                seq[i] = order[lo + tk["ev_pick"][i] % (hi - lo)]
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp_out(a, b, t)
+        _cmp_state(g, o, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def test_relaunch_without_commit_is_identical():
+    st = synth.zipf_state(W=4096, seed=5)
+    g = GpuBalancer(4096, len(st["log"]) * 2 + 200_000)
+    g.load(st)
+    outs = []
+    for _ in range(3):
+        g.launch(1000.0, 10.0, n_pending=50_000)
+        g.wait()
+        outs.append((g.assignments(), g.orphans(), g.evicted()))
+    for x in outs[1:]:
+        for u, v in zip(outs[0], x):
+            np.testing.assert_array_equal(u, v)
+
+
+def test_wide_free_counts_rerun():
+    """A result pushes free past the launch's round table: the tick reruns wider."""
+    W = 3
+    st = dict(reg=np.ones(W, np.uint8), free=np.array([64, 3, 200], np.int32), hb=np.full(W, 999.0),
+              epoch=np.zeros(W, np.uint32), queue=np.array([0, 1], np.int32), log=np.array([0, 0], np.int32))
+    g, o = _pair(st, 10_000)
+    args = (1000.0, 10.0, [synth.EV_RESULT], [0], [0], [999.5], [1], 1000)
+    a, b = g.tick(*args), o.tick(*args)
+    assert a["result"]["reruns"] >= 1
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+    # large counts by register/reconnect
+    args = (1001.0, 10.0, [synth.EV_REGISTER, synth.EV_RECONNECT], [2, 1], [3000, 7], [1000.5, 1000.7], [-1, -1],
+            5000)
+    a, b = g.tick(*args), o.tick(*args)
+    _cmp_out(a, b, 1)
+    _cmp_state(g, o, 1)
+
+
+def test_edge_cases():
+    # no workers registered, tasks pending
+    st = dict(reg=np.zeros(4, np.uint8), free=np.zeros(4, np.int32), hb=np.zeros(4), epoch=np.zeros(4, np.uint32),
+              queue=np.zeros(0, np.int32), log=np.zeros(0, np.int32))
+    g, o = _pair(st, 1000)
+    for t, args in enumerate([
+        (10.0, 10.0, [], [], [], [], [], 5),                        # empty everything
+        (11.0, 10.0, [synth.EV_HEARTBEAT], [2], [0], [10.5], [-1], 5),  # unknown id -> reconnect
+        (12.0, 10.0, [synth.EV_RESULT], [2], [0], [11.0], [-1], 5),     # free 0 -> 1: back of queue
+        (40.0, 10.0, [], [], [], [], [], 5),                        # everybody expires
+    ]):
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp_out(a, b, t)
+        _cmp_state(g, o, t)
+
+
+def test_log_full_is_an_error():
+    st = synth.uniform_state(W=100, seed=1)
+    g = GpuBalancer(100, 1000)
+    g.load(st)
+    with pytest.raises(FaasbalError):
+        g.tick(1000.0, 10.0, n_pending=5000)
+
+
+def test_invalid_events_rejected():
+    st = synth.uniform_state(W=10, seed=1)
+    g = GpuBalancer(10, 1000)
+    g.load(st)
+    with pytest.raises(FaasbalError):
+        g.tick(1000.0, 10.0, [0], [10], [1], [999.0], [-1], 0)   # slot out of range
+    with pytest.raises(FaasbalError):
+        g.tick(1000.0, 10.0, [0, 0], [1, 2], [1, 1], [999.0, 998.0], [-1, -1], 0)  # ts decreasing
