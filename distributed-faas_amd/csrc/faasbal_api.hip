@@ -47,6 +47,7 @@ struct fb_ctx {
     // per-tick sparse post-message records
     uint32_t *touched = nullptr;
     uint8_t *post_reg = nullptr, *post_flags = nullptr, *st = nullptr;
+    unsigned long long *dmask = nullptr;
     int32_t *post_free = nullptr;
     double *post_hb = nullptr;
     uint32_t *post_epoch = nullptr;
@@ -60,7 +61,9 @@ struct fb_ctx {
     int32_t *front_list = nullptr, *back_list = nullptr;
     void *h_stage = nullptr;
     // scan / plan / emit
-    int32_t *c_arr = nullptr, *qbmax = nullptr;
+    int32_t *c_arr = nullptr, *qbmax = nullptr, *qbm_raw = nullptr;
+    unsigned long long *csum = nullptr;
+    uint8_t *ofl = nullptr;
     uint32_t *fcnt = nullptr, *wcnt = nullptr;
     int64_t *fpre = nullptr, *wpre = nullptr;
     uint32_t *qcnt = nullptr;
@@ -69,7 +72,15 @@ struct fb_ctx {
     int R_cap = 0;         // entries of A
     int64_t *orphans = nullptr;
     int32_t *evicted = nullptr;
-    DevParams *P = nullptr, *hP = nullptr;
+    DevTotals *P = nullptr;
+    HostOut *hout = nullptr, *hout_dev = nullptr;  // host-mapped results written by k_emit
+    unsigned long long *dbg = nullptr;             // diagnostic stamps
+    size_t dbg_n = 0;
+    int force_plan = 0;
+    void *arena = nullptr;    // every fixed-size device buffer, carved from one allocation
+    size_t arena_bytes = 0;
+    bool table_owned = false; // qcnt/qpre grown beyond the arena's reservation
+    bool A_owned = false;
     // last launch
     bool launched = false, waited = false;
     double l_now = 0, l_tte = 0;
@@ -117,6 +128,32 @@ int dalloc(fb_ctx *c, T **p, size_t n) {
     return FB_OK;
 }
 
+// One device allocation for every fixed-size buffer: random per-slot gathers then
+// stay within large, contiguous mappings (fewer GPU TLB misses than many small
+// hipMalloc regions).
+struct ArenaPlan {
+    std::vector<std::pair<void **, size_t>> req;
+    template <typename T>
+    void add(T **p, size_t n) {
+        req.push_back({(void **)p, std::max<size_t>(n, 1) * sizeof(T)});
+    }
+};
+
+int arena_commit(fb_ctx *c, ArenaPlan &ap) {
+    size_t total = 0;
+    for (auto &r : ap.req) total += (r.second + 255) & ~(size_t)255;
+    total = (total + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
+    hipError_t e = hipMalloc(&c->arena, total);
+    if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(arena %zu B) failed: %s", total, hipGetErrorString(e));
+    c->arena_bytes = total;
+    char *p = (char *)c->arena;
+    for (auto &r : ap.req) {
+        *r.first = p;
+        p += (r.second + 255) & ~(size_t)255;
+    }
+    return FB_OK;
+}
+
 hipEvent_t pool_event(fb_ctx *c) {
     if (!c->ev_pool.empty()) {
         hipEvent_t e = c->ev_pool.back();
@@ -153,25 +190,35 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
         size_t cap = std::max(need, c->table_cap * 2);
         if (cap > ((size_t)1 << 31))
             return fail(c, FB_ERANGE, "round table of %zu entries (R=%d rows x %d blocks) exceeds the limit", need, R, nbq);
-        hipFree(c->qcnt);
-        hipFree(c->qpre);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->table_owned) {
+            hipFree(c->qcnt);
+            hipFree(c->qpre);
+        }
         c->qcnt = nullptr;
         c->qpre = nullptr;
         int rc;
         if ((rc = dalloc(c, &c->qcnt, cap)) || (rc = dalloc(c, &c->qpre, cap))) return rc;
         c->table_cap = cap;
+        c->table_owned = true;
     }
     if (R > c->R_cap) {
-        hipFree(c->A);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->A_owned) hipFree(c->A);
         c->A = nullptr;
         int rc;
         if ((rc = dalloc(c, &c->A, (size_t)R))) return rc;
         c->R_cap = R;
+        c->A_owned = true;
     }
     return FB_OK;
 }
 
-int choose_R(int32_t maxc) { return std::max(64, round_up(std::max(maxc, 1), 64)); }
+int choose_R(int32_t maxc) {
+    int R = 32;
+    while (R < maxc) R <<= 1;
+    return R;
+}
 
 // Enqueue every kernel of the tick described by c->l_* (events already on device).
 int enqueue_tick(fb_ctx *c) {
@@ -180,13 +227,12 @@ int enqueue_tick(fb_ctx *c) {
     const int R = c->l_R;
     const int64_t head = c->l_head, Qn = c->l_Qn;
     const int64_t Qlog = Qn + 2 * (int64_t)E;
-    const int nbw = (int)cdiv(W, kBS);
+    const int nbw = (int)std::max<int64_t>(1, cdiv(W, kBS));
     const int nbf = (int)cdiv(head, kFTile);
     const int nbq = (int)std::max<int64_t>(1, cdiv(Qlog, kBS));
     int rc;
     if ((rc = ensure_table(c, R, nbq))) return rc;
     const int cur = c->cur, nxt = 1 - cur;
-    HIPCHK(c, hipMemsetAsync(c->P, 0, sizeof(DevParams), c->stream));
     if (E > 0) {
         HIPCHK(c, hipMemsetAsync(c->front_list, 0xFF, sizeof(int32_t) * E, c->stream));
         HIPCHK(c, hipMemsetAsync(c->back_list, 0xFF, sizeof(int32_t) * E, c->stream));
@@ -234,110 +280,85 @@ int enqueue_tick(fb_ctx *c) {
         Timer t(c, "ev_apply");
         launch_ev_apply(a, c->stream);
     }
-    if (nbw > 0) {
-        SlotArgs a{};
-        a.W = W;
-        a.tick = c->tick;
-        a.now = c->l_now;
-        a.tte = c->l_tte;
-        a.touched = c->touched;
-        a.reg = c->reg;
-        a.hb = c->hb;
-        a.free_in = c->free_[cur];
-        a.post_reg = c->post_reg;
-        a.post_hb = c->post_hb;
-        a.post_free = c->post_free;
-        a.post_flags = c->post_flags;
-        a.st = c->st;
-        a.free_out = c->free_[nxt];
-        a.inq_out = c->inq[nxt];
-        a.wcnt = c->wcnt;
+    TickArgs a{};
+    a.W = W;
+    a.E = E;
+    a.R = R;
+    a.nbw = nbw;
+    a.nbf = nbf;
+    a.nbq = nbq;
+    // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
+    a.fused = (!c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
+    a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
+    a.tick = c->tick;
+    a.now = c->l_now;
+    a.tte = c->l_tte;
+    a.Qn = Qn;
+    a.Qlog = Qlog;
+    a.head_in = head;
+    a.T = c->l_T;
+    a.log_cap = c->log_cap;
+    a.reg = c->reg;
+    a.hb = c->hb;
+    a.free_in = c->free_[cur];
+    a.epoch = c->epoch;
+    a.queue_in = c->queue[cur];
+    a.touched = c->touched;
+    a.post_reg = c->post_reg;
+    a.post_flags = c->post_flags;
+    a.post_hb = c->post_hb;
+    a.post_free = c->post_free;
+    a.front_list = c->front_list;
+    a.back_list = c->back_list;
+    a.st = c->st;
+    a.dmask = c->dmask;
+    a.c_arr = c->c_arr;
+    a.ofl = c->ofl;
+    a.wcnt = c->wcnt;
+    a.fcnt = c->fcnt;
+    a.qcnt = c->qcnt;
+    a.qbmax = c->qbmax;
+    a.qbm_raw = c->qbm_raw;
+    a.csum = c->csum;
+    a.fpre = c->fpre;
+    a.wpre = c->wpre;
+    a.qpre = c->qpre;
+    a.A = c->A;
+    a.P = c->P;
+    a.log_slot = c->log_slot;
+    a.free_out = c->free_[nxt];
+    a.inq_out = c->inq[nxt];
+    a.queue_out = c->queue[nxt];
+    a.orphans = c->orphans;
+    a.evicted = c->evicted;
+    a.hout = c->hout_dev;
+    {
+        const size_t need = (size_t)2 * (nbw + nbf + nbq) * 16 + 16;
+        if (need > c->dbg_n) {
+            hipFree(c->dbg);
+            c->dbg = nullptr;
+            if ((rc = dalloc(c, &c->dbg, need))) return rc;
+            c->dbg_n = need;
+        }
+        a.dbg = c->dbg;
+    }
+    {
         Timer t(c, "slots");
-        launch_slots(a, nbw, c->stream);
+        launch_slots(a, c->stream);
     }
     {
-        ScanArgs a{};
-        a.nbf = nbf;
-        a.nbq = nbq;
-        a.R = R;
-        a.E = E;
-        a.tick = c->tick;
-        a.Qn = Qn;
-        a.Qlog = Qlog;
-        a.head_in = head;
-        a.log_lo = 0;
-        a.log_slot = c->log_slot;
-        a.st = c->st;
-        a.epoch = c->epoch;
-        a.touched = c->touched;
-        a.post_flags = c->post_flags;
-        a.front_list = c->front_list;
-        a.queue_in = c->queue[cur];
-        a.back_list = c->back_list;
-        a.free_out = c->free_[nxt];
-        a.c_arr = c->c_arr;
-        a.fcnt = c->fcnt;
-        a.qcnt = c->qcnt;
-        a.qbmax = c->qbmax;
-        a.P = c->P;
         Timer t(c, "scan");
-        launch_scan(a, nbf + nbq, c->stream);
+        launch_scan(a, c->stream);
     }
-    {
-        PlanArgs a{};
-        a.nbf = nbf;
-        a.nbw = nbw;
-        a.nbq = nbq;
-        a.R = R;
-        a.fcnt = c->fcnt;
-        a.wcnt = c->wcnt;
-        a.qcnt = c->qcnt;
-        a.qbmax = c->qbmax;
-        a.fpre = c->fpre;
-        a.wpre = c->wpre;
-        a.qpre = c->qpre;
-        a.A = c->A;
-        a.P = c->P;
+    if (!a.fused) {
         Timer t(c, "plan");
-        launch_plan(a, 2 + R, c->stream);
+        launch_plan(a, c->stream);
     }
     {
-        EmitArgs a{};
-        a.nbq = nbq;
-        a.nbf = nbf;
-        a.W = W;
-        a.R = R;
-        a.E = E;
-        a.Qn = Qn;
-        a.Qlog = Qlog;
-        a.head_in = head;
-        a.log_lo = 0;
-        a.T = c->l_T;
-        a.log_cap = c->log_cap;
-        a.c_arr = c->c_arr;
-        a.front_list = c->front_list;
-        a.queue_in = c->queue[cur];
-        a.back_list = c->back_list;
-        a.qpre = c->qpre;
-        a.A = c->A;
-        a.fpre = c->fpre;
-        a.wpre = c->wpre;
-        a.qbmax = c->qbmax;
-        a.st = c->st;
-        a.epoch = c->epoch;
-        a.log_slot_ro = c->log_slot;
-        a.log_slot = c->log_slot;
-        a.free_out = c->free_[nxt];
-        a.queue_out = c->queue[nxt];
-        a.inq_out = c->inq[nxt];
-        a.orphans = c->orphans;
-        a.evicted = c->evicted;
-        a.P = c->P;
         Timer t(c, "emit");
-        launch_emit(a, nbq + nbf + nbw, c->stream);
+        launch_emit(a, c->stream);
     }
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemcpyAsync(c->hP, c->P, sizeof(DevParams), hipMemcpyDeviceToHost, c->stream));
     return FB_OK;
 }
 
@@ -364,48 +385,64 @@ int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_ev
     }
     const size_t W = (size_t)max_workers, E = (size_t)c->E_cap, F = (size_t)max_log;
     const size_t Qlog = W + 2 * E;
-    int rc = 0;
-    for (int i = 0; i < 2 && !rc; ++i) {
-        rc = dalloc(c, &c->free_[i], W);
-        if (!rc) rc = dalloc(c, &c->inq[i], W);
-        if (!rc) rc = dalloc(c, &c->queue[i], W);
+    ArenaPlan ap;
+    for (int i = 0; i < 2; ++i) {
+        ap.add(&c->free_[i], W);
+        ap.add(&c->inq[i], W);
+        ap.add(&c->queue[i], W);
     }
-    if (!rc) rc = dalloc(c, &c->reg, W);
-    if (!rc) rc = dalloc(c, &c->hb, W);
-    if (!rc) rc = dalloc(c, &c->epoch, W);
-    if (!rc) rc = dalloc(c, &c->log_slot, F);
-    if (!rc) rc = dalloc(c, &c->touched, W);
-    if (!rc) rc = dalloc(c, &c->post_reg, W);
-    if (!rc) rc = dalloc(c, &c->post_flags, W);
-    if (!rc) rc = dalloc(c, &c->st, W);
-    if (!rc) rc = dalloc(c, &c->post_free, W);
-    if (!rc) rc = dalloc(c, &c->post_hb, W);
-    if (!rc) rc = dalloc(c, &c->post_epoch, W);
-    if (!rc) rc = dalloc(c, &c->ev_kind, E);
-    if (!rc) rc = dalloc(c, &c->ev_status, E);
-    if (!rc) rc = dalloc(c, &c->ev_val, E);
-    if (!rc) rc = dalloc(c, &c->ev_slot, E);
-    if (!rc) rc = dalloc(c, &c->ev_ts, E);
-    if (!rc) rc = dalloc(c, &c->ev_seq, E);
-    for (int i = 0; i < 2 && !rc; ++i) {
-        rc = dalloc(c, &c->keys[i], E);
-        if (!rc) rc = dalloc(c, &c->vals[i], E);
+    ap.add(&c->reg, W);
+    ap.add(&c->hb, W);
+    ap.add(&c->epoch, W);
+    ap.add(&c->touched, W);
+    ap.add(&c->post_reg, W);
+    ap.add(&c->post_flags, W);
+    ap.add(&c->st, W);
+    ap.add(&c->dmask, (W + 63) / 64);
+    ap.add(&c->post_free, W);
+    ap.add(&c->post_hb, W);
+    ap.add(&c->post_epoch, W);
+    ap.add(&c->ev_kind, E);
+    ap.add(&c->ev_status, E);
+    ap.add(&c->ev_val, E);
+    ap.add(&c->ev_slot, E);
+    ap.add(&c->ev_ts, E);
+    ap.add(&c->ev_seq, E);
+    for (int i = 0; i < 2; ++i) {
+        ap.add(&c->keys[i], E);
+        ap.add(&c->vals[i], E);
     }
-    if (!rc) rc = dalloc(c, &c->rs_hist, 256 * (size_t)cdiv(E, kRsTile));
-    if (!rc) rc = dalloc(c, &c->front_list, E);
-    if (!rc) rc = dalloc(c, &c->back_list, E);
-    if (!rc) rc = dalloc(c, &c->c_arr, Qlog);
-    if (!rc) rc = dalloc(c, &c->qbmax, (size_t)cdiv(Qlog, kBS));
-    if (!rc) rc = dalloc(c, &c->fcnt, (size_t)cdiv(F, kFTile));
-    if (!rc) rc = dalloc(c, &c->fpre, (size_t)cdiv(F, kFTile));
-    if (!rc) rc = dalloc(c, &c->wcnt, (size_t)cdiv(W, kBS));
-    if (!rc) rc = dalloc(c, &c->wpre, (size_t)cdiv(W, kBS));
-    if (!rc) rc = dalloc(c, &c->orphans, F);
-    if (!rc) rc = dalloc(c, &c->evicted, W);
-    if (!rc) rc = dalloc(c, &c->P, 1);
-    if (!rc && hipHostMalloc((void **)&c->hP, sizeof(DevParams), hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
+    ap.add(&c->rs_hist, 256 * (size_t)cdiv(E, kRsTile));
+    ap.add(&c->front_list, E);
+    ap.add(&c->back_list, E);
+    ap.add(&c->c_arr, Qlog);
+    ap.add(&c->qbmax, (size_t)cdiv(Qlog, kBS));
+    ap.add(&c->qbm_raw, (size_t)cdiv(Qlog, kBS));
+    ap.add(&c->csum, (size_t)cdiv(Qlog, kBS));
+    ap.add(&c->ofl, (size_t)cdiv(F, kFTile) * kBS);
+    ap.add(&c->fcnt, (size_t)cdiv(F, kFTile));
+    ap.add(&c->fpre, (size_t)cdiv(F, kFTile));
+    ap.add(&c->wcnt, (size_t)cdiv(W, kBS));
+    ap.add(&c->wpre, (size_t)cdiv(W, kBS));
+    ap.add(&c->evicted, W);
+    ap.add(&c->P, 1);
+    const size_t tab = (size_t)128 * (size_t)cdiv(Qlog, kBS);
+    ap.add(&c->qcnt, tab);
+    ap.add(&c->qpre, tab);
+    ap.add(&c->A, 128);
+    ap.add(&c->log_slot, F);
+    ap.add(&c->orphans, F);
+    int rc = arena_commit(c, ap);
+    if (!rc) {
+        c->table_cap = tab;
+        c->R_cap = 128;
+    }
+    if (!rc && hipHostMalloc((void **)&c->hout, sizeof(HostOut), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+        rc = FB_ENOMEM;
+    if (!rc && hipHostGetDevicePointer((void **)&c->hout_dev, c->hout, 0) != hipSuccess) rc = FB_EHIP;
+    if (!rc) memset(c->hout, 0, sizeof(HostOut));
+    if (!rc && getenv("FAASBAL_FORCE_PLAN")) c->force_plan = atoi(getenv("FAASBAL_FORCE_PLAN"));
     if (!rc && hipHostMalloc(&c->h_stage, E * 32, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
-    if (!rc) rc = ensure_table(c, 64, (int)cdiv(Qlog, kBS));
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
     if (rc) {
@@ -420,15 +457,14 @@ int fb_destroy(fb_ctx *c) {
     if (!c) return FB_OK;
     hipSetDevice(c->device);
     if (c->stream) hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->free_[0], c->free_[1], c->inq[0], c->inq[1], c->queue[0], c->queue[1], c->reg, c->hb,
-                    c->epoch, c->log_slot, c->touched, c->post_reg, c->post_flags, c->st, c->post_free,
-                    c->post_hb, c->post_epoch, c->ev_kind, c->ev_status, c->ev_val, c->ev_slot, c->ev_ts, c->ev_seq,
-                    c->keys[0], c->keys[1], c->vals[0], c->vals[1], c->rs_hist, c->front_list, c->back_list,
-                    c->c_arr, c->qbmax, c->fcnt, c->fpre, c->wcnt, c->wpre, c->qcnt, c->qpre, c->A,
-                    c->orphans, c->evicted, c->P};
-    for (void *p : bufs)
-        if (p) hipFree(p);
-    if (c->hP) hipHostFree(c->hP);
+    if (c->table_owned) {
+        hipFree(c->qcnt);
+        hipFree(c->qpre);
+    }
+    if (c->A_owned) hipFree(c->A);
+    if (c->dbg) hipFree(c->dbg);
+    if (c->arena) hipFree(c->arena);
+    if (c->hout) hipHostFree(c->hout);
     if (c->h_stage) hipHostFree(c->h_stage);
     for (auto &t : c->tl) {
         hipEventDestroy(t.a);
@@ -561,20 +597,20 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     HIPCHK(c, hipSetDevice(c->device));
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (c->hP->status == 0) break;
-        if (c->hP->status == 2)
+        if (c->hout->status == 0) break;
+        if (c->hout->status == 2)
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
                         (long long)c->l_head, (long long)c->log_cap);
         // the queue holds free counts beyond the round table: widen and rerun
-        const int R = choose_R(c->hP->maxc);
+        const int R = choose_R(c->hout->maxc);
         if (R <= c->l_R || c->reruns > 4)
-            return fail(c, FB_ERANGE, "fill level beyond the round table (maxc %d, R %d)", c->hP->maxc, c->l_R);
+            return fail(c, FB_ERANGE, "fill level beyond the round table (maxc %d, R %d)", c->hout->maxc, c->l_R);
         c->l_R = R;
         c->reruns++;
         int rc = enqueue_tick(c);
         if (rc) return rc;
     }
-    const DevParams &p = *c->hP;
+    const HostOut &p = *c->hout;
     fb_tick_result r{};
     r.n_assigned = p.N_eff;
     r.n_orphans = p.O;
@@ -717,6 +753,32 @@ int fb_timing_read(fb_ctx *c, int32_t max_kernels, const char **names, double *t
         if (launches) launches[i] = cnt[i];
     }
     if (n_kernels) *n_kernels = n;
+    return FB_OK;
+}
+
+// Device self-test of the wave/block primitives (DPP scans); *errors = mismatches.
+int fb_selftest(fb_ctx *c, int32_t *errors) {
+    if (!c || !errors) return FB_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    uint32_t *d = nullptr;
+    int rc = dalloc(c, &d, 1);
+    if (rc) return rc;
+    HIPCHK(c, hipMemsetAsync(d, 0, 4, c->stream));
+    for (uint32_t seed = 1; seed <= 8; ++seed) launch_selftest(d, seed * 7919u, c->stream);
+    uint32_t h = 0;
+    HIPCHK(c, hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    hipFree(d);
+    *errors = (int32_t)h;
+    return FB_OK;
+}
+
+// Diagnostic: copy the stamp buffer (meaningful only in FAASBAL_STAMPS builds).
+int fb_debug_read(fb_ctx *c, unsigned long long *dst, int64_t n, int64_t *n_total) {
+    if (!c) return FB_EINVAL;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (n_total) *n_total = (int64_t)c->dbg_n;
+    if (dst && n > 0) HIPCHK(c, hipMemcpy(dst, c->dbg, (size_t)std::min<int64_t>(n, c->dbg_n) * 8, hipMemcpyDeviceToHost));
     return FB_OK;
 }
 

@@ -11,6 +11,10 @@ constexpr int kFItems = 8;         // log entries per thread in log-role blocks
 constexpr int kFTile = kBS * kFItems;
 constexpr int kRsItems = 8;        // radix sort: keys per thread per tile
 constexpr int kRsTile = kBS * kRsItems;
+constexpr int kRFused = 128;       // fused tick: round table of at most 128 rows ...
+constexpr int kTabLd = 16;         // ... read by at most 16 int4 loads per thread
+constexpr int kPeel = 4;           // fused tick: block-count arrays of at most 4*256 entries
+constexpr int kLdsBitmapSlots = 1 << 17;  // died bitmap staged in LDS up to 128K slots (16 KB)
 
 // event kinds / status (include/faasbal.h)
 constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3;
@@ -24,19 +28,25 @@ constexpr uint8_t kStEvicted = 4;    // record deleted during the tick and not r
 constexpr int kPfDiedStart = 1;
 constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 
-// device-resident per-tick scalars (zeroed by every launch)
-struct DevParams {
-    unsigned long long cap_total;  // sum of c over live queued workers
-    unsigned long long new_qlen;   // next LRU queue length
-    int64_t O;                     // orphans
+// results of a tick, written by k_emit into host-mapped pinned memory
+struct HostOut {
+    int64_t O;          // orphans redistributed first
     int64_t n_evicted;
-    int64_t N_eff;                 // tasks dispatched
-    int64_t p;                     // tasks of the partial round L
-    int64_t AL;                    // |A_L|
-    int32_t maxc;                  // max c
-    int32_t L;                     // fill level
-    int32_t status;                // 1 = round table too narrow (rerun wider), 2 = log full
+    int64_t N_eff;      // tasks dispatched
+    int64_t p;          // tasks of the partial round L
+    int64_t AL;         // |A_L|
+    int64_t new_qlen;   // next LRU queue length
+    int64_t cap_total;  // sum of c over live queued workers
+    int32_t L;          // fill level
+    int32_t maxc;       // max c
+    int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
     int32_t pad;
+};
+
+// totals computed by k_plan (large grids only; device memory, no atomics)
+struct DevTotals {
+    int64_t O, n_evicted, cap_total;
+    int32_t maxc, pad;
 };
 
 struct EvArgs {
@@ -65,67 +75,45 @@ struct EvArgs {
     int32_t *front_list, *back_list;
 };
 
-struct SlotArgs {
-    int W;
+// one argument block for k_scan / k_plan / k_emit
+struct TickArgs {
+    int W, E, R, nbw, nbf, nbq;
+    int fused;       // 1: k_emit derives the cross-block prefixes itself (no k_plan launch)
+    int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
     uint32_t tick;
     double now, tte;
-    const uint32_t *touched;
+    int64_t Qn, Qlog, head_in, T, log_cap;
+    // committed state
     const uint8_t *reg;
     const double *hb;
     const int32_t *free_in;
-    const uint8_t *post_reg;
+    const uint32_t *epoch;
+    const int32_t *queue_in;
+    // this tick's message results
+    const uint32_t *touched;
+    const uint8_t *post_reg, *post_flags;
     const double *post_hb;
     const int32_t *post_free;
-    const uint8_t *post_flags;
+    const int32_t *front_list, *back_list;
+    // intermediates
     uint8_t *st;
-    int32_t *free_out;
-    uint8_t *inq_out;
-    uint32_t *wcnt;
-};
-
-struct ScanArgs {
-    int nbf, nbq, R, E;
-    uint32_t tick;
-    int64_t Qn, Qlog, head_in, log_lo;
-    const int32_t *log_slot;
-    const uint8_t *st;
-    const uint32_t *epoch;
-    const uint32_t *touched;
-    const uint8_t *post_flags;
-    const int32_t *front_list, *queue_in, *back_list;
-    const int32_t *free_out;
-    int32_t *c_arr;
-    uint32_t *fcnt;
-    uint32_t *qcnt;
-    int32_t *qbmax;
-    DevParams *P;
-};
-
-struct PlanArgs {
-    int nbf, nbw, nbq, R;
-    const uint32_t *fcnt, *wcnt, *qcnt;
-    const int32_t *qbmax;
+    unsigned long long *dmask;  // bit s: the registration alive at tick start died this tick
+    int32_t *c_arr;  // raw free_processes of a live LRU position, INT32_MIN otherwise
+    uint8_t *ofl;    // orphan flags, one byte per F-thread (8 log entries)
+    uint32_t *wcnt, *fcnt, *qcnt;
+    int32_t *qbmax, *qbm_raw;
+    unsigned long long *csum;
     int64_t *fpre, *wpre, *qpre, *A;
-    DevParams *P;
-};
-
-struct EmitArgs {
-    int nbq, nbf, W, R, E;
-    int64_t Qn, Qlog, head_in, log_lo, T, log_cap;
-    const int32_t *c_arr;
-    const int32_t *front_list, *queue_in, *back_list;
-    const int64_t *qpre, *A, *fpre, *wpre;
-    const int32_t *qbmax;
-    const uint8_t *st;
-    const uint32_t *epoch;
-    const int32_t *log_slot_ro;
+    DevTotals *P;
+    // outputs
     int32_t *log_slot;
-    int32_t *free_out;
-    int32_t *queue_out;
+    int32_t *free_out;  // next free_processes; INT32_MIN for slots without a live record
     uint8_t *inq_out;
+    int32_t *queue_out;
     int64_t *orphans;
     int32_t *evicted;
-    DevParams *P;
+    HostOut *hout;
+    unsigned long long *dbg;  // diagnostic stamps (FAASBAL_STAMPS builds only)
 };
 
 struct CommitArgs {
@@ -147,10 +135,11 @@ void launch_scan_1wg(uint32_t *a, int n, Stream st);
 void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,
                        int shift, const uint32_t *hist, int nblk, int identity_vals, Stream st);
 void launch_ev_apply(const EvArgs &a, Stream st);
-void launch_slots(const SlotArgs &a, int grid, Stream st);
-void launch_scan(const ScanArgs &a, int grid, Stream st);
-void launch_plan(const PlanArgs &a, int grid, Stream st);
-void launch_emit(const EmitArgs &a, int grid, Stream st);
+void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
+void launch_slots(const TickArgs &a, Stream st);
+void launch_scan(const TickArgs &a, Stream st);
+void launch_plan(const TickArgs &a, Stream st);
+void launch_emit(const TickArgs &a, Stream st);
 void launch_commit(const CommitArgs &a, int grid, Stream st);
 
 }  // namespace fb

@@ -21,11 +21,119 @@
 
 namespace fb {
 
+// Diagnostic builds (-DFAASBAL_STAMPS) record s_memtime at phase boundaries of
+// thread 0 of every block into a.dbg[block * 16 + slot]; no output reads them.
+#ifdef FAASBAL_STAMPS
+#define STAMP(a, kernel_off, slot)                                                                      \
+    do {                                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+        if (threadIdx.x == 0) (a).dbg[((kernel_off) + blockIdx.x) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+    } while (0)
+#define STAMPR(a, kernel_off, slot)                                                                     \
+    do {                                                                                                \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+        if (threadIdx.x == 0) (a).dbg[((kernel_off) + blockIdx.x) * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+        __builtin_amdgcn_sched_barrier(0);                                                              \
+    } while (0)
+#else
+#define STAMPR(a, kernel_off, slot) \
+    do {                            \
+    } while (0)
+#define STAMP(a, kernel_off, slot) \
+    do {                           \
+    } while (0)
+#endif
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ int popc_lt(uint64_t m) {
     // number of set bits of m below this lane
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
+}
+
+// ---- DPP wave primitives (gfx9 row_shr / row_bcast): no LDS crossbar traffic,
+// unlike __shfl_* which lowers to ds_bpermute.
+template <int CTRL, int ROWM, int BANKM, bool BC>
+__device__ __forceinline__ uint32_t dpp(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, CTRL, ROWM, BANKM, BC);
+}
+// Inclusive prefix sum over the 64 lanes.
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+    uint32_t x = v + dpp<0x111, 0xf, 0xf, true>(v) + dpp<0x112, 0xf, 0xf, true>(v) + dpp<0x113, 0xf, 0xf, true>(v);
+    x += dpp<0x114, 0xf, 0xe, false>(x);  // row_shr:4, banks 1-3
+    x += dpp<0x118, 0xf, 0xc, false>(x);  // row_shr:8, banks 2-3
+    x += dpp<0x142, 0xa, 0xf, false>(x);  // row_bcast:15 into rows 1, 3
+    x += dpp<0x143, 0xc, 0xf, false>(x);  // row_bcast:31 into rows 2, 3
+    return x;
+}
+// Inclusive prefix max over the 64 lanes (values >= 0).
+__device__ __forceinline__ uint32_t wave_incl_max_u32(uint32_t v) {
+    uint32_t x = max(max(v, dpp<0x111, 0xf, 0xf, true>(v)), max(dpp<0x112, 0xf, 0xf, true>(v), dpp<0x113, 0xf, 0xf, true>(v)));
+    x = max(x, dpp<0x114, 0xf, 0xe, false>(x));
+    x = max(x, dpp<0x118, 0xf, 0xc, false>(x));
+    x = max(x, dpp<0x142, 0xa, 0xf, false>(x));
+    x = max(x, dpp<0x143, 0xc, 0xf, false>(x));
+    return x;
+}
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan_u32(v), 63);
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_u32(v), 63);
+}
+// Block-wide exclusive prefix sum (u32), one value per thread.
+__device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t *lds4, uint32_t &total) {
+    const uint32_t x = wave_incl_scan_u32(v);
+    if (lane_id() == 63) lds4[wave_id()] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < kWaves; ++w) {
+        const uint32_t t = lds4[w];
+        pre += (w < wave_id()) ? t : 0u;
+        tot += t;
+    }
+    __syncthreads();
+    total = tot;
+    return pre + x - v;
+}
+
+// Device self-test of the DPP primitives against a serial LDS reference.
+__global__ __launch_bounds__(kBS) void k_selftest(uint32_t *err, uint32_t seed) {
+    __shared__ uint32_t vals[kBS];
+    __shared__ uint32_t l4[kWaves];
+    uint32_t h = (threadIdx.x + 1) * 2654435761u ^ seed;
+    h ^= h >> 13;
+    h *= 0x5bd1e995u;
+    h ^= h >> 15;
+    const uint32_t v = (seed & 1) ? (h & 0xffu) : (h & 0xffffu);
+    vals[threadIdx.x] = v;
+    __syncthreads();
+    const int wb = wave_id() * 64;
+    uint32_t ref = 0, mref = 0;
+    for (int i = wb; i <= (int)threadIdx.x; ++i) {
+        ref += vals[i];
+        mref = vals[i] > mref ? vals[i] : mref;
+    }
+    uint32_t tot_ref = 0, wsum = 0, wmax = 0, bpre = 0;
+    for (int i = 0; i < kBS; ++i) {
+        tot_ref += vals[i];
+        if (i < (int)threadIdx.x) bpre += vals[i];
+        if (i >= wb && i < wb + 64) {
+            wsum += vals[i];
+            wmax = vals[i] > wmax ? vals[i] : wmax;
+        }
+    }
+    uint32_t bad = 0;
+    bad += wave_incl_scan_u32(v) != ref;
+    bad += wave_incl_max_u32(v) != mref;
+    bad += wave_sum_u32(v) != wsum;
+    bad += wave_max_u32(v) != wmax;
+    uint32_t tot;
+    bad += block_excl_scan_u32(v, l4, tot) != bpre;
+    bad += tot != tot_ref;
+    if (bad) atomicAdd(err, bad);
 }
 
 // Block-wide exclusive scan of one value per thread (BS = 256 = 4 waves).
@@ -203,307 +311,696 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     if (qstat == kQsBack) a.back_list[qidx] = (int32_t)s;
 }
 
-// ------------------------------------------------------------ slot purge
-__global__ __launch_bounds__(kBS) void k_slots(SlotArgs a) {
-    __shared__ uint32_t l4[kWaves];
-    const int s = blockIdx.x * kBS + threadIdx.x;
-    uint32_t ev = 0;
-    if (s < a.W) {
-        const bool t = a.touched[s] == a.tick;
-        const int reg0 = a.reg[s];
-        int reg = reg0;
-        double hb = a.hb[s];
-        int32_t fr = a.free_in[s];
-        int flags = 0;
-        if (t) { reg = a.post_reg[s]; hb = a.post_hb[s]; fr = a.post_free[s]; flags = a.post_flags[s]; }
-        // PushWorker.is_alive (:209-212): time.time() - last_heartbeat > time_to_expire
-        const bool dead = reg && ((a.now - hb) > a.tte);
-        const bool alive = reg && !dead;
-        const bool died_start = reg0 && (dead || (flags & kPfDiedStart));
-        const bool evicted = (reg0 || t) && !alive;
-        a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
-        a.free_out[s] = fr;
-        a.inq_out[s] = 0;
-        ev = evicted ? 1u : 0u;
+
+// ------------------------------------------------------------ slot state
+// Current record of slot s after this tick's messages (touched) or as committed.
+struct Cur {
+    int reg0, reg, flags;
+    bool t;
+    double hb;
+    int32_t fr;
+};
+
+__device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
+    Cur c;
+    c.t = a.E > 0 && a.touched[s] == a.tick;
+    c.reg0 = a.reg[s];
+    if (c.t) {
+        c.reg = a.post_reg[s];
+        c.hb = a.post_hb[s];
+        c.fr = a.post_free[s];
+        c.flags = a.post_flags[s];
+    } else {
+        c.reg = c.reg0;
+        c.hb = a.hb[s];
+        c.fr = a.free_in[s];
+        c.flags = 0;
     }
-    uint32_t tot;
-    block_excl_scan<uint32_t>(ev, l4, tot);
-    if (threadIdx.x == 0) a.wcnt[blockIdx.x] = tot;
+    return c;
 }
 
-// ------------------------------------------------------------ scan
-__device__ __forceinline__ int lq_slot(int64_t pos, const ScanArgs &a) {
+// PushWorker.is_alive (task_dispatcher.py:209-212): time.time() - last_heartbeat > time_to_expire,
+// fp64 subtract then compare, exactly as written.
+__device__ __forceinline__ bool is_dead(const TickArgs &a, const Cur &c) { return c.reg && ((a.now - c.hb) > a.tte); }
+
+__device__ __forceinline__ int lq_slot(const TickArgs &a, int64_t pos) {
     if (pos < a.E) return a.front_list[pos];
     pos -= a.E;
     if (pos < a.Qn) return a.queue_in[pos];
-    pos -= a.Qn;
-    return a.back_list[pos];
+    return a.back_list[pos - a.Qn];
 }
 
-__device__ __forceinline__ int lq_c(int64_t pos, int s, const ScanArgs &a) {
-    if (s < 0) return 0;
-    if (!(a.st[s] & kStAlive)) return 0;
-    if (pos >= a.E && pos < a.E + a.Qn && a.touched[s] == a.tick && ((a.post_flags[s] >> 1) & 3) != kQsKeep)
-        return 0;  // moved to the front, re-appended or removed by this tick's messages
-    const int f = a.free_out[s];
-    return f > 1 ? f : 1;  // a queued worker with free <= 0 still takes one task (:409-419)
+// ------------------------------------------------------------ helpers
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) v += __shfl_xor(v, d, 64);
+    return v;
+}
+template <typename T>
+__device__ __forceinline__ T wave_max(T v) {
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+        const T y = __shfl_xor(v, d, 64);
+        v = v > y ? v : y;
+    }
+    return v;
 }
 
-__device__ __forceinline__ bool is_orphan(int64_t seq, const int32_t *__restrict__ log_slot,
-                                          const uint8_t *__restrict__ st, const uint32_t *__restrict__ epoch) {
-    const int32_t s = log_slot[seq];
-    return s >= 0 && (st[s] & kStDiedStart) && (uint64_t)seq >= (uint64_t)epoch[s];
+// Counts of "c > r" in this wave for rounds r0 .. r0+rn-1 (rn <= 64): lane i
+// receives the count of round r0 + i (one ballot per round, no LDS traffic).
+__device__ __forceinline__ uint32_t wave_round_counts(int c, int r0, int rn) {
+    uint32_t m0 = 0, m1 = 0, m2 = 0, m3 = 0;
+    const int lane = lane_id();
+    int i = 0;
+    for (; i + 3 < rn; i += 4) {
+        const uint32_t n0 = (uint32_t)__popcll(__ballot(c > r0 + i));
+        const uint32_t n1 = (uint32_t)__popcll(__ballot(c > r0 + i + 1));
+        const uint32_t n2 = (uint32_t)__popcll(__ballot(c > r0 + i + 2));
+        const uint32_t n3 = (uint32_t)__popcll(__ballot(c > r0 + i + 3));
+        m0 = (lane == i) ? n0 : m0;
+        m1 = (lane == i + 1) ? n1 : m1;
+        m2 = (lane == i + 2) ? n2 : m2;
+        m3 = (lane == i + 3) ? n3 : m3;
+    }
+    for (; i < rn; ++i) {
+        const uint32_t n = (uint32_t)__popcll(__ballot(c > r0 + i));
+        m0 = (lane == i) ? n : m0;
+    }
+    return m0 | m1 | m2 | m3;  // each lane is set by exactly one chain (others stay 0)
 }
 
-__global__ __launch_bounds__(kBS) void k_scan(ScanArgs a) {
+// Sum of cnt[i] over i < n with all loads in flight at once (n <= kPeel*256 on
+// the fused path; a tail loop covers larger n); also the sum over i < lim.
+__device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int n, int lim,
+                                           unsigned long long &tot, unsigned long long &pre) {
+    uint32_t v[kPeel];
+#pragma unroll
+    for (int k = 0; k < kPeel; ++k) {
+        const int i = threadIdx.x + k * kBS;
+        v[k] = i < n ? cnt[i] : 0u;
+    }
+    tot = pre = 0;
+#pragma unroll
+    for (int k = 0; k < kPeel; ++k) {
+        const int i = threadIdx.x + k * kBS;
+        tot += v[k];
+        pre += i < lim ? v[k] : 0u;
+    }
+    for (int i = threadIdx.x + kPeel * kBS; i < n; i += kBS) {
+        const uint32_t x = cnt[i];
+        tot += x;
+        pre += i < lim ? x : 0u;
+    }
+}
+
+// ------------------------------------------------------------ k_slots
+// Heartbeat purge of every slot (purge_workers, :241-249): liveness, the
+// died-registration bitmap, next free_processes (INT32_MIN = no live record).
+__global__ __launch_bounds__(kBS) void k_slots(TickArgs a) {
+    __shared__ uint32_t l4[kWaves];
+    STAMP(a, 0, 0);
+    const int s = blockIdx.x * kBS + threadIdx.x;
+    bool died_start = false, evicted = false;
+    if (s < a.W) {
+        const Cur c = cur_slot(a, s);
+        const bool dead = is_dead(a, c);
+        const bool alive = c.reg && !dead;
+        died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
+        evicted = (c.reg0 || c.t) && !alive;
+        a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
+        a.free_out[s] = alive ? c.fr : INT32_MIN;
+        a.inq_out[s] = 0;
+    }
+    const uint64_t dm = __ballot(died_start);
+    if (lane_id() == 0 && blockIdx.x * kBS + wave_id() * 64 < a.W) a.dmask[(blockIdx.x * kBS) / 64 + wave_id()] = dm;
+    const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
+    if (lane_id() == 0) l4[wave_id()] = ev;
+    __syncthreads();
+    if (threadIdx.x == 0) a.wcnt[blockIdx.x] = l4[0] + l4[1] + l4[2] + l4[3];
+    STAMP(a, 0, 15);
+}
+
+// ------------------------------------------------------------ k_scan
+// F-blocks flag orphaned log entries (died bitmap in LDS); Q-blocks compute the
+// effective free count c of every LRU position and the block's count of c > r
+// for every round r (table laid out [block][round]).
+__global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long dyn[];
     __shared__ uint32_t l4[kWaves];
     __shared__ int32_t m4[kWaves];
     __shared__ unsigned long long s4[kWaves];
     __shared__ uint32_t wc[kWaves][kBS];
-    if ((int)blockIdx.x < a.nbf) {
-        // ---- log role: count orphans in this tile
-        const int64_t base = a.log_lo + (int64_t)blockIdx.x * kFTile + (int64_t)threadIdx.x * kFItems;
-        uint32_t cnt = 0;
+    const int bid = blockIdx.x;
+    const int SO = a.nbw;
+    STAMP(a, SO, 0);
+    if (bid < a.nbf) {
+        // ---- F-role: orphan flags of log entries [b*2048 + t*8, +8)
+        const int b = bid;
+        const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
+        int32_t v[kFItems];
+        if (base + kFItems <= a.head_in) {
+            const int4 x0 = *reinterpret_cast<const int4 *>(a.log_slot + base);
+            const int4 x1 = *reinterpret_cast<const int4 *>(a.log_slot + base + 4);
+            v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
+            v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) v[j] = (base + j < a.head_in) ? a.log_slot[base + j] : -1;
+        }
+        const int nwords = (a.W + 63) >> 6;
+        const unsigned long long *dm = a.dmask;
+        if (a.lds_bitmap) {
+            // <= 2048 words = 1024 int4: at most 4 loads per thread, all in flight together
+            const int n4 = (nwords + 1) >> 1;
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
+            uint4 t[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = threadIdx.x + k * kBS;
+                t[k] = src[i < n4 ? i : n4 - 1];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int i = threadIdx.x + k * kBS;
+                if (i < n4) reinterpret_cast<uint4 *>(dyn)[i] = t[k];
+            }
+            __syncthreads();
+            dm = dyn;
+        }
+        uint32_t died = 0;
 #pragma unroll
         for (int j = 0; j < kFItems; ++j) {
-            const int64_t q = base + j;
-            if (q < a.head_in && is_orphan(q, a.log_slot, a.st, a.epoch)) ++cnt;
+            const int sj = v[j] < 0 ? 0 : v[j];
+            const unsigned long long wd = dm[sj >> 6];
+            died |= (v[j] >= 0 && ((wd >> (sj & 63)) & 1ull)) ? (1u << j) : 0u;
         }
-        uint32_t tot;
-        block_excl_scan<uint32_t>(cnt, l4, tot);
-        if (threadIdx.x == 0) a.fcnt[blockIdx.x] = tot;
+        uint32_t flags = 0;
+        if (died) {
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j)
+                if (((died >> j) & 1u) && (uint64_t)(base + j) >= (uint64_t)a.epoch[v[j]]) flags |= 1u << j;
+        }
+        a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
+        const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
+        if (lane_id() == 0) l4[wave_id()] = wv;
+        __syncthreads();
+        if (threadIdx.x == 0) a.fcnt[b] = l4[0] + l4[1] + l4[2] + l4[3];
+        STAMP(a, SO, 15);
         return;
     }
-    // ---- queue role
-    const int b = (int)blockIdx.x - a.nbf;
+    // ---- Q-role: LRU positions [b*256, +256) of fronts ++ queue ++ backs
+    const int b = bid - a.nbf;
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
     int c = 0;
     if (pos < a.Qlog) {
-        const int s = lq_slot(pos, a);
-        c = lq_c(pos, s, a);
-        a.c_arr[pos] = c;
+        const int s = lq_slot(a, pos);
+        int32_t raw = s >= 0 ? a.free_out[s] : INT32_MIN;  // INT32_MIN: no live record
+        // an old queue entry moved to the front, re-appended or removed by this tick's messages
+        if (raw != INT32_MIN && a.E > 0 && pos >= a.E && pos < a.E + a.Qn && a.touched[s] == a.tick &&
+            ((a.post_flags[s] >> 1) & 3) != kQsKeep)
+            raw = INT32_MIN;
+        if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
+        a.c_arr[pos] = raw;
     }
-    const int bm = block_reduce_max<int32_t>(c, m4);
-    unsigned long long csum;
-    block_excl_scan<unsigned long long>((unsigned long long)c, s4, csum);
-    if (threadIdx.x == 0) {
-        if (bm > 0) atomicMax(&a.P->maxc, bm);
-        if (csum) atomicAdd(&a.P->cap_total, csum);
-        a.qbmax[b] = bm < a.R ? bm : a.R;
-    }
-    // per-round counts of c > r for r < min(bm, R): waves count their part,
-    // 256 rounds at a time, then one thread per round sums the four waves.
-    const int rmax = bm < a.R ? bm : a.R;
-    for (int r0 = 0; r0 < rmax; r0 += kBS) {
-        const int rn = (rmax - r0) < kBS ? (rmax - r0) : kBS;
-        for (int i = 0; i < rn; ++i) {
-            uint64_t m = __ballot(c > r0 + i);
-            if (lane_id() == 0) wc[wave_id()][i] = (uint32_t)__popcll(m);
-        }
-        __syncthreads();
-        if ((int)threadIdx.x < rn) {
-            uint32_t t = 0;
+    STAMP(a, SO, 1);
+    const uint32_t wmx = wave_max_u32((uint32_t)c);
+    if (lane_id() == 0) m4[wave_id()] = (int32_t)wmx;
+    unsigned long long csum = 0;
+    for (int rc = 0; rc < a.R; rc += kBS) {
+        const int rn = (a.R - rc) < kBS ? (a.R - rc) : kBS;
 #pragma unroll
-            for (int w = 0; w < kWaves; ++w) t += wc[w][threadIdx.x];
-            a.qcnt[(size_t)(r0 + threadIdx.x) * a.nbq + b] = t;
+        for (int g = 0; g < kBS / 64; ++g) {
+            const int r0 = rc + g * 64;
+            uint32_t cnt = 0;
+            if (r0 < rc + rn && r0 < (int)wmx) {
+                int k = rc + rn - r0;
+                k = k < 64 ? k : 64;
+                k = k < (int)wmx - r0 ? k : (int)wmx - r0;
+                cnt = wave_round_counts(c, r0, k);
+            }
+            wc[wave_id()][g * 64 + lane_id()] = cnt;
         }
         __syncthreads();
+        uint32_t t = 0;
+        if ((int)threadIdx.x < rn) {
+            t = wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
+            a.qcnt[(size_t)b * a.R + rc + threadIdx.x] = t;
+        }
+        // sum_r count(c > r) over r < R = sum of min(c, R): the block's capacity when c <= R
+        const uint32_t ts = wave_sum_u32(t);
+        if (lane_id() == 0) l4[wave_id()] = ts;
+        __syncthreads();
+        csum += (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
+        __syncthreads();
     }
+    if (threadIdx.x == 0) {
+        int bm = m4[0];
+        for (int w = 1; w < kWaves; ++w) bm = m4[w] > bm ? m4[w] : bm;
+        a.qbm_raw[b] = bm;
+        a.csum[b] = csum;
+    }
+    STAMP(a, SO, 15);
 }
 
-// ------------------------------------------------------------ plan
-// wg 0: orphan block offsets; wg 1: evicted block offsets; wg 2+r: row r of the
-// round table (exclusive scan across queue blocks) and its total A(r) = |A_r|.
-__global__ __launch_bounds__(kBS) void k_plan(PlanArgs a) {
+// ------------------------------------------------------------ k_plan (large grids only)
+// wg 0: orphan block offsets + O; wg 1: evicted block offsets; wg 2: max c and
+// capacity; wg 3+r: exclusive scan of round r's counts across queue blocks.
+__global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     __shared__ unsigned long long l4[kWaves];
-    if (blockIdx.x == 0 || blockIdx.x == 1) {
-        const uint32_t *cnt = blockIdx.x == 0 ? a.fcnt : a.wcnt;
-        int64_t *pre = blockIdx.x == 0 ? a.fpre : a.wpre;
-        const int n = blockIdx.x == 0 ? a.nbf : a.nbw;
+    __shared__ int32_t m4[kWaves];
+    const int bid = blockIdx.x;
+    if (bid <= 1) {
+        const uint32_t *cnt = bid == 0 ? a.fcnt : a.wcnt;
+        int64_t *pre = bid == 0 ? a.fpre : a.wpre;
+        const int n = bid == 0 ? a.nbf : a.nbw;
         unsigned long long carry = 0;
         for (int base = 0; base < n; base += kBS) {
             const int i = base + threadIdx.x;
             unsigned long long v = i < n ? cnt[i] : 0ull, tot;
-            unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
+            const unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
             if (i < n) pre[i] = (int64_t)(carry + ex);
             carry += tot;
         }
         if (threadIdx.x == 0) {
-            if (blockIdx.x == 0) a.P->O = (int64_t)carry;
+            if (bid == 0) a.P->O = (int64_t)carry;
             else a.P->n_evicted = (int64_t)carry;
         }
         return;
     }
-    const int r = (int)blockIdx.x - 2;
+    if (bid == 2) {
+        int32_t mx = 0;
+        unsigned long long sum = 0;
+        for (int i = threadIdx.x; i < a.nbq; i += kBS) {
+            mx = a.qbm_raw[i] > mx ? a.qbm_raw[i] : mx;
+            sum += a.csum[i];
+        }
+        mx = block_reduce_max<int32_t>(mx, m4);
+        unsigned long long tot;
+        block_excl_scan<unsigned long long>(sum, l4, tot);
+        if (threadIdx.x == 0) {
+            a.P->maxc = mx;
+            a.P->cap_total = (int64_t)tot;
+        }
+        return;
+    }
+    const int r = bid - 3;
     if (r >= a.R) return;
     unsigned long long carry = 0;
     for (int base = 0; base < a.nbq; base += kBS) {
         const int b = base + threadIdx.x;
         unsigned long long v = 0, tot;
-        if (b < a.nbq && r < a.qbmax[b]) v = a.qcnt[(size_t)r * a.nbq + b];
-        unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
-        if (b < a.nbq) a.qpre[(size_t)r * a.nbq + b] = (int64_t)(carry + ex);
+        if (b < a.nbq) v = a.qcnt[(size_t)b * a.R + r];
+        const unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
+        if (b < a.nbq) a.qpre[(size_t)b * a.R + r] = (int64_t)(carry + ex);
         carry += tot;
     }
     if (threadIdx.x == 0) a.A[r] = (int64_t)carry;
 }
 
-// ------------------------------------------------------------ emit
-// Fill level: L = max{ r in [0, maxc] : S(r) <= N_eff }, searched 256 rounds at a time.
-struct Level {
-    int L;
-    int status;
-    int64_t p, AL, N_eff;
+// ------------------------------------------------------------ k_emit
+// Water-filling emission for one queue block once the fill level is known:
+// rounds [0, rfull) in full, round L partially (ranks < p), round L+1 ranks.
+// pre(i) / Srd(i): this block's prefix and S(r) of round r = rc + i.
+struct EmitLds {
+    uint32_t wc[kWaves][kBS];   // per-wave counts of c > r
+    int32_t wbase[kWaves][kBS]; // rank base of a wave in A_r
+    int32_t wpos[kWaves][kBS];  // S(r) + rank base (task index base), r <= L
 };
 
-__device__ Level find_level(const EmitArgs &a, unsigned long long *l4) {
-    Level lv;
-    const int64_t O = a.P->O;
-    const int64_t N = O + a.T;
-    const int64_t cap = (int64_t)a.P->cap_total;
-    const int maxc = a.P->maxc;
-    lv.N_eff = N < cap ? N : cap;
-    lv.status = 0;
-    // S(r+1) = S(r) + A(r); count r in [1, min(maxc, R)] with S(r) <= N_eff
-    const int rlim = maxc < a.R ? maxc : a.R;
-    int64_t carry = 0;  // S(base)
-    int Lc = 0;
-    for (int base = 0; base < rlim; base += kBS) {
-        const int r = base + threadIdx.x;  // computes S(r+1)
-        unsigned long long v = r < rlim ? (unsigned long long)a.A[r] : 0ull, tot;
-        unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
-        const int64_t S1 = carry + (int64_t)(ex + v);
-        const bool ok = r < rlim && S1 <= lv.N_eff;
-        uint64_t m = __ballot(ok);
-        if (lane_id() == 0) l4[wave_id()] = (unsigned long long)__popcll(m);
-        __syncthreads();
-        int k = 0;
-        for (int w = 0; w < kWaves; ++w) k += (int)l4[w];
-        __syncthreads();
-        Lc += k;
-        carry += (int64_t)tot;
-        if (k < kBS) break;  // S is non-decreasing: the first failure ends the search
-    }
-    lv.L = Lc;
-    if (a.head_in + lv.N_eff > a.log_cap) {  // never write past the in-flight log
-        lv.status = 2;
-        lv.p = lv.AL = 0;
-        return lv;
-    }
-    // exact rows exist for r < R; rounds 0..L+1 (bounded by maxc-1) must be covered
-    if (maxc > a.R && lv.L >= a.R - 1) lv.status = 1;
-    // S(L) and A(L)
-    int64_t SL = 0;
-    for (int base = 0; base < lv.L && !lv.status; base += kBS) {
-        const int r = base + threadIdx.x;
-        unsigned long long v = r < lv.L ? (unsigned long long)a.A[r] : 0ull, tot;
-        block_excl_scan<unsigned long long>(v, l4, tot);
-        SL += (int64_t)tot;
-    }
-    lv.p = lv.N_eff - SL;
-    lv.AL = (!lv.status && lv.L < a.R && lv.L < maxc) ? a.A[lv.L] : 0;
-    return lv;
-}
-
-__global__ __launch_bounds__(kBS) void k_emit(EmitArgs a) {
-    __shared__ unsigned long long l4[kWaves];
-    __shared__ uint32_t l4u[kWaves];
-    __shared__ uint32_t rc[2][kWaves];
-    const int nq = a.nbq;
-    if ((int)blockIdx.x < nq) {
-        const int b = blockIdx.x;
-        const Level lv = find_level(a, l4);
-        if (b == 0 && threadIdx.x == 0) {
-            a.P->L = lv.L;
-            a.P->status = lv.status;
-            a.P->N_eff = lv.status ? 0 : lv.N_eff;
-            a.P->p = lv.p;
-            a.P->AL = lv.AL;
-        }
-        if (lv.status) return;
+__global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
+    __shared__ EmitLds E_;
+    __shared__ uint32_t part[kWaves * 32][9];    // fused prologue: per-wave class partials
+    __shared__ uint32_t red[kWaves][4];
+    __shared__ unsigned long long red64[kWaves];
+    __shared__ int64_t S_l[kBS + 1];             // S(r) of the current round chunk
+    __shared__ int64_t pre_c[kBS];               // this block's prefix of round r (chunk)
+    __shared__ uint32_t tot_f[kRFused];          // fused: A(r)
+    __shared__ int32_t misc[8];
+    const int bid = blockIdx.x;
+    const int SO = a.nbw + a.nbf + a.nbq;
+    STAMP(a, SO, 0);
+    const int lane = lane_id(), w = wave_id();
+    if (bid < a.nbq) {
+        const int b = bid;
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
-        int c = 0, s = -1;
-        if (pos < a.Qlog) {
-            c = a.c_arr[pos];
-            if (c > 0) {
-                const int64_t q = pos;
-                if (q < a.E) s = a.front_list[q];
-                else if (q < a.E + a.Qn) s = a.queue_in[q - a.E];
-                else s = a.back_list[q - a.E - a.Qn];
+        int32_t raw = INT32_MIN;
+        int s = -1;
+        int64_t O, nev = 0, cap;
+        int maxc, bm;
+        int rlim;
+        int L = 0;
+        int64_t S_L = 0, N_eff;
+        if (a.fused) {
+            // ---- every prologue load in flight at once (clamped indices, no branches)
+            const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
+            const int32_t raw0 = a.c_arr[pq];
+            int s0;
+            if (a.E == 0) s0 = a.queue_in[pq];
+            else s0 = lq_slot(a, pq);
+            const int R = a.R;       // 32, 64 or 128
+            const int cls = R >> 2;  // int4 columns per table row
+            const int lcls = 31 - __builtin_clz(cls);
+            const int nq4 = (a.nbq * R) >> 2;
+            const uint4 *tab = reinterpret_cast<const uint4 *>(a.qcnt);
+            uint4 tv[kTabLd];
+#pragma unroll
+            for (int k = 0; k < kTabLd; ++k) {
+                const int q = threadIdx.x + k * kBS;
+                tv[k] = tab[q < nq4 ? q : nq4 - 1];
             }
-        }
-        const int L = lv.L;
-        const int bm = a.qbmax[b];  // rows r < bm carry counts (bm <= R)
-        const int rend = (L + 1) < (bm - 1) ? (L + 1) : (bm - 1);
-        int64_t S = 0;  // S(r)
-        int64_t rankL = -1, rankL1 = -1;
-        const int64_t head = a.head_in;
-        for (int r = 0; r <= rend; ++r) {
-            const bool act = c > r;
-            const uint64_t m = __ballot(act);
-            if (lane_id() == 0) rc[r & 1][wave_id()] = (uint32_t)__popcll(m);
-            __syncthreads();
-            uint32_t wpre = 0;
-            for (int w = 0; w < wave_id(); ++w) wpre += rc[r & 1][w];
-            if (act) {
-                const int64_t rank = a.qpre[(size_t)r * nq + b] + wpre + popc_lt(m);
-                if (r < L) {
-                    a.log_slot[head + S + rank] = s;
-                } else if (r == L) {
-                    rankL = rank;
-                    if (rank < lv.p) a.log_slot[head + S + rank] = s;
-                } else {
-                    rankL1 = rank;
+            uint32_t fv[kPeel], wv[kPeel], mv[kPeel], cv[kPeel];
+            const int nbf1 = a.nbf > 0 ? a.nbf - 1 : 0, nbw1 = a.nbw - 1, nbq1 = a.nbq - 1;
+#pragma unroll
+            for (int k = 0; k < kPeel; ++k) {
+                const int i = threadIdx.x + k * kBS;
+                fv[k] = a.fcnt[i < nbf1 ? i : nbf1];
+                wv[k] = a.wcnt[i < nbw1 ? i : nbw1];
+                mv[k] = (uint32_t)a.qbm_raw[i < nbq1 ? i : nbq1];
+                cv[k] = (uint32_t)a.csum[i < nbq1 ? i : nbq1];
+            }
+            // ---- per-thread partials
+            if (threadIdx.x == 0 && (fv[0] + wv[0] + mv[0] + cv[0] + tv[0].x + tv[kTabLd - 1].w + (uint32_t)raw0 + (uint32_t)s0) == 0x7fffffffu)
+                a.c_arr[0] = 0;  // (never true in practice) keeps the stamp below behind the loads
+            STAMP(a, SO, 9);
+            uint32_t fo = 0, wo = 0, mo = 0, co = 0;
+#pragma unroll
+            for (int k = 0; k < kPeel; ++k) {
+                const int i = threadIdx.x + k * kBS;
+                fo += i < a.nbf ? fv[k] : 0u;
+                wo += i < a.nbw ? wv[k] : 0u;
+                mo = (i < a.nbq && mv[k] > mo) ? mv[k] : mo;
+                co += i < a.nbq ? cv[k] : 0u;
+                if (i == b) misc[4] = (int32_t)mv[k];  // this block's max c
+            }
+            for (int i = threadIdx.x + kPeel * kBS; i < a.nbf; i += kBS) fo += a.fcnt[i];
+            for (int i = threadIdx.x + kPeel * kBS; i < a.nbw; i += kBS) wo += a.wcnt[i];
+            for (int i = threadIdx.x + kPeel * kBS; i < a.nbq; i += kBS) {
+                mo = (uint32_t)a.qbm_raw[i] > mo ? (uint32_t)a.qbm_raw[i] : mo;
+                co += (uint32_t)a.csum[i];
+                if (i == b) misc[4] = a.qbm_raw[i];
+            }
+            // table: thread t covers rows r0..r0+3, r0 = 4 (t mod cls), of blocks q / cls
+            uint32_t pp[4] = {0, 0, 0, 0}, tt[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int k = 0; k < kTabLd; ++k) {
+                const int q = threadIdx.x + k * kBS;
+                const bool in = q < nq4;
+                const bool before = in && (q >> lcls) < b;
+                tt[0] += in ? tv[k].x : 0u; tt[1] += in ? tv[k].y : 0u;
+                tt[2] += in ? tv[k].z : 0u; tt[3] += in ? tv[k].w : 0u;
+                pp[0] += before ? tv[k].x : 0u; pp[1] += before ? tv[k].y : 0u;
+                pp[2] += before ? tv[k].z : 0u; pp[3] += before ? tv[k].w : 0u;
+            }
+            for (int q = threadIdx.x + kTabLd * kBS; q < nq4; q += kBS) {
+                const uint4 v = tab[q];
+                const bool before = (q >> lcls) < b;
+                tt[0] += v.x; tt[1] += v.y; tt[2] += v.z; tt[3] += v.w;
+                pp[0] += before ? v.x : 0u; pp[1] += before ? v.y : 0u;
+                pp[2] += before ? v.z : 0u; pp[3] += before ? v.w : 0u;
+            }
+            // lanes of one class (lane mod cls) hold partials of the same 4 rows
+            for (int d = cls; d < 64; d <<= 1) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    pp[u] += __shfl_xor(pp[u], d, 64);
+                    tt[u] += __shfl_xor(tt[u], d, 64);
                 }
             }
-            S += a.A[r];
+            if (lane < cls) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    part[w * 32 + lane][u] = pp[u];
+                    part[w * 32 + lane][4 + u] = tt[u];
+                }
+            }
+            fo = wave_sum_u32(fo);
+            wo = wave_sum_u32(wo);
+            co = wave_sum_u32(co);
+            mo = wave_max_u32(mo);
+            if (lane == 0) {
+                red[w][0] = fo;
+                red[w][1] = wo;
+                red[w][2] = co;
+                red[w][3] = mo;
+            }
+            raw = pos < a.Qlog ? raw0 : INT32_MIN;
+            s = s0;
+            STAMP(a, SO, 10);
+            __syncthreads();
+            STAMP(a, SO, 11);
+            O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+            nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
+            cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
+            maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
+            bm = misc[4];
+            // round-table rows: this block's prefix and the total, summed over the threads of row r's class
+            if ((int)threadIdx.x < R) {
+                const int r = threadIdx.x, c0 = r >> 2, u = r & 3;
+                const uint32_t p = part[c0][u] + part[32 + c0][u] + part[64 + c0][u] + part[96 + c0][u];
+                const uint32_t t = part[c0][4 + u] + part[32 + c0][4 + u] + part[64 + c0][4 + u] + part[96 + c0][4 + u];
+                pre_c[r] = (int64_t)p;
+                tot_f[r] = t;
+            }
+            __syncthreads();
+            STAMP(a, SO, 1);
+            rlim = maxc < R ? maxc : R;
+            if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
+            const int64_t N = O + a.T;
+            N_eff = N < cap ? N : cap;
+            // ---- fill level: one chunk (rlim <= 128); S(r+1) by a block scan of A(r)
+            {
+                const int r = threadIdx.x;
+                const uint32_t v = r < rlim ? tot_f[r] : 0u;
+                uint32_t tot;
+                const uint32_t ex = block_excl_scan_u32(v, (uint32_t *)red, tot);
+                const int64_t S1 = (int64_t)(ex + v);
+                const bool ok = r < rlim && S1 <= N_eff;
+                const int kw = __popcll(__ballot(ok));
+                if (lane == 0) misc[w] = kw;
+                S_l[r + 1] = S1;
+                if (r == 0) S_l[0] = 0;
+                __syncthreads();
+                L = misc[0] + misc[1] + misc[2] + misc[3];
+                S_L = S_l[L];
+            }
+        } else {
+            // ---- large grids: totals and scanned table from k_plan
+            if (pos < a.Qlog) {
+                raw = a.c_arr[pos];
+                s = lq_slot(a, pos);
+            }
+            bm = a.qbm_raw[b];
+            O = a.P->O;
+            nev = a.P->n_evicted;
+            cap = a.P->cap_total;
+            maxc = a.P->maxc;
+            rlim = maxc < a.R ? maxc : a.R;
+            if (maxc > a.R) cap = INT64_MAX;
+            const int64_t N = O + a.T;
+            N_eff = N < cap ? N : cap;
+            int64_t carry = 0;  // S(rc)
+            for (int rc = 0; rc < rlim; rc += kBS) {
+                const int r = rc + threadIdx.x;
+                const unsigned long long v = r < rlim ? (unsigned long long)a.A[r] : 0ull;
+                unsigned long long tot;
+                const unsigned long long ex = block_excl_scan<unsigned long long>(v, red64, tot);
+                const int64_t S1 = carry + (int64_t)(ex + v);  // S(r + 1)
+                const bool ok = r < rlim && S1 <= N_eff;
+                const int k_w = __popcll(__ballot(ok));
+                if (lane == 0) misc[w] = k_w;
+                S_l[threadIdx.x + 1] = S1;
+                if (threadIdx.x == 0) S_l[0] = carry;
+                __syncthreads();
+                const int k = misc[0] + misc[1] + misc[2] + misc[3];
+                L += k;
+                S_L = S_l[k];
+                __syncthreads();
+                if (k < kBS) break;
+                carry += (int64_t)tot;
+            }
         }
-        uint32_t member = 0;
+        int status = 0;
+        if (maxc > a.R && L >= a.R - 1) status = 1;   // rows beyond the table needed: rerun wider
+        if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log
+        const int64_t p = N_eff - S_L;
+        auto getA = [&](int r) -> int64_t { return r < rlim ? (a.fused ? (int64_t)tot_f[r] : a.A[r]) : (int64_t)0; };
+        const int64_t AL = (L < maxc && L < rlim) ? getA(L) : 0;
+        STAMP(a, SO, 2);
+        if (b == 0 && threadIdx.x == 0) {
+            a.hout->O = O;
+            a.hout->n_evicted = nev;
+            a.hout->cap_total = cap;
+            a.hout->maxc = maxc;
+            a.hout->L = L;
+            a.hout->status = status;
+            a.hout->N_eff = status ? 0 : N_eff;
+            a.hout->p = p;
+            a.hout->AL = AL;
+            if (AL == 0) a.hout->new_qlen = 0;
+        }
+        if (status) return;
+        // ---- water-filling emission, 256 rounds per chunk, rounds 0 .. L+1
+        const int c = raw != INT32_MIN ? (raw > 1 ? raw : 1) : 0;
+        int32_t *const out = a.log_slot + a.head_in;
+        int64_t rankL = -1, exL1 = 0;
+        int64_t carryS = 0;  // S(rc)
+        const int wmx = (int)wave_max_u32((uint32_t)c);
+        for (int rc = 0; rc <= L + 1; rc += kBS) {
+            const int rn = (L + 2 - rc) < kBS ? (L + 2 - rc) : kBS;
+            if (!a.fused) {
+                // chunk tables from k_plan: pre(r), S(r)
+                const int r = rc + threadIdx.x;
+                int64_t pr = 0, Av = 0;
+                if ((int)threadIdx.x < rn && r < rlim) {
+                    pr = a.qpre[(size_t)b * a.R + r];
+                    Av = a.A[r];
+                }
+                unsigned long long tot;
+                const unsigned long long ex = block_excl_scan<unsigned long long>((unsigned long long)Av, red64, tot);
+                pre_c[threadIdx.x] = pr;
+                S_l[threadIdx.x] = carryS + (int64_t)ex;
+                carryS += (int64_t)tot;
+            }
+            // fused: one chunk, pre_c[r] / S_l[r] from the prologue (rows >= rlim read as 0 / S(rlim))
+            STAMP(a, SO, 5);
+            // per-wave counts of c > r for the chunk's rounds
+#pragma unroll
+            for (int g = 0; g < kBS / 64; ++g) {
+                const int r0 = rc + g * 64;
+                uint32_t cnt = 0;
+                if (r0 < rc + rn && r0 < wmx) {
+                    int k = rc + rn - r0;
+                    k = k < 64 ? k : 64;
+                    k = k < wmx - r0 ? k : wmx - r0;
+                    cnt = wave_round_counts(c, r0, k);
+                }
+                E_.wc[w][g * 64 + lane] = cnt;
+            }
+            __syncthreads();
+            STAMP(a, SO, 6);
+            // rank base of every (wave, round) and its task index base
+            for (int e = threadIdx.x; e < kWaves * rn; e += kBS) {
+                const int ww = e / rn, i = e - ww * rn;
+                const int r = rc + i;
+                int64_t rb, Sr;
+                if (a.fused) {
+                    rb = r < rlim ? pre_c[r] : 0;
+                    Sr = S_l[r < rlim ? r : rlim];
+                } else {
+                    rb = pre_c[i];
+                    Sr = S_l[i];
+                }
+                for (int q = 0; q < ww; ++q) rb += E_.wc[q][i];
+                E_.wbase[ww][i] = (int32_t)rb;
+                E_.wpos[ww][i] = (r <= L) ? (int32_t)(Sr + rb) : 0;
+            }
+            __syncthreads();
+            STAMP(a, SO, 7);
+            // full rounds: every active lane takes one task; the wave's task index
+            // bases for 64 rounds sit in one register (lane i: round rc + i0 + i)
+            int rfull = L < bm ? L : bm;
+            rfull = rfull < rc + rn ? rfull : rc + rn;
+            for (int i0 = 0; rc + i0 < rfull; i0 += 64) {
+                const int bases = E_.wpos[w][(i0 + lane) < kBS ? (i0 + lane) : kBS - 1];
+                const int nr = (rfull - rc - i0) < 64 ? (rfull - rc - i0) : 64;
+                int i = 0;
+                for (; i + 3 < nr; i += 4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const bool act = c > rc + i0 + i + u;
+                        const uint64_t m = __ballot(act);
+                        const int base = __builtin_amdgcn_readlane(bases, i + u);
+                        if (act) out[base + popc_lt(m)] = s;
+                    }
+                }
+                for (; i < nr; ++i) {
+                    const bool act = c > rc + i0 + i;
+                    const uint64_t m = __ballot(act);
+                    const int base = __builtin_amdgcn_readlane(bases, i);
+                    if (act) out[base + popc_lt(m)] = s;
+                }
+            }
+            STAMP(a, SO, 8);
+            // round L (partial: ranks < p) and round L+1 (ranks for the next queue)
+            if (L >= rc && L < rc + rn) {
+                const int iL = L - rc;
+                const bool act = c > L;
+                const uint64_t m = __ballot(act);
+                rankL = (int64_t)E_.wbase[w][iL] + popc_lt(m);
+                if (act && rankL < p) out[E_.wpos[w][iL] + popc_lt(m)] = s;
+            }
+            if (L + 1 >= rc && L + 1 < rc + rn) {
+                const int i1 = L + 1 - rc;
+                exL1 = (int64_t)E_.wbase[w][i1] + popc_lt(__ballot(c > L + 1));
+            }
+            __syncthreads();
+        }
+        STAMP(a, SO, 4);
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
-            if (c > L && rankL < lv.p) n_q += 1;
-            if (n_q) a.free_out[s] = a.free_out[s] - (int32_t)n_q;
+            if (c > L && rankL < p) n_q += 1;
+            a.free_out[s] = raw - (int32_t)n_q;
             int64_t np = -1;
             if (c > L) {
-                if (rankL >= lv.p) np = rankL - lv.p;
-                else if (c > L + 1) np = (lv.AL - lv.p) + rankL1;
+                if (rankL >= p) np = rankL - p;
+                else if (c > L + 1) np = (AL - p) + exL1;
+                // the one position of rank p in A_L knows the next queue's length
+                if (rankL == p) a.hout->new_qlen = (AL - p) + exL1;
             }
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.inq_out[s] = 1;
-                member = 1;
             }
         }
-        uint32_t tot;
-        block_excl_scan<uint32_t>(member, l4u, tot);
-        if (threadIdx.x == 0 && tot) atomicAdd(&a.P->new_qlen, (unsigned long long)tot);
+        STAMPR(a, SO, 14);
+        STAMP(a, SO, 15);
         return;
     }
-    if ((int)blockIdx.x < nq + a.nbf) {
+    if (bid < a.nbq + a.nbf) {
         // ---- orphan compaction, ascending sequence
-        const int b = blockIdx.x - nq;
-        const int64_t base = a.log_lo + (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
-        uint32_t flags = 0, cnt = 0;
-#pragma unroll
-        for (int j = 0; j < kFItems; ++j) {
-            const int64_t q = base + j;
-            if (q < a.head_in && is_orphan(q, a.log_slot_ro, a.st, a.epoch)) { flags |= 1u << j; ++cnt; }
+        const int b = bid - a.nbq;
+        const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
+        int64_t off;
+        if (a.fused) {
+            unsigned long long tot, pre;
+            peeled_sum(a.fcnt, b, b, tot, pre);
+            const uint32_t ws = wave_sum_u32((uint32_t)pre);
+            if (lane == 0) red[w][0] = ws;
+            __syncthreads();
+            off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        } else {
+            off = a.fpre[b];
         }
         uint32_t tot;
-        uint32_t ex = block_excl_scan<uint32_t>(cnt, l4u, tot);
-        int64_t o = a.fpre[b] + ex;
+        const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tot);
+        int64_t o = off + ex;
+        const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
 #pragma unroll
         for (int j = 0; j < kFItems; ++j)
             if (flags & (1u << j)) a.orphans[o++] = base + j;
+        STAMP(a, SO, 15);
         return;
     }
     // ---- evicted compaction, ascending slot
-    const int b = blockIdx.x - nq - a.nbf;
+    const int b = bid - a.nbq - a.nbf;
     const int s = b * kBS + threadIdx.x;
     const uint32_t e = (s < a.W && (a.st[s] & kStEvicted)) ? 1u : 0u;
+    int64_t off;
+    if (a.fused) {
+        unsigned long long tot, pre;
+        peeled_sum(a.wcnt, b, b, tot, pre);
+        const uint32_t ws = wave_sum_u32((uint32_t)pre);
+        if (lane == 0) red[w][0] = ws;
+        __syncthreads();
+        off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    } else {
+        off = a.wpre[b];
+    }
     uint32_t tot;
-    const uint32_t ex = block_excl_scan<uint32_t>(e, l4u, tot);
-    if (e) a.evicted[a.wpre[b] + ex] = s;
+    const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tot);
+    if (e) a.evicted[off + ex] = s;
+    STAMP(a, SO, 15);
 }
 
 // ------------------------------------------------------------ commit
@@ -539,17 +1036,21 @@ void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout,
 void launch_ev_apply(const EvArgs &a, Stream st) {
     hipLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st, a);
 }
-void launch_slots(const SlotArgs &a, int grid, Stream st) {
-    hipLaunchKernelGGL(k_slots, dim3(grid), dim3(kBS), 0, st, a);
+void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
+    hipLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st, err, seed);
 }
-void launch_scan(const ScanArgs &a, int grid, Stream st) {
-    hipLaunchKernelGGL(k_scan, dim3(grid), dim3(kBS), 0, st, a);
+void launch_slots(const TickArgs &a, Stream st) {
+    hipLaunchKernelGGL(k_slots, dim3(a.nbw), dim3(kBS), 0, st, a);
 }
-void launch_plan(const PlanArgs &a, int grid, Stream st) {
-    hipLaunchKernelGGL(k_plan, dim3(grid), dim3(kBS), 0, st, a);
+void launch_scan(const TickArgs &a, Stream st) {
+    const size_t lds = a.lds_bitmap ? (size_t)((a.W + 63) / 64) * 8 : 0;
+    hipLaunchKernelGGL(k_scan, dim3(a.nbf + a.nbq), dim3(kBS), lds, st, a);
 }
-void launch_emit(const EmitArgs &a, int grid, Stream st) {
-    hipLaunchKernelGGL(k_emit, dim3(grid), dim3(kBS), 0, st, a);
+void launch_plan(const TickArgs &a, Stream st) {
+    hipLaunchKernelGGL(k_plan, dim3(3 + a.R), dim3(kBS), 0, st, a);
+}
+void launch_emit(const TickArgs &a, Stream st) {
+    hipLaunchKernelGGL(k_emit, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st, a);
 }
 void launch_commit(const CommitArgs &a, int grid, Stream st) {
     hipLaunchKernelGGL(k_commit, dim3(grid), dim3(kBS), 0, st, a);

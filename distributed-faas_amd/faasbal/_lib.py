@@ -19,7 +19,7 @@ ERRNAMES = {FB_EINVAL: "FB_EINVAL", FB_ENOMEM: "FB_ENOMEM", FB_EHIP: "FB_EHIP", 
 EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read_state", "fb_tick_launch",
            "fb_tick_wait", "fb_tick_commit", "fb_get_assignments", "fb_get_orphans", "fb_get_evicted",
            "fb_get_event_status", "fb_tick", "fb_device_view_get", "fb_timing_enable", "fb_timing_read",
-           "fb_sync")
+           "fb_selftest", "fb_debug_read", "fb_sync")
 
 
 class TickResult(C.Structure):
@@ -51,7 +51,7 @@ _P = C.c_void_p
 def load(path=LIB_PATH):
     """Load and prototype libfaasbal.so.  Raises if it has not been built."""
     global _LIB
-    if _LIB is not None:
+    if _LIB is not None and path == LIB_PATH:
         return _LIB
     if not os.path.exists(path):
         raise ImportError("libfaasbal.so not found at %s: run `python -c 'import __graft_entry__ as g; "
@@ -77,11 +77,14 @@ def load(path=LIB_PATH):
         "fb_timing_enable": (C.c_int, [_P, C.c_int]),
         "fb_timing_read": (C.c_int, [_P, i32, C.POINTER(C.c_char_p), C.POINTER(dbl), C.POINTER(i64),
                                      C.POINTER(i32)]),
+        "fb_debug_read": (C.c_int, [_P, _P, i64, C.POINTER(i64)]),
+        "fb_selftest": (C.c_int, [_P, C.POINTER(i32)]),
         "fb_sync": (C.c_int, [_P]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _LIB = lib
+    if path == LIB_PATH:
+        _LIB = lib
     return lib

@@ -29,8 +29,8 @@ def _arr(a, dt):
 class GpuBalancer:
     """Device-resident worker table + LRU queue + in-flight log on one GPU."""
 
-    def __init__(self, max_workers, max_log, max_events=65536, device=0):
-        self.lib = _lib.load()
+    def __init__(self, max_workers, max_log, max_events=65536, device=0, lib_path=None):
+        self.lib = _lib.load() if lib_path is None else _lib.load(lib_path)
         self.h = C.c_void_p()
         rc = self.lib.fb_create(C.byref(self.h), int(max_workers), int(max_log), int(max_events), int(device))
         if rc != 0:
@@ -171,6 +171,18 @@ class GpuBalancer:
         n = C.c_int32()
         self._chk(self.lib.fb_timing_read(self.h, max_kernels, names, ms, cnt, C.byref(n)))
         return {names[i].decode(): (ms[i], cnt[i]) for i in range(n.value)}
+
+    def selftest(self):
+        e = C.c_int32()
+        self._chk(self.lib.fb_selftest(self.h, C.byref(e)))
+        return e.value
+
+    def debug_read(self):
+        n = C.c_int64()
+        self._chk(self.lib.fb_debug_read(self.h, None, 0, C.byref(n)))
+        out = np.zeros(max(n.value, 1), np.uint64)
+        self._chk(self.lib.fb_debug_read(self.h, _p(out), n.value, C.byref(n)))
+        return out[: n.value]
 
     def device_view(self):
         v = _lib.DeviceView()

@@ -13,21 +13,24 @@ OUT = os.path.join(HERE, "libfaasbal.so")
 ARCH = os.environ.get("FAASBAL_ARCH", "gfx950")
 
 
-def build_lib(verbose=False):
+def build_lib(verbose=False, out=None, defines=()):
+    """Compile libfaasbal.so (or a diagnostic variant with extra -D defines)."""
+    OUT_ = out or OUT
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     hdrs = [os.path.join(CSRC, "faasbal_kernels.h"), os.path.join(REPO, "include", "faasbal.h")]
-    if os.path.exists(OUT):
-        t = os.path.getmtime(OUT)
+    if os.path.exists(OUT_):
+        t = os.path.getmtime(OUT_)
         if all(os.path.getmtime(p) < t for p in srcs + hdrs):
             return OUT
     cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-Wno-unused-value",
-           "-I" + os.path.join(REPO, "include"), "-I" + CSRC, *srcs, "-o", OUT + ".tmp"]
+           *["-D" + d for d in defines],
+           "-I" + os.path.join(REPO, "include"), "-I" + CSRC, *srcs, "-o", OUT_ + ".tmp"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    os.replace(OUT_ + ".tmp", OUT_)
+    return OUT_
 
 
 if __name__ == "__main__":

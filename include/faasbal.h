@@ -127,6 +127,13 @@ int fb_timing_enable(fb_ctx *ctx, int enable);
 int fb_timing_read(fb_ctx *ctx, int32_t max_kernels, const char **names, double *total_ms,
                    int64_t *launches, int32_t *n_kernels);
 
+/* Device self-test of the kernels' wave/block scan primitives; *errors = 0 on success. */
+int fb_selftest(fb_ctx *ctx, int32_t *errors);
+
+/* Diagnostic: copy up to n words of the in-kernel stamp buffer (written only by
+ * builds compiled with -DFAASBAL_STAMPS); *n_total = buffer length in words. */
+int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_total);
+
 /* Synchronise the context stream (for wall-clock benchmarking). */
 int fb_sync(fb_ctx *ctx);
 

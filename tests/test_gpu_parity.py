@@ -223,3 +223,28 @@ def test_invalid_events_rejected():
         g.tick(1000.0, 10.0, [0], [10], [1], [999.0], [-1], 0)   # slot out of range
     with pytest.raises(FaasbalError):
         g.tick(1000.0, 10.0, [0, 0], [1, 2], [1, 1], [999.0, 998.0], [-1, -1], 0)  # ts decreasing
+
+
+@pytest.fixture
+def force_plan(monkeypatch):
+    """Route ticks through the 3-launch path (k_plan), used for large grids."""
+    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "1")
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_random_multitick_plan_path(force_plan, seed):
+    test_random_multitick_vs_oracle(seed)
+
+
+def test_config3_plan_path(force_plan):
+    test_config3_full_size()
+
+
+def test_golden_plan_path(force_plan):
+    for path in GOLDEN[:12] + GOLDEN[-3:]:
+        test_golden_replay(path)
+
+
+def test_device_primitives_selftest():
+    g = GpuBalancer(16, 16)
+    assert g.selftest() == 0
