@@ -95,6 +95,17 @@ struct fb_ctx {
     std::vector<TimedLaunch> tl;
     std::vector<hipEvent_t> ev_pool;
     std::string err;
+    // sharding (fb_create_sharded): this rank owns global slots [slot_base, slot_base + W)
+    int shard = 0, rank = 0, world = 1;
+    int32_t slot_base = 0, W_global = 0, Wq_cap = 0;  // Wq_cap: LRU queue capacity (global slots)
+    int64_t head_local = 0, l_head_local = 0;
+    uint32_t *lseq = nullptr;                         // global sequence of each local log entry
+    uint32_t *ocnt = nullptr;
+    int64_t *opre = nullptr, *oA = nullptr;
+    uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
+    int64_t xcap = 0;
+    int phase = 0;                                    // 1: phase 1 enqueued; 2: phase 2 enqueued
+    hipStream_t own_s = nullptr;                      // the context's own stream (fb_set_stream may borrow another)
 };
 
 namespace {
@@ -214,6 +225,23 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
     return FB_OK;
 }
 
+// Exchange buffer of a sharded tick, summed by one uint8 all-reduce: every byte
+// has at most one nonzero contributor (the owner of the slot, event or position),
+// so the SUM is exact.  [0, c8) is zeroed before phase 1; c8 is written in full.
+struct XLayout {
+    size_t rec, front, back, evs, c8, total;
+};
+XLayout xlayout(int world, int64_t E, int64_t Qlog) {
+    XLayout x;
+    x.rec = 0;
+    x.front = (size_t)32 * world;
+    x.back = x.front + 4 * (size_t)E;
+    x.evs = x.back + 4 * (size_t)E;
+    x.c8 = x.evs + (size_t)E;
+    x.total = (x.c8 + (size_t)Qlog + 15) & ~(size_t)15;
+    return x;
+}
+
 int choose_R(int32_t maxc) {
     int R = 32;
     while (R < maxc) R <<= 1;
@@ -233,12 +261,26 @@ int enqueue_tick(fb_ctx *c) {
     int rc;
     if ((rc = ensure_table(c, R, nbq))) return rc;
     const int cur = c->cur, nxt = 1 - cur;
-    if (E > 0) {
-        HIPCHK(c, hipMemsetAsync(c->front_list, 0xFF, sizeof(int32_t) * E, c->stream));
-        HIPCHK(c, hipMemsetAsync(c->back_list, 0xFF, sizeof(int32_t) * E, c->stream));
+    const XLayout xl = xlayout(c->world, E, Qlog);
+    int32_t *front = c->front_list, *back = c->back_list;
+    uint8_t *evs = c->ev_status;
+    if (c->shard) {
+        if (!c->xbuf || c->xcap < (int64_t)xl.total)
+            return fail(c, FB_ESTATE, "sharded tick needs an exchange buffer of %zu bytes (bound: %lld)", xl.total,
+                        (long long)c->xcap);
+        front = (int32_t *)(c->xbuf + xl.front);
+        back = (int32_t *)(c->xbuf + xl.back);
+        evs = c->xbuf + xl.evs;
+        if (c->phase != 2) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
+    }
+    if (E > 0 && !(c->shard && c->phase == 2)) {
+        if (!c->shard) {
+            HIPCHK(c, hipMemsetAsync(front, 0, sizeof(int32_t) * E, c->stream));
+            HIPCHK(c, hipMemsetAsync(back, 0, sizeof(int32_t) * E, c->stream));
+        }
         // stable radix sort of events by slot
         int bits = 1;
-        while ((1ll << bits) < (int64_t)W) ++bits;
+        while ((1ll << bits) < (int64_t)(c->shard ? c->W_global : W)) ++bits;
         const int passes = (bits + 7) / 8;
         const int nb = (int)cdiv(E, kRsTile);
         const uint32_t *kin = (const uint32_t *)c->ev_slot, *vin = nullptr;
@@ -253,6 +295,11 @@ int enqueue_tick(fb_ctx *c) {
         }
         EvArgs a{};
         a.E = E;
+        a.shard = c->shard;
+        a.slot_base = c->slot_base;
+        a.W = W;
+        a.head_local = c->l_head_local;
+        a.lseq = c->lseq;
         a.tick = c->tick;
         a.tte = c->l_tte;
         a.head_in = head;
@@ -262,7 +309,7 @@ int enqueue_tick(fb_ctx *c) {
         a.ev_val = c->ev_val;
         a.ev_ts = c->ev_ts;
         a.ev_seq = c->ev_seq;
-        a.ev_status = c->ev_status;
+        a.ev_status = evs;
         a.reg = c->reg;
         a.free_in = c->free_[cur];
         a.hb = c->hb;
@@ -275,8 +322,8 @@ int enqueue_tick(fb_ctx *c) {
         a.post_epoch = c->post_epoch;
         a.post_flags = c->post_flags;
         a.touched = c->touched;
-        a.front_list = c->front_list;
-        a.back_list = c->back_list;
+        a.front_list = front;
+        a.back_list = back;
         Timer t(c, "ev_apply");
         launch_ev_apply(a, c->stream);
     }
@@ -288,7 +335,7 @@ int enqueue_tick(fb_ctx *c) {
     a.nbf = nbf;
     a.nbq = nbq;
     // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
-    a.fused = (!c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
+    a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
     a.tick = c->tick;
     a.now = c->l_now;
@@ -308,8 +355,8 @@ int enqueue_tick(fb_ctx *c) {
     a.post_flags = c->post_flags;
     a.post_hb = c->post_hb;
     a.post_free = c->post_free;
-    a.front_list = c->front_list;
-    a.back_list = c->back_list;
+    a.front_list = front;
+    a.back_list = back;
     a.st = c->st;
     a.dmask = c->dmask;
     a.c_arr = c->c_arr;
@@ -332,6 +379,20 @@ int enqueue_tick(fb_ctx *c) {
     a.orphans = c->orphans;
     a.evicted = c->evicted;
     a.hout = c->hout_dev;
+    if (c->shard) {
+        a.shard = c->phase == 2 ? 2 : 1;
+        a.slot_base = c->slot_base;
+        a.rank = c->rank;
+        a.world = c->world;
+        a.head_local = c->l_head_local;
+        a.lseq = c->lseq;
+        a.lseq_out = c->lseq;
+        a.xc8 = c->xbuf + xl.c8;
+        a.xrec = (unsigned long long *)(c->xbuf + xl.rec);
+        a.ocnt = c->ocnt;
+        a.opre = c->opre;
+        a.oA = c->oA;
+    }
     {
         const size_t need = (size_t)2 * (nbw + nbf + nbq) * 16 + 16;
         if (need > c->dbg_n) {
@@ -341,6 +402,32 @@ int enqueue_tick(fb_ctx *c) {
             c->dbg_n = need;
         }
         a.dbg = c->dbg;
+    }
+    if (a.shard == 1) {
+        // phase 1: own slots' purge, orphan flags and free counts into the exchange buffer
+        {
+            Timer t(c, "slots");
+            launch_slots(a, c->stream);
+        }
+        Timer t(c, "scan");
+        launch_scan(a, c->stream);
+        HIPCHK(c, hipGetLastError());
+        return FB_OK;
+    }
+    if (a.shard == 2) {
+        if (R > kRFused) return fail(c, FB_ERANGE, "sharded tick: free counts need %d rounds (limit %d)", R, kRFused);
+        {
+            Timer t(c, "scan");
+            launch_scan(a, c->stream);
+        }
+        {
+            Timer t(c, "plan");
+            launch_plan(a, c->stream);
+        }
+        Timer t(c, "emit");
+        launch_emit_shard(a, c->stream);
+        HIPCHK(c, hipGetLastError());
+        return FB_OK;
     }
     {
         Timer t(c, "slots");
@@ -368,28 +455,42 @@ extern "C" {
 
 const char *fb_last_error(const fb_ctx *ctx) { return ctx ? ctx->err.c_str() : "null context"; }
 
-int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_events, int device) {
+}  // extern "C"
+
+namespace {
+int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_events, int device, int shard,
+               int rank, int world, int32_t n_workers_global) {
     if (!out) return FB_EINVAL;
     *out = nullptr;
     if (max_workers < 1 || max_log < 1 || max_events < 0 || max_log >= ((int64_t)1 << 31) ||
         max_workers >= (1 << 30) || max_events >= (1 << 28))
         return FB_EINVAL;
+    if (shard && (world < 1 || rank < 0 || rank >= world || n_workers_global < max_workers ||
+                  n_workers_global >= (1 << 30)))
+        return FB_EINVAL;
     fb_ctx *c = new fb_ctx();
     c->device = device;
+    c->shard = shard;
+    c->rank = shard ? rank : 0;
+    c->world = shard ? world : 1;
+    c->W_global = shard ? n_workers_global : max_workers;
+    c->Wq_cap = c->W_global;
     c->W_cap = max_workers;
     c->E_cap = std::max(max_events, 1);
     c->log_cap = max_log;
-    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&c->own_s, hipStreamNonBlocking) != hipSuccess) {
         delete c;
         return FB_EHIP;
     }
+    c->stream = c->own_s;
     const size_t W = (size_t)max_workers, E = (size_t)c->E_cap, F = (size_t)max_log;
-    const size_t Qlog = W + 2 * E;
+    const size_t Wq = (size_t)c->Wq_cap;  // queue entries are global slots
+    const size_t Qlog = Wq + 2 * E;
     ArenaPlan ap;
     for (int i = 0; i < 2; ++i) {
         ap.add(&c->free_[i], W);
         ap.add(&c->inq[i], W);
-        ap.add(&c->queue[i], W);
+        ap.add(&c->queue[i], Wq);
     }
     ap.add(&c->reg, W);
     ap.add(&c->hb, W);
@@ -432,6 +533,12 @@ int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_ev
     ap.add(&c->A, 128);
     ap.add(&c->log_slot, F);
     ap.add(&c->orphans, F);
+    if (shard) {
+        ap.add(&c->lseq, F);
+        ap.add(&c->ocnt, tab);
+        ap.add(&c->opre, tab);
+        ap.add(&c->oA, 128);
+    }
     int rc = arena_commit(c, ap);
     if (!rc) {
         c->table_cap = tab;
@@ -452,6 +559,18 @@ int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_ev
     *out = c;
     return FB_OK;
 }
+}  // namespace
+
+extern "C" {
+
+int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_events, int device) {
+    return create_ctx(out, max_workers, max_log, max_events, device, 0, 0, 1, max_workers);
+}
+
+int fb_create_sharded(fb_ctx **out, int32_t max_workers_local, int32_t n_workers_global, int64_t max_log_local,
+                      int32_t max_events, int device, int32_t rank, int32_t world) {
+    return create_ctx(out, max_workers_local, max_log_local, max_events, device, 1, rank, world, n_workers_global);
+}
 
 int fb_destroy(fb_ctx *c) {
     if (!c) return FB_OK;
@@ -471,7 +590,7 @@ int fb_destroy(fb_ctx *c) {
         hipEventDestroy(t.b);
     }
     for (auto e : c->ev_pool) hipEventDestroy(e);
-    if (c->stream) hipStreamDestroy(c->stream);
+    if (c->own_s) hipStreamDestroy(c->own_s);
     delete c;
     return FB_OK;
 }
@@ -480,6 +599,7 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
                   const double *last_heartbeat, const uint32_t *epoch, const int32_t *queue, int64_t queue_len,
                   const int32_t *log_slot, int64_t log_len) {
     if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_load_shard");
     if (n_workers < 0 || n_workers > c->W_cap) return fail(c, FB_EINVAL, "n_workers %d outside [0, %d]", n_workers, c->W_cap);
     if (log_len < 0 || log_len > c->log_cap) return fail(c, FB_EINVAL, "log_len %lld exceeds capacity", (long long)log_len);
     if (queue_len < 0 || queue_len > n_workers) return fail(c, FB_EINVAL, "queue_len %lld", (long long)queue_len);
@@ -534,9 +654,121 @@ int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, doubl
     }
     if (queue && c->Qn) HIPCHK(c, hipMemcpy(queue, c->queue[c->cur], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
     if (queue_len) *queue_len = c->Qn;
-    if (log_slot && c->head) HIPCHK(c, hipMemcpy(log_slot, c->log_slot, (size_t)c->head * 4, hipMemcpyDeviceToHost));
-    if (log_len) *log_len = c->head;
+    const int64_t nlog = c->shard ? c->head_local : c->head;
+    if (log_slot && nlog) HIPCHK(c, hipMemcpy(log_slot, c->log_slot, (size_t)nlog * 4, hipMemcpyDeviceToHost));
+    if (log_len) *log_len = nlog;
     return FB_OK;
+}
+
+int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t *registered,
+                  const int32_t *free_processes, const double *last_heartbeat, const uint32_t *epoch,
+                  const int32_t *queue, int64_t queue_len, const int32_t *log_slot, const uint32_t *log_seq,
+                  int64_t log_len, int64_t log_head) {
+    if (!c) return FB_EINVAL;
+    if (!c->shard) return fail(c, FB_ESTATE, "fb_load_shard on a one-GPU context");
+    if (n_workers < 0 || n_workers > c->W_cap || slot_base < 0 || (int64_t)slot_base + n_workers > c->W_global)
+        return fail(c, FB_EINVAL, "slot range [%d, %d + %d) outside the %d-slot table", slot_base, slot_base, n_workers,
+                    c->W_global);
+    if (log_len < 0 || log_len > c->log_cap || log_head < log_len || log_head >= ((int64_t)1 << 31))
+        return fail(c, FB_EINVAL, "log_len %lld / log_head %lld", (long long)log_len, (long long)log_head);
+    if (queue_len < 0 || queue_len > c->W_global) return fail(c, FB_EINVAL, "queue_len %lld", (long long)queue_len);
+    const size_t W = (size_t)n_workers;
+    std::vector<uint8_t> inq(W ? W : 1, 0), seen((size_t)c->W_global, 0);
+    int32_t maxc = 1;
+    for (int64_t i = 0; i < queue_len; ++i) {
+        const int32_t s = queue[i];
+        if (s < 0 || s >= c->W_global || seen[s])
+            return fail(c, FB_EINVAL, "queue[%lld] = %d is out of range or duplicated", (long long)i, s);
+        seen[s] = 1;
+        const int32_t ls = s - slot_base;
+        if (ls >= 0 && ls < n_workers) {
+            if (!registered[ls]) return fail(c, FB_EINVAL, "queue[%lld] = %d is not registered", (long long)i, s);
+            inq[ls] = 1;
+            maxc = std::max(maxc, free_processes[ls]);
+        }
+    }
+    for (int64_t i = 0; i < log_len; ++i) {
+        const int32_t s = log_slot[i];
+        if (s < -1 || (s >= 0 && (s < slot_base || s >= slot_base + n_workers)))
+            return fail(c, FB_EINVAL, "log_slot[%lld] = %d is not one of this rank's slots", (long long)i, s);
+        if ((int64_t)log_seq[i] >= log_head || (i && log_seq[i] <= log_seq[i - 1]))
+            return fail(c, FB_EINVAL, "log_seq must ascend below log_head (entry %lld)", (long long)i);
+    }
+    std::vector<uint8_t> reg(W ? W : 1, 0);
+    for (size_t s = 0; s < W; ++s) reg[s] = registered[s] ? 1 : 0;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->cur = 0;
+    if (W) {
+        HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->free_[0], free_processes, W * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->hb, last_heartbeat, W * 8, hipMemcpyHostToDevice));
+        if (epoch) HIPCHK(c, hipMemcpy(c->epoch, epoch, W * 4, hipMemcpyHostToDevice));
+        else HIPCHK(c, hipMemset(c->epoch, 0, W * 4));
+        HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
+    }
+    if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
+    if (log_len) {
+        HIPCHK(c, hipMemcpy(c->log_slot, log_slot, (size_t)log_len * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->lseq, log_seq, (size_t)log_len * 4, hipMemcpyHostToDevice));
+    }
+    c->slot_base = slot_base;
+    c->W = n_workers;
+    c->Qn = queue_len;
+    c->head = log_head;
+    c->head_local = log_len;
+    c->tick += 1;
+    c->maxc_hint = maxc;
+    c->launched = c->waited = false;
+    c->phase = 0;
+    return FB_OK;
+}
+
+int fb_read_shard_log(fb_ctx *c, uint32_t *log_seq, int64_t *log_len, int64_t *log_head) {
+    if (!c) return FB_EINVAL;
+    if (!c->shard) return fail(c, FB_ESTATE, "fb_read_shard_log on a one-GPU context");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (log_seq && c->head_local)
+        HIPCHK(c, hipMemcpy(log_seq, c->lseq, (size_t)c->head_local * 4, hipMemcpyDeviceToHost));
+    if (log_len) *log_len = c->head_local;
+    if (log_head) *log_head = c->head;
+    return FB_OK;
+}
+
+int fb_bind_exchange(fb_ctx *c, void *device_buffer, int64_t bytes) {
+    if (!c) return FB_EINVAL;
+    if (!c->shard) return fail(c, FB_ESTATE, "fb_bind_exchange on a one-GPU context");
+    if (bytes < 0 || (bytes && !device_buffer)) return fail(c, FB_EINVAL, "exchange buffer");
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->xbuf = (uint8_t *)device_buffer;
+    c->xcap = bytes;
+    return FB_OK;
+}
+
+int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
+    if (!c || !bytes) return FB_EINVAL;
+    const int64_t E = n_events < 0 ? c->E_cap : n_events;
+    const int64_t Qn = n_events < 0 ? c->Wq_cap : (c->launched ? c->l_Qn : c->Qn);
+    *bytes = (int64_t)xlayout(c->world, E, Qn + 2 * E).total;
+    return FB_OK;
+}
+
+int fb_set_stream(fb_ctx *c, void *stream) {
+    if (!c) return FB_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    c->stream = stream ? (hipStream_t)stream : c->own_s;
+    return FB_OK;
+}
+
+int fb_tick_continue(fb_ctx *c) {
+    if (!c) return FB_EINVAL;
+    if (!c->shard) return fail(c, FB_ESTATE, "fb_tick_continue on a one-GPU context");
+    if (!c->launched || c->phase != 1) return fail(c, FB_ESTATE, "fb_tick_continue without fb_tick_launch");
+    HIPCHK(c, hipSetDevice(c->device));
+    c->phase = 2;
+    return enqueue_tick(c);
 }
 
 int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
@@ -549,7 +781,8 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
     const int E = n_events;
     int32_t vmax = 0;
     for (int i = 0; i < E; ++i) {
-        if (slot[i] < 0 || slot[i] >= c->W) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %d)", i, slot[i], c->W);
+        const int32_t Wv = c->shard ? c->W_global : c->W;
+        if (slot[i] < 0 || slot[i] >= Wv) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %d)", i, slot[i], Wv);
         if (kind[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, kind[i]);
         if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
             return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
@@ -583,7 +816,9 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
     c->l_E = E;
     c->l_T = n_pending;
     c->l_head = c->head;
+    c->l_head_local = c->head_local;
     c->l_Qn = c->Qn;
+    c->phase = 1;
     c->l_R = choose_R(std::max(c->maxc_hint, vmax));
     c->reruns = 0;
     c->launched = true;
@@ -594,6 +829,7 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
 int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     if (!c) return FB_EINVAL;
     if (!c->launched) return fail(c, FB_ESTATE, "fb_tick_wait without fb_tick_launch");
+    if (c->shard && c->phase != 2) return fail(c, FB_ESTATE, "sharded tick: exchange, then fb_tick_continue");
     HIPCHK(c, hipSetDevice(c->device));
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -620,6 +856,8 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     r.fill_level = p.L;
     r.max_free = p.maxc;
     r.reruns = c->reruns;
+    r.n_local = c->shard ? p.n_local : p.N_eff;
+    r.n_orphans_local = c->shard ? p.O_local : p.O;
     c->last = r;
     c->waited = true;
     if (res) *res = r;
@@ -647,16 +885,38 @@ int fb_tick_commit(fb_ctx *c) {
     }
     c->cur = 1 - c->cur;
     c->head = c->last.log_head;
+    c->head_local += c->shard ? c->last.n_local : 0;
     c->Qn = c->last.queue_len;
     c->maxc_hint = std::max(1, c->last.max_free);
     c->tick += 1;
     c->launched = c->waited = false;
+    c->phase = 0;
+    return FB_OK;
+}
+
+int fb_get_local_assignments(fb_ctx *c, int64_t first, int64_t n, int64_t *task, int32_t *slot) {
+    if (!c) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (first < 0 || n < 0 || first + n > c->last.n_local) return fail(c, FB_EINVAL, "assignment range");
+    if (!n) return FB_OK;
+    const int64_t base = c->shard ? c->l_head_local : c->l_head;
+    if (slot) HIPCHK(c, hipMemcpy(slot, c->log_slot + base + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+    if (task) {
+        if (c->shard) {
+            std::vector<uint32_t> q((size_t)n);
+            HIPCHK(c, hipMemcpy(q.data(), c->lseq + base + first, (size_t)n * 4, hipMemcpyDeviceToHost));
+            for (int64_t i = 0; i < n; ++i) task[i] = (int64_t)q[i] - c->l_head;
+        } else {
+            for (int64_t i = 0; i < n; ++i) task[i] = first + i;
+        }
+    }
     return FB_OK;
 }
 
 int fb_get_assignments(fb_ctx *c, int64_t first, int64_t n, int32_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_get_local_assignments");
     if (first < 0 || n < 0 || first + n > c->last.n_assigned) return fail(c, FB_EINVAL, "assignment range");
     if (n) HIPCHK(c, hipMemcpy(dst, c->log_slot + c->l_head + first, (size_t)n * 4, hipMemcpyDeviceToHost));
     return FB_OK;
@@ -665,7 +925,7 @@ int fb_get_assignments(fb_ctx *c, int64_t first, int64_t n, int32_t *dst) {
 int fb_get_orphans(fb_ctx *c, int64_t n, int64_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
-    if (n < 0 || n > c->last.n_orphans) return fail(c, FB_EINVAL, "orphan count");
+    if (n < 0 || n > c->last.n_orphans_local) return fail(c, FB_EINVAL, "orphan count");
     if (n) HIPCHK(c, hipMemcpy(dst, c->orphans, (size_t)n * 8, hipMemcpyDeviceToHost));
     return FB_OK;
 }
@@ -682,7 +942,8 @@ int fb_get_event_status(fb_ctx *c, int32_t n, uint8_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (n < 0 || n > c->l_E) return fail(c, FB_EINVAL, "event count");
-    if (n) HIPCHK(c, hipMemcpy(dst, c->ev_status, (size_t)n, hipMemcpyDeviceToHost));
+    const uint8_t *src = c->shard ? c->xbuf + xlayout(c->world, c->l_E, c->l_Qn + 2 * (int64_t)c->l_E).evs : c->ev_status;
+    if (n) HIPCHK(c, hipMemcpy(dst, src, (size_t)n, hipMemcpyDeviceToHost));
     return FB_OK;
 }
 

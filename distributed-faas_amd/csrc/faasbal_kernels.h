@@ -41,16 +41,23 @@ struct HostOut {
     int32_t maxc;       // max c
     int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
     int32_t pad;
+    int64_t n_local;    // sharded: tasks appended to this rank's log shard
+    int64_t O_local;    // sharded: this rank's orphans
 };
 
 // totals computed by k_plan (large grids only; device memory, no atomics)
 struct DevTotals {
-    int64_t O, n_evicted, cap_total;
+    int64_t O, n_evicted, cap_total;  // O: orphans of every rank (tasks dispatched first)
     int32_t maxc, pad;
+    int64_t O_local;                  // sharded: this rank's orphans
 };
 
 struct EvArgs {
     int E;
+    int shard;          // 0: one GPU; else this rank owns global slots [slot_base, slot_base + W)
+    int slot_base, W;
+    int64_t head_local; // sharded: local log length (entries carry their global seq in lseq)
+    const uint32_t *lseq;
     uint32_t tick;
     double tte;
     int64_t head_in;
@@ -72,7 +79,7 @@ struct EvArgs {
     uint32_t *post_epoch;
     uint8_t *post_flags;
     uint32_t *touched;
-    int32_t *front_list, *back_list;
+    int32_t *front_list, *back_list;  // slot + 1 (0 = empty), zeroed before the tick
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -94,7 +101,7 @@ struct TickArgs {
     const uint8_t *post_reg, *post_flags;
     const double *post_hb;
     const int32_t *post_free;
-    const int32_t *front_list, *back_list;
+    const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates
     uint8_t *st;
     unsigned long long *dmask;  // bit s: the registration alive at tick start died this tick
@@ -114,10 +121,22 @@ struct TickArgs {
     int32_t *evicted;
     HostOut *hout;
     unsigned long long *dbg;  // diagnostic stamps (FAASBAL_STAMPS builds only)
+    // sharding: 0 one GPU; 1 phase 1 (own slots -> exchange); 2 phase 2 (after the
+    // exchange all-reduce).  W above is then the local slot count; queue entries are global ids.
+    int shard;
+    int slot_base, rank, world;
+    int64_t head_local;            // local log entries; lseq[i] = global sequence of entry i (ascending)
+    const uint32_t *lseq;
+    uint32_t *lseq_out;
+    uint8_t *xc8;                  // exchange: min(c, 255) per LRU position (single contributor per byte)
+    unsigned long long *xrec;      // exchange: per rank {O, sum c, max c, -}
+    uint32_t *ocnt;                // [block][round] counts of this rank's positions
+    int64_t *opre, *oA;
 };
 
 struct CommitArgs {
     int W;
+    int slot_base;
     uint32_t tick;
     const uint8_t *st;
     const uint32_t *touched;
@@ -140,6 +159,7 @@ void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
 void launch_plan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
+void launch_emit_shard(const TickArgs &a, Stream st);
 void launch_commit(const CommitArgs &a, int grid, Stream st);
 
 }  // namespace fb

@@ -252,11 +252,24 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
 // One thread per slot segment of the slot-sorted events; processes that
 // slot's messages in arrival order (task_dispatcher.py:343-390 per message,
 // with the purge of the preceding loop iteration at the same clock).
+// Sharded: local log position of global sequence q (entries ascend), or -1.
+__device__ __forceinline__ int64_t lseq_find(const uint32_t *lseq, int64_t n, int64_t q) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)lseq[mid] < q) lo = mid + 1;
+        else hi = mid;
+    }
+    return (lo < n && (int64_t)lseq[lo] == q) ? lo : -1;
+}
+
 __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     const int j = blockIdx.x * kBS + threadIdx.x;
     if (j >= a.E) return;
-    const uint32_t s = a.skeys[j];
-    if (j > 0 && a.skeys[j - 1] == s) return;
+    const uint32_t gs = a.skeys[j];
+    if (j > 0 && a.skeys[j - 1] == gs) return;
+    if (a.shard && ((int)gs < a.slot_base || (int)gs >= a.slot_base + a.W)) return;  // another rank's worker
+    const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
     int reg = a.reg[s];
     int32_t fr = a.free_in[s];
     double hb = a.hb[s];
@@ -265,7 +278,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     int qstat = inq ? kQsKeep : kQsOut;
     int qidx = -1;
     int cur_is_start = reg, died_start = 0;
-    for (int k = j; k < a.E && a.skeys[k] == s; ++k) {
+    for (int k = j; k < a.E && a.skeys[k] == gs; ++k) {
         const int i = (int)a.svals[k];
         const int kind = a.ev_kind[i];
         const int32_t val = a.ev_val[i];
@@ -296,7 +309,10 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
             fr += 1;
             hb = ts;
             const int64_t q = a.ev_seq[i];
-            if (q >= 0 && q < a.head_in && a.log_slot[q] == (int32_t)s) a.log_slot[q] = -1;
+            if (q >= 0 && q < a.head_in) {
+                const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
+                if (li >= 0 && a.log_slot[li] == (int32_t)gs) a.log_slot[li] = -1;
+            }
             if (fr == 1 && !inq) { inq = 1; qstat = kQsBack; qidx = i; }
         }
         a.ev_status[i] = status;
@@ -307,8 +323,8 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     a.post_epoch[s] = epoch;
     a.post_flags[s] = (uint8_t)(died_start | (qstat << 1));
     a.touched[s] = a.tick;
-    if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)s;
-    if (qstat == kQsBack) a.back_list[qidx] = (int32_t)s;
+    if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)gs + 1;
+    if (qstat == kQsBack) a.back_list[qidx] = (int32_t)gs + 1;
 }
 
 
@@ -343,11 +359,18 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
 // fp64 subtract then compare, exactly as written.
 __device__ __forceinline__ bool is_dead(const TickArgs &a, const Cur &c) { return c.reg && ((a.now - c.hb) > a.tte); }
 
+// Global slot at logical LRU position pos of fronts ++ queue ++ backs, or -1.
 __device__ __forceinline__ int lq_slot(const TickArgs &a, int64_t pos) {
-    if (pos < a.E) return a.front_list[pos];
+    if (pos < a.E) return a.front_list[pos] - 1;
     pos -= a.E;
     if (pos < a.Qn) return a.queue_in[pos];
-    return a.back_list[pos - a.Qn];
+    return a.back_list[pos - a.Qn] - 1;
+}
+// Local index of global slot s if this rank owns it, else -1 (one GPU: s itself).
+__device__ __forceinline__ int own_slot(const TickArgs &a, int s) {
+    if (!a.shard) return s;
+    const int ls = s - a.slot_base;
+    return (s >= 0 && ls >= 0 && ls < a.W) ? ls : -1;
 }
 
 // ------------------------------------------------------------ helpers
@@ -453,20 +476,26 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
     __shared__ uint32_t wc[kWaves][kBS];
     const int bid = blockIdx.x;
     const int SO = a.nbw;
+    const int nbf = a.shard == 2 ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
     STAMP(a, SO, 0);
-    if (bid < a.nbf) {
+    if (bid < nbf) {
         // ---- F-role: orphan flags of log entries [b*2048 + t*8, +8)
         const int b = bid;
+        const int64_t nlog = a.shard ? a.head_local : a.head_in;
         const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
         int32_t v[kFItems];
-        if (base + kFItems <= a.head_in) {
+        if (base + kFItems <= nlog) {
             const int4 x0 = *reinterpret_cast<const int4 *>(a.log_slot + base);
             const int4 x1 = *reinterpret_cast<const int4 *>(a.log_slot + base + 4);
             v[0] = x0.x; v[1] = x0.y; v[2] = x0.z; v[3] = x0.w;
             v[4] = x1.x; v[5] = x1.y; v[6] = x1.z; v[7] = x1.w;
         } else {
 #pragma unroll
-            for (int j = 0; j < kFItems; ++j) v[j] = (base + j < a.head_in) ? a.log_slot[base + j] : -1;
+            for (int j = 0; j < kFItems; ++j) v[j] = (base + j < nlog) ? a.log_slot[base + j] : -1;
+        }
+        if (a.shard) {  // log slots are global ids; this rank's bitmap and epochs are local
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) v[j] = v[j] < 0 ? -1 : v[j] - a.slot_base;
         }
         const int nwords = (a.W + 63) >> 6;
         const unsigned long long *dm = a.dmask;
@@ -499,60 +528,91 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
         if (died) {
 #pragma unroll
             for (int j = 0; j < kFItems; ++j)
-                if (((died >> j) & 1u) && (uint64_t)(base + j) >= (uint64_t)a.epoch[v[j]]) flags |= 1u << j;
+                if ((died >> j) & 1u) {
+                    const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
+                    if (seq >= (uint64_t)a.epoch[v[j]]) flags |= 1u << j;
+                }
         }
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
         const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
         if (lane_id() == 0) l4[wave_id()] = wv;
         __syncthreads();
-        if (threadIdx.x == 0) a.fcnt[b] = l4[0] + l4[1] + l4[2] + l4[3];
+        if (threadIdx.x == 0) {
+            const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
+            a.fcnt[b] = n;
+            if (a.shard && n) atomicAdd(&a.xrec[a.rank * 4 + 0], (unsigned long long)n);
+        }
         STAMP(a, SO, 15);
         return;
     }
     // ---- Q-role: LRU positions [b*256, +256) of fronts ++ queue ++ backs
-    const int b = bid - a.nbf;
+    const int b = bid - nbf;
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
-    int c = 0;
-    if (pos < a.Qlog) {
+    int c = 0, oc = 0;
+    if (a.shard == 2) {
+        // phase 2 of a sharded tick: every rank's effective free counts arrived in the exchange
+        if (pos < a.Qlog) {
+            c = a.xc8[pos];
+            oc = (c > 0 && own_slot(a, lq_slot(a, pos)) >= 0) ? c : 0;
+        }
+    } else if (pos < a.Qlog) {
         const int s = lq_slot(a, pos);
-        int32_t raw = s >= 0 ? a.free_out[s] : INT32_MIN;  // INT32_MIN: no live record
+        const int ls = s >= 0 ? own_slot(a, s) : -1;
+        int32_t raw = ls >= 0 ? a.free_out[ls] : INT32_MIN;  // INT32_MIN: no live record (or not mine)
         // an old queue entry moved to the front, re-appended or removed by this tick's messages
-        if (raw != INT32_MIN && a.E > 0 && pos >= a.E && pos < a.E + a.Qn && a.touched[s] == a.tick &&
-            ((a.post_flags[s] >> 1) & 3) != kQsKeep)
+        if (raw != INT32_MIN && a.E > 0 && pos >= a.E && pos < a.E + a.Qn && a.touched[ls] == a.tick &&
+            ((a.post_flags[ls] >> 1) & 3) != kQsKeep)
             raw = INT32_MIN;
         if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
         a.c_arr[pos] = raw;
+        if (a.shard == 1) a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
     }
     STAMP(a, SO, 1);
     const uint32_t wmx = wave_max_u32((uint32_t)c);
+    if (a.shard == 1) {
+        // phase 1: this rank's capacity and max c go to its exchange record (exact values)
+        const uint32_t ws = wave_sum_u32((uint32_t)c);
+        if (lane_id() == 0) {
+            atomicAdd(&a.xrec[a.rank * 4 + 1], (unsigned long long)ws);
+            atomicMax(&a.xrec[a.rank * 4 + 2], (unsigned long long)wmx);
+        }
+        STAMP(a, SO, 15);
+        return;
+    }
     if (lane_id() == 0) m4[wave_id()] = (int32_t)wmx;
     unsigned long long csum = 0;
     for (int rc = 0; rc < a.R; rc += kBS) {
         const int rn = (a.R - rc) < kBS ? (a.R - rc) : kBS;
+        for (int tab = 0; tab < (a.shard == 2 ? 2 : 1); ++tab) {
+            const int cc = tab ? oc : c;
 #pragma unroll
-        for (int g = 0; g < kBS / 64; ++g) {
-            const int r0 = rc + g * 64;
-            uint32_t cnt = 0;
-            if (r0 < rc + rn && r0 < (int)wmx) {
-                int k = rc + rn - r0;
-                k = k < 64 ? k : 64;
-                k = k < (int)wmx - r0 ? k : (int)wmx - r0;
-                cnt = wave_round_counts(c, r0, k);
+            for (int g = 0; g < kBS / 64; ++g) {
+                const int r0 = rc + g * 64;
+                uint32_t cnt = 0;
+                if (r0 < rc + rn && r0 < (int)wmx) {
+                    int k = rc + rn - r0;
+                    k = k < 64 ? k : 64;
+                    k = k < (int)wmx - r0 ? k : (int)wmx - r0;
+                    cnt = wave_round_counts(cc, r0, k);
+                }
+                wc[wave_id()][g * 64 + lane_id()] = cnt;
             }
-            wc[wave_id()][g * 64 + lane_id()] = cnt;
+            __syncthreads();
+            uint32_t t = 0;
+            if ((int)threadIdx.x < rn) {
+                t = wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
+                uint32_t *tabp = tab ? a.ocnt : a.qcnt;
+                tabp[(size_t)b * a.R + rc + threadIdx.x] = t;
+            }
+            if (tab == 0) {
+                // sum_r count(c > r) over r < R = sum of min(c, R): the block's capacity when c <= R
+                const uint32_t ts = wave_sum_u32(t);
+                if (lane_id() == 0) l4[wave_id()] = ts;
+                __syncthreads();
+                csum += (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
+            }
+            __syncthreads();
         }
-        __syncthreads();
-        uint32_t t = 0;
-        if ((int)threadIdx.x < rn) {
-            t = wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
-            a.qcnt[(size_t)b * a.R + rc + threadIdx.x] = t;
-        }
-        // sum_r count(c > r) over r < R = sum of min(c, R): the block's capacity when c <= R
-        const uint32_t ts = wave_sum_u32(t);
-        if (lane_id() == 0) l4[wave_id()] = ts;
-        __syncthreads();
-        csum += (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
-        __syncthreads();
     }
     if (threadIdx.x == 0) {
         int bm = m4[0];
@@ -583,8 +643,27 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
             carry += tot;
         }
         if (threadIdx.x == 0) {
-            if (bid == 0) a.P->O = (int64_t)carry;
-            else a.P->n_evicted = (int64_t)carry;
+            if (bid == 0) {
+                a.P->O_local = (int64_t)carry;
+                if (!a.shard) a.P->O = (int64_t)carry;
+            } else {
+                a.P->n_evicted = (int64_t)carry;
+            }
+        }
+        return;
+    }
+    if (bid == 2 && a.shard) {
+        // sharded: exact totals from every rank's exchange record
+        if (threadIdx.x == 0) {
+            unsigned long long O = 0, cap = 0, mx = 0;
+            for (int g = 0; g < a.world; ++g) {
+                O += a.xrec[g * 4 + 0];
+                cap += a.xrec[g * 4 + 1];
+                mx = a.xrec[g * 4 + 2] > mx ? a.xrec[g * 4 + 2] : mx;
+            }
+            a.P->O = (int64_t)O;
+            a.P->cap_total = (int64_t)cap;
+            a.P->maxc = (int32_t)mx;
         }
         return;
     }
@@ -604,18 +683,23 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
         }
         return;
     }
-    const int r = bid - 3;
-    if (r >= a.R) return;
+    // rows: r < R of all positions, then (sharded) r < R of this rank's positions
+    const int rr = bid - 3;
+    const bool mine = rr >= a.R;
+    const int r = mine ? rr - a.R : rr;
+    if (r >= a.R || (mine && !a.shard)) return;
+    const uint32_t *cnt = mine ? a.ocnt : a.qcnt;
+    int64_t *pre = mine ? a.opre : a.qpre;
     unsigned long long carry = 0;
     for (int base = 0; base < a.nbq; base += kBS) {
         const int b = base + threadIdx.x;
         unsigned long long v = 0, tot;
-        if (b < a.nbq) v = a.qcnt[(size_t)b * a.R + r];
+        if (b < a.nbq) v = cnt[(size_t)b * a.R + r];
         const unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
-        if (b < a.nbq) a.qpre[(size_t)b * a.R + r] = (int64_t)(carry + ex);
+        if (b < a.nbq) pre[(size_t)b * a.R + r] = (int64_t)(carry + ex);
         carry += tot;
     }
-    if (threadIdx.x == 0) a.A[r] = (int64_t)carry;
+    if (threadIdx.x == 0) (mine ? a.oA : a.A)[r] = (int64_t)carry;
 }
 
 // ------------------------------------------------------------ k_emit
@@ -1003,6 +1087,221 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
     STAMP(a, SO, 15);
 }
 
+// ------------------------------------------------------------ k_emit_shard
+// Phase 2 of a sharded tick.  Every rank computes the global water-filling from
+// the exchanged counts (identical on all ranks), writes the whole next LRU queue,
+// and appends only its own workers' tasks to its log shard -- in ascending global
+// sequence, because own tasks are placed round-major by their own rank.
+struct EmitShardLds {
+    uint32_t wc[kWaves][kBS], owc[kWaves][kBS];
+    int32_t wbase[kWaves][kBS], wpos[kWaves][kBS], obase[kWaves][kBS], opos[kWaves][kBS];
+};
+
+__global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
+    __shared__ EmitShardLds E_;
+    __shared__ unsigned long long red64[kWaves];
+    __shared__ int64_t S_l[kBS + 1], So_l[kBS + 1];
+    __shared__ int64_t pre_c[kBS], opre_c[kBS];
+    __shared__ int32_t misc[8];
+    const int bid = blockIdx.x;
+    const int lane = lane_id(), w = wave_id();
+    if (bid < a.nbq) {
+        const int b = bid;
+        const int64_t pos = (int64_t)b * kBS + threadIdx.x;
+        int c = 0, s = -1, ls = -1;
+        int32_t raw = INT32_MIN;
+        if (pos < a.Qlog) {
+            c = a.xc8[pos];
+            s = lq_slot(a, pos);
+            ls = s >= 0 ? own_slot(a, s) : -1;
+            if (ls >= 0) raw = a.c_arr[pos];
+        }
+        const bool own = c > 0 && ls >= 0;
+        const int bm = a.qbm_raw[b];
+        const int64_t O = a.P->O;
+        int64_t cap = a.P->cap_total;
+        const int maxc = a.P->maxc;
+        const int rlim = maxc < a.R ? maxc : a.R;
+        if (maxc > a.R) cap = INT64_MAX;
+        const int64_t N = O + a.T;
+        const int64_t N_eff = N < cap ? N : cap;
+        // fill level L = max{ r in [0, maxc] : S(r) <= N_eff }
+        int L = 0;
+        int64_t S_L = 0;
+        {
+            int64_t carry = 0;
+            for (int rc = 0; rc < rlim; rc += kBS) {
+                const int r = rc + threadIdx.x;
+                const unsigned long long v = r < rlim ? (unsigned long long)a.A[r] : 0ull;
+                unsigned long long tot;
+                const unsigned long long ex = block_excl_scan<unsigned long long>(v, red64, tot);
+                const int64_t S1 = carry + (int64_t)(ex + v);
+                const int k_w = __popcll(__ballot(r < rlim && S1 <= N_eff));
+                if (lane == 0) misc[w] = k_w;
+                S_l[threadIdx.x + 1] = S1;
+                if (threadIdx.x == 0) S_l[0] = carry;
+                __syncthreads();
+                const int k = misc[0] + misc[1] + misc[2] + misc[3];
+                L += k;
+                S_L = S_l[k];
+                __syncthreads();
+                if (k < kBS) break;
+                carry += (int64_t)tot;
+            }
+        }
+        int status = 0;
+        if (maxc > a.R && L >= a.R - 1) status = 1;
+        if (a.head_local + N_eff > a.log_cap) status = 2;
+        const int64_t p = N_eff - S_L;
+        const int64_t AL = (L < maxc && L < rlim) ? a.A[L] : 0;
+        if (b == 0 && threadIdx.x == 0) {
+            a.hout->O = O;
+            a.hout->O_local = a.P->O_local;
+            a.hout->n_evicted = a.P->n_evicted;
+            a.hout->cap_total = cap;
+            a.hout->maxc = maxc;
+            a.hout->L = L;
+            a.hout->status = status;
+            a.hout->N_eff = status ? 0 : N_eff;
+            a.hout->p = p;
+            a.hout->AL = AL;
+        }
+        if (status) return;
+        int64_t rankL = -1, orankL = 0, exL1 = 0, oSL = 0;
+        int64_t carryS = 0, carryO = 0;
+        const int wmx = (int)wave_max_u32((uint32_t)c);
+        const int oc = own ? c : 0;
+        for (int rc = 0; rc <= L + 1; rc += kBS) {
+            const int rn = (L + 2 - rc) < kBS ? (L + 2 - rc) : kBS;
+            {
+                const int r = rc + threadIdx.x;
+                int64_t pr = 0, opr = 0, Av = 0, oAv = 0;
+                if ((int)threadIdx.x < rn && r < rlim) {
+                    pr = a.qpre[(size_t)b * a.R + r];
+                    opr = a.opre[(size_t)b * a.R + r];
+                    Av = a.A[r];
+                    oAv = a.oA[r];
+                }
+                unsigned long long tot, otot;
+                const unsigned long long ex = block_excl_scan<unsigned long long>((unsigned long long)Av, red64, tot);
+                const unsigned long long oex = block_excl_scan<unsigned long long>((unsigned long long)oAv, red64, otot);
+                pre_c[threadIdx.x] = pr;
+                opre_c[threadIdx.x] = opr;
+                S_l[threadIdx.x] = carryS + (int64_t)ex;
+                So_l[threadIdx.x] = carryO + (int64_t)oex;
+                carryS += (int64_t)tot;
+                carryO += (int64_t)otot;
+            }
+#pragma unroll
+            for (int g = 0; g < kBS / 64; ++g) {
+                const int r0 = rc + g * 64;
+                uint32_t cnt = 0, ocnt = 0;
+                if (r0 < rc + rn && r0 < wmx) {
+                    int k = rc + rn - r0;
+                    k = k < 64 ? k : 64;
+                    k = k < wmx - r0 ? k : wmx - r0;
+                    cnt = wave_round_counts(c, r0, k);
+                    ocnt = wave_round_counts(oc, r0, k);
+                }
+                E_.wc[w][g * 64 + lane] = cnt;
+                E_.owc[w][g * 64 + lane] = ocnt;
+            }
+            __syncthreads();
+            for (int e = threadIdx.x; e < kWaves * rn; e += kBS) {
+                const int ww = e / rn, i = e - ww * rn;
+                const int r = rc + i;
+                int64_t rb = pre_c[i], orb = opre_c[i];
+                for (int q = 0; q < ww; ++q) {
+                    rb += E_.wc[q][i];
+                    orb += E_.owc[q][i];
+                }
+                E_.wbase[ww][i] = (int32_t)rb;
+                E_.obase[ww][i] = (int32_t)orb;
+                E_.wpos[ww][i] = (r <= L) ? (int32_t)(S_l[i] + rb) : 0;
+                E_.opos[ww][i] = (r <= L) ? (int32_t)(So_l[i] + orb) : 0;
+            }
+            __syncthreads();
+            int rfull = L < bm ? L : bm;
+            rfull = rfull < rc + rn ? rfull : rc + rn;
+            int32_t *const lslot = a.log_slot + a.head_local;
+            uint32_t *const lseq = a.lseq_out + a.head_local;
+            const uint32_t hin = (uint32_t)a.head_in;
+            for (int i = 0; rc + i < rfull; ++i) {
+                const int r = rc + i;
+                const uint64_t m = __ballot(c > r);
+                const uint64_t om = __ballot(oc > r);
+                if (oc > r) {
+                    const int lp = E_.opos[w][i] + popc_lt(om);
+                    lslot[lp] = s;
+                    lseq[lp] = hin + (uint32_t)(E_.wpos[w][i] + popc_lt(m));
+                }
+            }
+            if (L >= rc && L < rc + rn) {
+                const int iL = L - rc;
+                const uint64_t m = __ballot(c > L);
+                const uint64_t om = __ballot(oc > L);
+                rankL = (int64_t)E_.wbase[w][iL] + popc_lt(m);
+                orankL = (int64_t)E_.obase[w][iL] + popc_lt(om);
+                oSL = So_l[iL];
+                if (oc > L && rankL < p) {
+                    const int lp = E_.opos[w][iL] + popc_lt(om);
+                    lslot[lp] = s;
+                    lseq[lp] = hin + (uint32_t)(E_.wpos[w][iL] + popc_lt(m));
+                }
+                if (b == 0 && threadIdx.x == 0 && AL == 0) {
+                    a.hout->new_qlen = 0;
+                    a.hout->n_local = oSL;  // every worker saturated: all own capacity used
+                }
+            }
+            if (L + 1 >= rc && L + 1 < rc + rn) {
+                const int i1 = L + 1 - rc;
+                exL1 = (int64_t)E_.wbase[w][i1] + popc_lt(__ballot(c > L + 1));
+            }
+            __syncthreads();
+        }
+        if (c > 0) {
+            int64_t n_q = c < L ? c : L;
+            if (c > L && rankL < p) n_q += 1;
+            if (own) a.free_out[ls] = raw - (int32_t)n_q;
+            int64_t np = -1;
+            if (c > L) {
+                if (rankL >= p) np = rankL - p;
+                else if (c > L + 1) np = (AL - p) + exL1;
+                if (rankL == p) {
+                    // first position of round L left without a task: both queue and own-log lengths
+                    a.hout->new_qlen = (AL - p) + exL1;
+                    a.hout->n_local = oSL + orankL;
+                }
+            }
+            if (np >= 0) {
+                a.queue_out[np] = s;  // the next queue is replicated on every rank
+                if (own) a.inq_out[ls] = 1;
+            }
+        }
+        return;
+    }
+    if (bid < a.nbq + a.nbf) {
+        // ---- own orphans (global sequence numbers, ascending)
+        const int b = bid - a.nbq;
+        const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tot);
+        int64_t o = a.fpre[b] + ex;
+        const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
+#pragma unroll
+        for (int j = 0; j < kFItems; ++j)
+            if (flags & (1u << j)) a.orphans[o++] = (int64_t)a.lseq[base + j];
+        return;
+    }
+    // ---- own evicted slots, as global ids
+    const int b = bid - a.nbq - a.nbf;
+    const int s = b * kBS + threadIdx.x;
+    const uint32_t e = (s < a.W && (a.st[s] & kStEvicted)) ? 1u : 0u;
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tot);
+    if (e) a.evicted[a.wpre[b] + ex] = a.slot_base + s;
+}
+
 // ------------------------------------------------------------ commit
 __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
     const int s = blockIdx.x * kBS + threadIdx.x;
@@ -1044,13 +1343,16 @@ void launch_slots(const TickArgs &a, Stream st) {
 }
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = a.lds_bitmap ? (size_t)((a.W + 63) / 64) * 8 : 0;
-    hipLaunchKernelGGL(k_scan, dim3(a.nbf + a.nbq), dim3(kBS), lds, st, a);
+    hipLaunchKernelGGL(k_scan, dim3((a.shard == 2 ? 0 : a.nbf) + a.nbq), dim3(kBS), a.shard == 2 ? 0 : lds, st, a);
 }
 void launch_plan(const TickArgs &a, Stream st) {
-    hipLaunchKernelGGL(k_plan, dim3(3 + a.R), dim3(kBS), 0, st, a);
+    hipLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st, a);
 }
 void launch_emit(const TickArgs &a, Stream st) {
     hipLaunchKernelGGL(k_emit, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st, a);
+}
+void launch_emit_shard(const TickArgs &a, Stream st) {
+    hipLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st, a);
 }
 void launch_commit(const CommitArgs &a, int grid, Stream st) {
     hipLaunchKernelGGL(k_commit, dim3(grid), dim3(kBS), 0, st, a);

@@ -19,13 +19,16 @@ ERRNAMES = {FB_EINVAL: "FB_EINVAL", FB_ENOMEM: "FB_ENOMEM", FB_EHIP: "FB_EHIP", 
 EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read_state", "fb_tick_launch",
            "fb_tick_wait", "fb_tick_commit", "fb_get_assignments", "fb_get_orphans", "fb_get_evicted",
            "fb_get_event_status", "fb_tick", "fb_device_view_get", "fb_timing_enable", "fb_timing_read",
-           "fb_selftest", "fb_debug_read", "fb_sync")
+           "fb_selftest", "fb_debug_read", "fb_sync", "fb_set_stream", "fb_get_local_assignments",
+           "fb_create_sharded", "fb_load_shard", "fb_read_shard_log", "fb_exchange_bytes", "fb_bind_exchange",
+           "fb_tick_continue")
 
 
 class TickResult(C.Structure):
     _fields_ = [("n_assigned", C.c_int64), ("n_orphans", C.c_int64), ("queue_len", C.c_int64),
                 ("log_head", C.c_int64), ("n_evicted", C.c_int32), ("fill_level", C.c_int32),
-                ("max_free", C.c_int32), ("reruns", C.c_int32)]
+                ("max_free", C.c_int32), ("reruns", C.c_int32), ("n_local", C.c_int64),
+                ("n_orphans_local", C.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -80,6 +83,14 @@ def load(path=LIB_PATH):
         "fb_debug_read": (C.c_int, [_P, _P, i64, C.POINTER(i64)]),
         "fb_selftest": (C.c_int, [_P, C.POINTER(i32)]),
         "fb_sync": (C.c_int, [_P]),
+        "fb_set_stream": (C.c_int, [_P, _P]),
+        "fb_get_local_assignments": (C.c_int, [_P, i64, i64, _P, _P]),
+        "fb_create_sharded": (C.c_int, [C.POINTER(_P), i32, i32, i64, i32, C.c_int, i32, i32]),
+        "fb_load_shard": (C.c_int, [_P, i32, i32, _P, _P, _P, _P, _P, i64, _P, _P, i64, i64]),
+        "fb_read_shard_log": (C.c_int, [_P, _P, C.POINTER(i64), C.POINTER(i64)]),
+        "fb_exchange_bytes": (C.c_int, [_P, i32, C.POINTER(i64)]),
+        "fb_bind_exchange": (C.c_int, [_P, _P, i64]),
+        "fb_tick_continue": (C.c_int, [_P]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)

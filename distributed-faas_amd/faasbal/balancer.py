@@ -32,15 +32,19 @@ class GpuBalancer:
     def __init__(self, max_workers, max_log, max_events=65536, device=0, lib_path=None):
         self.lib = _lib.load() if lib_path is None else _lib.load(lib_path)
         self.h = C.c_void_p()
-        rc = self.lib.fb_create(C.byref(self.h), int(max_workers), int(max_log), int(max_events), int(device))
-        if rc != 0:
-            raise FaasbalError(rc, "fb_create(max_workers=%d, max_log=%d, max_events=%d, device=%d) failed"
-                               % (max_workers, max_log, max_events, device))
+        self._create(max_workers, max_log, max_events, device)
+        self.device = int(device)
         self.max_workers = int(max_workers)
         self.max_log = int(max_log)
         self.max_events = int(max_events)
         self.n_workers = 0
         self._E = 0
+
+    def _create(self, max_workers, max_log, max_events, device):
+        rc = self.lib.fb_create(C.byref(self.h), int(max_workers), int(max_log), int(max_events), int(device))
+        if rc != 0:
+            raise FaasbalError(rc, "fb_create(max_workers=%d, max_log=%d, max_events=%d, device=%d) failed"
+                               % (max_workers, max_log, max_events, device))
 
     # ------------------------------------------------------------------ misc
     def _chk(self, rc):
@@ -79,15 +83,15 @@ class GpuBalancer:
 
     def read_state(self, with_log=True):
         W = self.n_workers
-        reg = np.zeros(max(W, 1), np.uint8)
-        free = np.zeros(max(W, 1), np.int32)
-        hb = np.zeros(max(W, 1), np.float64)
-        epoch = np.zeros(max(W, 1), np.uint32)
-        queue = np.zeros(max(W, 1), np.int32)
         qlen = C.c_int64()
         loglen = C.c_int64()
         self._chk(self.lib.fb_read_state(self.h, None, None, None, None, None, C.byref(qlen), None,
                                          C.byref(loglen)))
+        reg = np.zeros(max(W, 1), np.uint8)
+        free = np.zeros(max(W, 1), np.int32)
+        hb = np.zeros(max(W, 1), np.float64)
+        epoch = np.zeros(max(W, 1), np.uint32)
+        queue = np.zeros(max(qlen.value, 1), np.int32)
         log = np.zeros(max(loglen.value, 1), np.int32) if with_log else None
         self._chk(self.lib.fb_read_state(self.h, _p(reg), _p(free), _p(hb), _p(epoch), _p(queue),
                                          C.byref(qlen), _p(log) if with_log else None, C.byref(loglen)))
@@ -127,8 +131,16 @@ class GpuBalancer:
         self._chk(self.lib.fb_get_assignments(self.h, int(first), int(n), _p(out)))
         return out[:n]
 
+    def local_assignments(self, first=0, n=None):
+        """(task index, slot) of the tasks given to this context's workers."""
+        n = self.last["n_local"] - first if n is None else n
+        task = np.zeros(max(n, 1), np.int64)
+        slot = np.zeros(max(n, 1), np.int32)
+        self._chk(self.lib.fb_get_local_assignments(self.h, int(first), int(n), _p(task), _p(slot)))
+        return task[:n], slot[:n]
+
     def orphans(self):
-        n = self.last["n_orphans"]
+        n = self.last["n_orphans_local"]
         out = np.zeros(max(n, 1), np.int64)
         self._chk(self.lib.fb_get_orphans(self.h, int(n), _p(out)))
         return out[:n]
@@ -158,6 +170,10 @@ class GpuBalancer:
         return out
 
     # ---------------------------------------------------------------- timing
+    def set_stream(self, stream_handle):
+        """Run on another HIP stream (an int handle, e.g. torch's cuda_stream), or 0 for the own one."""
+        self._chk(self.lib.fb_set_stream(self.h, C.c_void_p(int(stream_handle)) if stream_handle else None))
+
     def sync(self):
         self._chk(self.lib.fb_sync(self.h))
 

@@ -51,6 +51,8 @@ typedef struct fb_tick_result {
     int32_t fill_level;  /* water-filling rounds completed (L)                            */
     int32_t max_free;    /* largest effective free count in the queue this tick           */
     int32_t reruns;      /* internal reruns with a wider round table                      */
+    int64_t n_local;         /* sharded: tasks dispatched to this rank's workers (else n_assigned) */
+    int64_t n_orphans_local; /* sharded: orphans from this rank's log shard (else n_orphans)       */
 } fb_tick_result;
 
 /* Device pointers of the context's state (for zero-copy consumers, e.g.
@@ -136,6 +138,41 @@ int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_to
 
 /* Synchronise the context stream (for wall-clock benchmarking). */
 int fb_sync(fb_ctx *ctx);
+
+/* Run the context's work on another HIP stream (e.g. the one a collective
+ * library uses), or on its own stream again with stream = NULL. */
+int fb_set_stream(fb_ctx *ctx, void *stream);
+
+/* One-GPU contexts: slot per task of the waited tick as (task index, slot)
+ * pairs, same content as fb_get_assignments.  Sharded contexts: only the tasks
+ * given to this rank's workers, in ascending task index. */
+int fb_get_local_assignments(fb_ctx *ctx, int64_t first, int64_t n, int64_t *task, int32_t *slot);
+
+/* ---- Sharded worker table (one process per GPU) ----
+ * Rank r owns the global slots [slot_base, slot_base + n_workers): their
+ * records, their in-flight log entries (global sequence numbers ascending) and
+ * the dispatch of tasks to them.  The LRU queue order is replicated.  A tick is
+ *   fb_tick_launch (every rank gets the same full event batch)
+ *   -> all-reduce(SUM, uint8) of the bound exchange buffer over all ranks
+ *   -> fb_tick_continue -> fb_tick_wait -> outputs -> fb_tick_commit.
+ * The whole-table result equals the one-GPU tick's: the union of the ranks'
+ * local assignments is fb_get_assignments; orphans / evicted are per rank
+ * (merge for the global lists); event status and queue are global. */
+int fb_create_sharded(fb_ctx **out, int32_t max_workers_local, int32_t n_workers_global,
+                      int64_t max_log_local, int32_t max_events, int device, int32_t rank, int32_t world);
+/* queue: global slots in LRU order; log_slot: global slot per local entry
+ * (-1 completed); log_seq: its global sequence number; log_head: global log length. */
+int fb_load_shard(fb_ctx *ctx, int32_t slot_base, int32_t n_workers, const uint8_t *registered,
+                  const int32_t *free_processes, const double *last_heartbeat, const uint32_t *epoch,
+                  const int32_t *queue, int64_t queue_len, const int32_t *log_slot, const uint32_t *log_seq,
+                  int64_t log_len, int64_t log_head);
+int fb_read_shard_log(fb_ctx *ctx, uint32_t *log_seq, int64_t *log_len, int64_t *log_head);
+/* Exchange buffer size for a tick of n_events events (n_events < 0: the maximum). */
+int fb_exchange_bytes(fb_ctx *ctx, int32_t n_events, int64_t *bytes);
+/* Device buffer (same size on every rank) the ranks all-reduce between phases. */
+int fb_bind_exchange(fb_ctx *ctx, void *device_buffer, int64_t bytes);
+/* Enqueue phase 2 of a sharded tick, after the exchange all-reduce. */
+int fb_tick_continue(fb_ctx *ctx);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,147 @@
+"""Sharded worker table (several ranks) vs the one-table oracle, on one GPU.
+
+Every rank is a separate library context (its own slot range, log shard and
+stream) in this process; the exchange all-reduce is a device-side SUM of the
+ranks' exchange tensors -- the same reduction RCCL performs across GPUs.  The
+merged outputs (assignments, orphans, evicted, reconnect flags) and the
+reassembled state must equal the oracle's bit for bit.
+"""
+import numpy as np
+import pytest
+
+from faasbal import synth
+from oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _group(st, world, log_cap, max_events=4096):
+    import torch  # noqa: F401  (loads the HIP runtime before libfaasbal)
+    from faasbal.sharded import ShardedBalancer
+
+    W = len(st["reg"])
+    bals = [ShardedBalancer(r, world, W, log_cap, max_events=max_events) for r in range(world)]
+    for b in bals:
+        b.load(st)
+    o = Oracle(W, log_cap)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    return bals, o
+
+
+def _group_tick(bals, *args):
+    import torch
+    from faasbal.sharded import merge_outputs
+
+    for b in bals:
+        b.launch(*args)
+    torch.cuda.synchronize()
+    total = bals[0].exchange().clone()
+    for b in bals[1:]:
+        total += b.exchange()  # single contributor per byte: the uint8 sum is exact
+    for b in bals:
+        b.exchange().copy_(total)
+    torch.cuda.synchronize()
+    for b in bals:
+        b.cont()
+    res = [b.wait() for b in bals]
+    for k in ("n_assigned", "n_orphans", "queue_len", "log_head", "fill_level"):
+        assert len({r[k] for r in res}) == 1, k
+    outs = []
+    for b in bals:
+        task, slot = b.local_assignments()
+        assert np.all(np.diff(task) > 0)  # ascending global order in every log shard
+        outs.append(dict(task=task, slot=slot, orphans=b.orphans(), evicted=b.evicted(), reconnect=b.event_status()))
+    for b in bals[1:]:
+        np.testing.assert_array_equal(outs[0]["reconnect"], b.event_status())
+    merged = merge_outputs(outs, res[0]["n_assigned"])
+    for b in bals:
+        b.commit()
+    return merged, res[0]
+
+
+def _cmp(bals, o, a, b, t):
+    for k in ("reconnect", "assign", "orphans", "evicted"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg="tick %d: %s" % (t, k))
+    so = o.export()
+    reg = so["reg"].astype(bool)
+    glog = np.full(len(so["log"]), -1, np.int32)
+    for bal in bals:
+        sg = bal.read_state()
+        lo, hi = bal.base, bal.base + bal.n_local
+        np.testing.assert_array_equal(sg["reg"], so["reg"][lo:hi], err_msg="tick %d reg" % t)
+        m = reg[lo:hi]
+        np.testing.assert_array_equal(sg["free"][m], so["free"][lo:hi][m], err_msg="tick %d free" % t)
+        np.testing.assert_array_equal(sg["hb"][m], so["hb"][lo:hi][m], err_msg="tick %d hb" % t)
+        np.testing.assert_array_equal(sg["queue"], so["queue"], err_msg="tick %d queue" % t)
+        assert sg["head"] == len(so["log"])
+        glog[sg["log_seq"]] = sg["log"]
+    np.testing.assert_array_equal(glog, so["log"], err_msg="tick %d log" % t)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_sharded_random_multitick(seed):
+    W = [37, 300, 1000][seed % 3]
+    world = [2, 3, 4][(seed // 3) % 3]
+    scen = synth.random_scenario(5000 + seed, W=W, n_ticks=5, max_events=[20, 200, 2000][seed % 3],
+                                 max_new=[50, 400, 3000][(seed // 3) % 3])
+    st = dict(reg=scen["init_reg"], free=scen["init_free"], hb=scen["init_hb"], epoch=scen["init_epoch"],
+              queue=scen["init_queue"], log=scen["init_log"])
+    bals, o = _group(st, world, len(st["log"]) + 40000)
+    carried = 0
+    for t, tk in enumerate(scen["ticks"]):
+        log = o.export()["log"]
+        seq = np.full(len(tk["ev_kind"]), -1, np.int64)
+        for i in np.nonzero(tk["ev_kind"] == synth.EV_RESULT)[0]:
+            mine = np.nonzero(log == tk["ev_slot"][i])[0]
+            if len(mine) and tk["ev_pick"][i] % 5 != 4:
+                seq[i] = mine[tk["ev_pick"][i] % len(mine)]
+        n = carried + tk["n_new"]
+        args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
+        a, _ = _group_tick(bals, *args)
+        b = o.tick(*args)
+        _cmp(bals, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_config3(world):
+    """BASELINE configs[2] table split over ranks: 1M tasks x 64K workers."""
+    st = synth.zipf_state(W=65536, seed=0)
+    T = 1_000_000
+    bals, o = _group(st, world, len(st["log"]) + T + len(st["log"]) + 16)
+    a, r = _group_tick(bals, 1000.0, 10.0, [], [], [], [], [], T)
+    b = o.tick(1000.0, 10.0, [], [], [], [], [], T)
+    assert r["n_orphans"] > 0
+    _cmp(bals, o, a, b, 0)
+
+
+def test_sharded_churn():
+    st = synth.zipf_state(W=65536, seed=3)
+    ticks = synth.churn_ticks(st, n_ticks=3, seed=2, tasks_per_tick=65536, join_frac=0.001, expire_frac=0.001,
+                              results_per_tick=8192)
+    bals, o = _group(st, 2, len(st["log"]) + 3 * 65536 + 200_000, max_events=20000)
+    carried = 0
+    for t, tk in enumerate(ticks):
+        log = o.export()["log"]
+        order = np.argsort(log, kind="stable")
+        sl = log[order]
+        seq = np.full(len(tk["ev_kind"]), -1, np.int64)
+        for i in np.nonzero(tk["ev_kind"] == synth.EV_RESULT)[0]:
+            s = tk["ev_slot"][i]
+            lo, hi = np.searchsorted(sl, s), np.searchsorted(sl, s, side="right")
+            if hi > lo:
+                seq[i] = order[lo + tk["ev_pick"][i] % (hi - lo)]
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
+        a, _ = _group_tick(bals, *args)
+        b = o.tick(*args)
+        _cmp(bals, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def test_sharded_world1_equals_one_gpu():
+    st = synth.zipf_state(W=4096, seed=9)
+    bals, o = _group(st, 1, len(st["log"]) * 2 + 100_000)
+    a, _ = _group_tick(bals, 1000.0, 10.0, [], [], [], [], [], 60_000)
+    b = o.tick(1000.0, 10.0, [], [], [], [], [], 60_000)
+    _cmp(bals, o, a, b, 0)
