@@ -40,6 +40,14 @@ def emit_bytes(W, Q, F, O, N, Qn_out):
     return 4 * N + 8 * Q + 8 * Q + 4 * Qn_out + 4 * F + 8 * O
 
 
+def emit_shard_bytes(Q, own_q, F_local, O_local, n_local, Qn_out):
+    """Algorithmic bytes of k_emit_shard on one rank: c8 exchange byte + queue
+    slot read + next-queue write per LRU position (1+4+4), own tasks (slot and
+    global sequence, 8 B), own c_arr read + free_processes write (8 B per own
+    queued worker), log shard re-read for orphan compaction and orphan ids."""
+    return 9 * Q + 4 * Qn_out + 8 * n_local + 8 * own_q + 4 * F_local + 8 * O_local
+
+
 def cpu_baseline(st, T, budget_s=10.0):
     """The oracle (C restatement of the reference loop, 1 core) on a bounded
     prefix of the same tick: the loop as written (O(W) purge per iteration)."""
@@ -83,79 +91,113 @@ def main():
     ap.add_argument("--tasks", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
+    ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    dev = 0
     if world > 1:
         import torch
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dev = local % max(1, torch.cuda.device_count())
+        torch.cuda.set_device(dev)
+        dist.init_process_group(args.backend, device_id=torch.device("cuda", dev) if args.backend == "nccl" else None)
 
     from faasbal import GpuBalancer, synth
 
-    W, T = args.workers, args.tasks
-    # weak scaling: every rank runs the configs[2] tick on its own shard of
-    # the pool (seeded per rank); see DESIGN.md §6 for the sharded global path.
-    st = synth.zipf_state(W=W, seed=rank)
-    cap = 2 * len(st["log"]) + T + 16
-    g = GpuBalancer(W, cap, max_events=1, device=local if world > 1 else 0)
-    g.load(st)
-    g.launch(1000.0, 10.0, n_pending=T)
+    # weak scaling: the pool grows with the GPUs.  N = 1 runs configs[2] on one
+    # table; N > 1 shards ONE global table of N x 64K workers / N x 1M tasks by
+    # worker-id range and runs the two-phase tick with the RCCL exchange
+    # all-reduce every step.
+    W, T = args.workers * world, args.tasks * world
+    st = synth.zipf_state(W=W, seed=0)
+    F = len(st["log"])
+    Q = len(st["queue"])
+    if world == 1:
+        g = GpuBalancer(W, 2 * F + T + 16, max_events=1, device=0)
+        g.load(st)
+
+        def step():
+            g.launch(1000.0, 10.0, n_pending=T)
+    else:
+        from faasbal.sharded import ShardedBalancer
+        g = ShardedBalancer(rank, world, W, 2 * F + T + 16, max_events=1, device=dev)
+        g.load(st)
+
+        def step():
+            g.launch(1000.0, 10.0, n_pending=T)
+            with torch.cuda.stream(g.stream):
+                dist.all_reduce(g.exchange())
+            g.cont()
+    step()
     res = g.wait()
     n_assigned = int(res["n_assigned"])
     O = int(res["n_orphans"])
-    F = len(st["log"])
-    Q = len(st["queue"])
 
     def barrier():
         if dist is not None:
-            import torch
             t = torch.zeros(1, device="cuda")
             dist.all_reduce(t)
             torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        g.launch(1000.0, 10.0, n_pending=T)
+        step()
     g.sync()
     # timed region: K back-to-back ticks on the device stream
     barrier()
     g.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        g.launch(1000.0, 10.0, n_pending=T)
+        step()
     g.sync()
     barrier()
     dt = time.perf_counter() - t0
     if dist is not None:
-        import torch
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     # per-kernel device time with HIP events on the balancer's stream (same K)
     g.timing_enable(True)
     for _ in range(args.steps):
-        g.launch(1000.0, 10.0, n_pending=T)
+        step()
     kt = g.timing_read()
     g.timing_enable(False)
     g.wait()
+    if world > 1:
+        # the exchange: all-reduce time per tick, measured alone on the same stream
+        xb = g.exchange()
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        with torch.cuda.stream(g.stream):
+            for _ in range(5):
+                dist.all_reduce(xb)
+            barrier()
+            ev0.record(g.stream)
+            for _ in range(args.steps):
+                dist.all_reduce(xb)
+            ev1.record(g.stream)
+        ev1.synchronize()
+        kt["exchange_allreduce"] = (ev0.elapsed_time(ev1), args.steps)
+        kt_x_bytes = xb.numel()
 
     kern = {k: (ms / n, n) for k, (ms, n) in kt.items()}
-    dom = max(kern, key=lambda k: kern[k][0])
+    dom = max((k for k in kern if k != "exchange_allreduce"), key=lambda k: kern[k][0])
     dom_ms = kern[dom][0]
-    tick_dev_ms = sum(v[0] for v in kern.values())
-    if dom == "emit":
+    tick_dev_ms = sum(v[0] for k, v in kern.items() if k != "exchange_allreduce")
+    if dom == "emit" and world == 1:
         dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]))
+    elif dom == "emit":
+        dom_bytes = emit_shard_bytes(Q, Q // world, F // world, int(res["n_orphans_local"]), int(res["n_local"]),
+                                     int(res["queue_len"]))
     else:
-        dom_bytes = tick_bytes(W, Q, F, O, n_assigned)
+        dom_bytes = tick_bytes(W // world, Q, F // world, O // world, n_assigned // world)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     B = tick_bytes(W, Q, F, O, n_assigned)
-    value = n_assigned * args.steps * world / dt
+    value = n_assigned * args.steps / dt  # whole job: the global tick's dispatches
     line = {
-        "metric": "task assignment decisions/s (1M tasks x 64K workers, Zipf loads + 5% heartbeat timeouts)",
+        "metric": "task assignments/sec + % HBM roofline, 1M tasks x 64K workers, 1/2/4/8 GPU",
         "value": value,
         "unit": "assignments/s",
         "n_gpus": world,
@@ -166,12 +208,16 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic (faasbal.synth.zipf_state, seed=rank)",
-        "config": {"workload": "configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
-                               "5%% dead -> %d orphans redistributed" % (T, W, O),
+        "data": "synthetic (faasbal.synth.zipf_state, seed=0)",
+        "config": {"workload": ("configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
+                                "5%% dead -> %d orphans redistributed" % (T, W, O)) if world == 1 else
+                               ("configs[2] per GPU, weak: one global tick of %d tasks x %d workers sharded by "
+                                "worker-id range over %d GPUs, exchange all-reduce of %d B per tick (RCCL), "
+                                "%d orphans redistributed" % (T, W, world, kt_x_bytes, O)),
                    "tasks_per_tick": T, "workers": W, "in_flight": F, "queue": Q,
                    "assigned_per_tick": n_assigned, "evicted": int(res["n_evicted"]),
-                   "fill_level": int(res["fill_level"]), "parallelism": "dp%d" % world},
+                   "fill_level": int(res["fill_level"]),
+                   "parallelism": "dp1" if world == 1 else "worker-table shards x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes": dom_bytes,
                      "kernel_avg_ms": dom_ms},
@@ -179,7 +225,7 @@ def main():
                  "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,
                  "kernels_avg_ms": {k: v[0] for k, v in kern.items()}},
     }
-    if rank == 0 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(st, T, args.cpu_budget)
     if rank == 0:
         print(json.dumps(line), flush=True)
