@@ -196,6 +196,15 @@ def main():
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     B = tick_bytes(W, Q, F, O, n_assigned)
     value = n_assigned * args.steps / dt  # whole job: the global tick's dispatches
+    # HBM bytes per launch of the dominant kernel from the committed PMC passes of
+    # this same command (tools_profile.sh -> tools/prof_summary.py), when they match
+    traffic, traffic_src = None, None
+    tp = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tp):
+        tj = json.load(open(tp))
+        if (tj.get("workers"), tj.get("tasks_per_tick"), tj.get("n_gpus")) == (W, T, world) and dom in tj["kernels"]:
+            traffic = tj["kernels"][dom]["hbm_bytes"]
+            traffic_src = "profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch)" % tj["tag"]
     line = {
         "metric": "task assignments/sec + % HBM roofline, 1M tasks x 64K workers, 1/2/4/8 GPU",
         "value": value,
@@ -219,7 +228,8 @@ def main():
                    "fill_level": int(res["fill_level"]),
                    "parallelism": "dp1" if world == 1 else "worker-table shards x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None, "algorithmic_bytes": dom_bytes,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes": dom_bytes,
                      "kernel_avg_ms": dom_ms},
         "tick": {"algorithmic_bytes": B, "device_ms": tick_dev_ms,
                  "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,

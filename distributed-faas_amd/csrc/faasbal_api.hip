@@ -176,22 +176,25 @@ hipEvent_t pool_event(fb_ctx *c) {
     return e;
 }
 
+// Per-kernel device time: the events ride in the dispatch packets of the timed
+// launches (start of the first, end of the last), so they bracket kernel
+// execution only -- the same interval rocprofv3's kernel trace reports.
 struct Timer {
     fb_ctx *c;
     const char *name;
-    hipEvent_t a = nullptr;
+    hipEvent_t a = nullptr, b = nullptr;
     Timer(fb_ctx *c_, const char *n) : c(c_), name(n) {
         if (c->timing) {
             a = pool_event(c);
-            hipEventRecord(a, c->stream);
+            b = pool_event(c);
         }
     }
+    Stream st() const { return Stream(c->stream, a, b); }
+    Stream first() const { return Stream(c->stream, a, nullptr); }
+    Stream mid() const { return Stream(c->stream); }
+    Stream last() const { return Stream(c->stream, nullptr, b); }
     ~Timer() {
-        if (c->timing) {
-            hipEvent_t b = pool_event(c);
-            hipEventRecord(b, c->stream);
-            c->tl.push_back({name, a, b});
-        }
+        if (c->timing) c->tl.push_back({name, a, b});
     }
 };
 
@@ -287,9 +290,9 @@ int enqueue_tick(fb_ctx *c) {
         for (int ps = 0; ps < passes; ++ps) {
             Timer t(c, "rs_sort");
             uint32_t *kout = c->keys[ps & 1], *vout = c->vals[ps & 1];
-            launch_rs_hist(kin, E, 8 * ps, c->rs_hist, nb, c->stream);
-            launch_scan_1wg(c->rs_hist, 256 * nb, c->stream);
-            launch_rs_scatter(kin, vin, kout, vout, E, 8 * ps, c->rs_hist, nb, ps == 0 ? 1 : 0, c->stream);
+            launch_rs_hist(kin, E, 8 * ps, c->rs_hist, nb, t.first());
+            launch_scan_1wg(c->rs_hist, 256 * nb, t.mid());
+            launch_rs_scatter(kin, vin, kout, vout, E, 8 * ps, c->rs_hist, nb, ps == 0 ? 1 : 0, t.last());
             kin = kout;
             vin = vout;
         }
@@ -325,7 +328,7 @@ int enqueue_tick(fb_ctx *c) {
         a.front_list = front;
         a.back_list = back;
         Timer t(c, "ev_apply");
-        launch_ev_apply(a, c->stream);
+        launch_ev_apply(a, t.st());
     }
     TickArgs a{};
     a.W = W;
@@ -407,10 +410,10 @@ int enqueue_tick(fb_ctx *c) {
         // phase 1: own slots' purge, orphan flags and free counts into the exchange buffer
         {
             Timer t(c, "slots");
-            launch_slots(a, c->stream);
+            launch_slots(a, t.st());
         }
         Timer t(c, "scan");
-        launch_scan(a, c->stream);
+        launch_scan(a, t.st());
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
@@ -418,32 +421,32 @@ int enqueue_tick(fb_ctx *c) {
         if (R > kRFused) return fail(c, FB_ERANGE, "sharded tick: free counts need %d rounds (limit %d)", R, kRFused);
         {
             Timer t(c, "scan");
-            launch_scan(a, c->stream);
+            launch_scan(a, t.st());
         }
         {
             Timer t(c, "plan");
-            launch_plan(a, c->stream);
+            launch_plan(a, t.st());
         }
         Timer t(c, "emit");
-        launch_emit_shard(a, c->stream);
+        launch_emit_shard(a, t.st());
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
     {
         Timer t(c, "slots");
-        launch_slots(a, c->stream);
+        launch_slots(a, t.st());
     }
     {
         Timer t(c, "scan");
-        launch_scan(a, c->stream);
+        launch_scan(a, t.st());
     }
     if (!a.fused) {
         Timer t(c, "plan");
-        launch_plan(a, c->stream);
+        launch_plan(a, t.st());
     }
     {
         Timer t(c, "emit");
-        launch_emit(a, c->stream);
+        launch_emit(a, t.st());
     }
     HIPCHK(c, hipGetLastError());
     return FB_OK;
@@ -880,7 +883,7 @@ int fb_tick_commit(fb_ctx *c) {
         a.hb = c->hb;
         a.epoch = c->epoch;
         Timer t(c, "commit");
-        launch_commit(a, (int)cdiv(c->W, kBS), c->stream);
+        launch_commit(a, (int)cdiv(c->W, kBS), t.st());
         HIPCHK(c, hipGetLastError());
     }
     c->cur = 1 - c->cur;

@@ -148,7 +148,15 @@ struct CommitArgs {
 };
 
 // Host-side launchers (defined in faasbal_kernels.hip; grid sizes are the caller's).
-using Stream = hipStream_t;
+// A launch target: the stream, plus optional dispatch-packet timing events
+// (hipExtLaunchKernel records them at the kernel's own start and end, the
+// interval rocprofv3's kernel trace reports).
+struct Stream {
+    hipStream_t s;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    Stream(hipStream_t s_) : s(s_) {}
+    Stream(hipStream_t s_, hipEvent_t a, hipEvent_t b) : s(s_), e0(a), e1(b) {}
+};
 void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, Stream st);
 void launch_scan_1wg(uint32_t *a, int n, Stream st);
 void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,

@@ -14,6 +14,7 @@
 // Water-filling: c = max(free,1) for live queued workers,
 // round r serves A_r = [q : c_q > r] in queue order, S(r) = sum_q min(c_q, r),
 // task k of round r goes to A_r[k - S(r)].  rank_r(q) = qpre[r][blk] + in-block rank.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -1322,39 +1323,39 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
 namespace fb {
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, Stream st) {
-    hipLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kBS), 0, st, keys, n, shift, hist, nblk);
+    hipExtLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kBS), 0, st.s, st.e0, st.e1, 0, keys, n, shift, hist, nblk);
 }
 void launch_scan_1wg(uint32_t *a, int n, Stream st) {
-    hipLaunchKernelGGL(k_scan_1wg, dim3(1), dim3(kBS), 0, st, a, n);
+    hipExtLaunchKernelGGL(k_scan_1wg, dim3(1), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a, n);
 }
 void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,
                        int shift, const uint32_t *hist, int nblk, int identity_vals, Stream st) {
-    hipLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kBS), 0, st, kin, vin, kout, vout, n, shift, hist, nblk,
+    hipExtLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kBS), 0, st.s, st.e0, st.e1, 0, kin, vin, kout, vout, n, shift, hist, nblk,
                        identity_vals);
 }
 void launch_ev_apply(const EvArgs &a, Stream st) {
-    hipLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st, a);
+    hipExtLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
-    hipLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st, err, seed);
+    hipExtLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st.s, st.e0, st.e1, 0, err, seed);
 }
 void launch_slots(const TickArgs &a, Stream st) {
-    hipLaunchKernelGGL(k_slots, dim3(a.nbw), dim3(kBS), 0, st, a);
+    hipExtLaunchKernelGGL(k_slots, dim3(a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = a.lds_bitmap ? (size_t)((a.W + 63) / 64) * 8 : 0;
-    hipLaunchKernelGGL(k_scan, dim3((a.shard == 2 ? 0 : a.nbf) + a.nbq), dim3(kBS), a.shard == 2 ? 0 : lds, st, a);
+    hipExtLaunchKernelGGL(k_scan, dim3((a.shard == 2 ? 0 : a.nbf) + a.nbq), dim3(kBS), a.shard == 2 ? 0 : lds, st.s, st.e0, st.e1, 0, a);
 }
 void launch_plan(const TickArgs &a, Stream st) {
-    hipLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st, a);
+    hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_emit(const TickArgs &a, Stream st) {
-    hipLaunchKernelGGL(k_emit, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st, a);
+    hipExtLaunchKernelGGL(k_emit, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
-    hipLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st, a);
+    hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_commit(const CommitArgs &a, int grid, Stream st) {
-    hipLaunchKernelGGL(k_commit, dim3(grid), dim3(kBS), 0, st, a);
+    hipExtLaunchKernelGGL(k_commit, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 }  // namespace fb
