@@ -7,6 +7,7 @@ task_dispatcher.py:324-419) as CDNA4 HIP kernels behind a C ABI
 """
 from ._lib import FaasbalError  # noqa: F401
 from .balancer import GpuBalancer  # noqa: F401
+from .dispatcher import GpuPushDispatcher  # noqa: F401
 from . import synth  # noqa: F401
 
 EV_REGISTER, EV_RECONNECT, EV_HEARTBEAT, EV_RESULT, EV_OTHER = 0, 1, 2, 3, 4

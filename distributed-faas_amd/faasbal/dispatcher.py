@@ -1,0 +1,343 @@
+"""GpuPushDispatcher: drop-in for the reference's heartbeat ``PushDispatcher``.
+
+Same constructor signature (``task_dispatcher.py:190``), same ZMQ ROUTER socket
+and message flow, same Redis records and pub/sub channel, same wire codec.
+What changes is the balancing state: the ``self.workers`` dict of
+``PushWorker`` records (``:194, :203-212``), the ``free_workers`` LRU
+OrderedDict (``:327``), ``purge_workers`` (``:241-249``) and the dispatch block
+(``:393-419``) live on the GPU, in ``GpuBalancer`` (``libfaasbal.so`` through
+ctypes).  The host loop works per *tick* instead of per message:
+
+1. drain every inbound ZMQ message (``poll(0)`` until empty, ``:330-345``),
+   stamping each with the clock at receipt, and map the worker identity
+   (``bytes``) to a dense table slot;
+2. drain every pending pub/sub task id (``get_message``, ``:394``);
+3. one GPU tick: the messages' state updates (``:347-387``), the purge at
+   ``now`` (``:390``), redistribution of dead workers' in-flight tasks
+   (build-defined; the reference drops them, README.md:263-264) and the LRU
+   dispatch of orphans then pending tasks;
+4. the host I/O the reference does per message, in the same order: a
+   ``reconnect`` request to unknown senders (``:356-358``), ``HSET`` of results
+   from known workers (``:381``), then per dispatched task ``HGET`` x2
+   (``query_redis``, ``:48-52``), ``send_message`` (``:410``) and
+   ``HSET status=RUNNING`` (``:413``).
+
+A tick is a legal arrival order for the reference loop (messages first, then
+tasks): the assignments are bit-identical to the reference's on it
+(tests/test_dispatcher.py replays the reference-captured goldens through this
+class with fake sockets and Redis).
+
+There is no CPU path: the balancer is the HIP library, and constructing this
+class without a GPU fails loudly.
+"""
+from __future__ import annotations
+
+import collections
+import time
+
+import numpy as np
+
+from . import codec
+from ._lib import FaasbalError
+from .balancer import GpuBalancer
+
+EV_REGISTER, EV_RECONNECT, EV_HEARTBEAT, EV_RESULT, EV_OTHER = 0, 1, 2, 3, 4
+_KINDS = {"register": EV_REGISTER, "reconnect": EV_RECONNECT, "heartbeat": EV_HEARTBEAT, "result": EV_RESULT}
+_I32 = (-(1 << 31), (1 << 31) - 1)
+
+
+class WorkerView:
+    """Read-only stand-in for ``PushDispatcher.PushWorker`` (``:203-212``)."""
+
+    __slots__ = ("free_processes", "last_heartbeat", "time_to_expire")
+
+    def __init__(self, free_processes, last_heartbeat, time_to_expire):
+        self.free_processes = int(free_processes)
+        self.last_heartbeat = float(last_heartbeat)
+        self.time_to_expire = time_to_expire
+
+    def is_alive(self, now=None):
+        now = time.time() if now is None else now
+        return not (now - self.last_heartbeat > self.time_to_expire)
+
+
+class GpuPushDispatcher:
+    """Heartbeat push dispatcher whose balancing state lives on an MI355X.
+
+    ``ip_address``, ``port``, ``time_to_expire``: as the reference
+    (``task_dispatcher.py:190``; ``TIME_TO_EXPIRE`` of ``config.ini``).
+    Keyword-only arguments size the device table and allow the transport objects
+    to be injected (the defaults build exactly what the reference builds:
+    ``redis.Redis(host='localhost', port=6379, db=1)`` subscribed to ``tasks``,
+    and a bound ZMQ ROUTER with a ``zmq.Poller``).
+    """
+
+    def __init__(self, ip_address, port, time_to_expire=10, *, max_workers=65536, max_inflight=1 << 24,
+                 max_events=65536, device=0, redis_client=None, subscriber=None, socket=None, poller=None,
+                 clock=time.time, tasks_channel="tasks"):
+        self.port = port
+        self.ip_address = ip_address
+        self.time_to_expire = time_to_expire
+        self.clock = clock
+        # TaskDispatcher.__init__ (task_dispatcher.py:30-36)
+        if redis_client is None:
+            import redis  # the reference's client; only needed when none is injected
+            redis_client = redis.Redis(host="localhost", port=6379, db=1)
+        self.redis_client = redis_client
+        if subscriber is None:
+            subscriber = self.redis_client.pubsub()
+            subscriber.subscribe(tasks_channel)
+        self.subscriber = subscriber
+        # PushDispatcher.__init__ (:196-201)
+        if socket is None:
+            self.bind_socket()
+        else:
+            self.socket = socket
+        if poller is None:
+            import zmq
+            poller = zmq.Poller()
+            poller.register(self.socket, zmq.POLLIN)
+        self.poller = poller
+        # device table: max_workers slots, all empty
+        self.max_workers = int(max_workers)
+        self.max_events = int(max_events)
+        self.max_inflight = int(max_inflight)
+        self.balancer = GpuBalancer(self.max_workers, self.max_inflight, max_events=self.max_events, device=device)
+        self._reset_host()
+        W = self.max_workers
+        self.balancer.load_state(np.zeros(W, np.uint8), np.zeros(W, np.int32), np.zeros(W, np.float64))
+        self.ticks = 0
+        self.compactions = 0
+
+    def _reset_host(self):
+        self.slot_of = {}                              # ZMQ identity -> slot
+        self.identity = [None] * self.max_workers      # slot -> ZMQ identity
+        self._free_slots = []                          # slots released by evictions (reused LIFO)
+        self._next_slot = 0
+        self.inflight = {}                             # log sequence -> (task_id, slot)
+        self.task_seq = {}                             # task_id -> log sequence while in flight
+        self.pending = collections.deque()             # task ids not yet dispatched (orphans first)
+        self.head = 0                                  # in-flight log length
+        self._last_ts = -np.inf
+
+    # ------------------------------------------------ reference socket / Redis API
+    def bind_socket(self):
+        """Create and bind the ROUTER socket (``task_dispatcher.py:215-219``)."""
+        import zmq
+        self.socket = zmq.Context().socket(zmq.ROUTER)
+        self.socket.bind(f"tcp://{self.ip_address}:{self.port}")
+
+    def send_message(self, worker_id: bytes, message: object):
+        """``:221-230``: dill+base64 payload to the worker identified by ``worker_id``."""
+        self.socket.send_multipart([worker_id, codec.serialize(message).encode("utf-8")])
+
+    def receive_message(self):
+        """``:232-239``: (identity, deserialized message)."""
+        worker, message = self.socket.recv_multipart()
+        return worker, codec.deserialize(message.decode("utf-8"))
+
+    def query_redis(self, message):
+        """``TaskDispatcher.query_redis`` (``:38-52``)."""
+        task_id = message["data"].decode("utf-8")
+        fn_payload = self.redis_client.hget(task_id, "fn_payload")
+        param_payload = self.redis_client.hget(task_id, "param_payload")
+        return task_id, fn_payload.decode("utf-8"), param_payload.decode("utf-8")
+
+    # ------------------------------------------------------------- slot mapping
+    def _slot(self, worker_id):
+        s = self.slot_of.get(worker_id)
+        if s is not None:
+            return s
+        if self._free_slots:
+            s = self._free_slots.pop()
+        elif self._next_slot < self.max_workers:
+            s = self._next_slot
+            self._next_slot += 1
+        else:
+            raise FaasbalError(-1, "worker table full: %d slots (raise max_workers)" % self.max_workers)
+        self.slot_of[worker_id] = s
+        self.identity[s] = worker_id
+        return s
+
+    def _release(self, s):
+        wid = self.identity[s]
+        if wid is not None:
+            del self.slot_of[wid]
+            self.identity[s] = None
+            self._free_slots.append(int(s))
+
+    def _stamp(self):
+        t = float(self.clock())
+        if t < self._last_ts:  # the wall clock stepped back: keep the tick's stamps ordered
+            t = self._last_ts
+        self._last_ts = t
+        return t
+
+    # --------------------------------------------------------------------- ticks
+    def _inbound_ready(self):
+        return self.socket in dict(self.poller.poll(0))
+
+    def _drain_inbound(self):
+        msgs = []
+        while len(msgs) < self.max_events and self._inbound_ready():
+            worker_id, message = self.receive_message()
+            msgs.append((worker_id, message, self._stamp()))
+        return msgs
+
+    def _drain_tasks(self):
+        while True:
+            m = self.subscriber.get_message()
+            if m is None:
+                break
+            if m["type"] == "message":
+                d = m["data"]
+                self.pending.append(d.decode("utf-8") if isinstance(d, (bytes, bytearray)) else str(d))
+
+    def tick(self):
+        """One tick of the heartbeat loop; returns the balancer's tick result dict."""
+        msgs = self._drain_inbound()
+        self._drain_tasks()
+        return self._run(msgs)
+
+    def _run(self, msgs):
+        # room for every dispatch this tick can make (orphans + pending) before sequence numbers are taken
+        if self.head + len(self.pending) + len(self.inflight) > self.max_inflight:
+            self.compact_log()
+        now = self._stamp()
+        E = len(msgs)
+        kind = np.empty(E, np.uint8)
+        slot = np.empty(E, np.int32)
+        val = np.zeros(E, np.int32)
+        ts = np.empty(E, np.float64)
+        seq = np.full(E, -1, np.int64)
+        for i, (wid, m, t) in enumerate(msgs):
+            typ = m.get("type") if isinstance(m, dict) else None
+            k = _KINDS.get(typ, EV_OTHER)
+            kind[i] = k
+            slot[i] = self._slot(wid)
+            ts[i] = t
+            if k == EV_REGISTER or k == EV_RECONNECT:
+                v = int(m["data"]["num_processes" if k == EV_REGISTER else "free_processes"])
+                if not (_I32[0] <= v <= _I32[1]):
+                    raise FaasbalError(-1, "process count %d does not fit int32" % v)
+                val[i] = v
+            elif k == EV_RESULT:
+                seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
+        out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
+                                 n_pending=len(self.pending))
+        res = out["result"]
+        # ---- per-message replies, in arrival order (:356-358, :374-387)
+        status = out["reconnect"]
+        for i, (wid, m, _) in enumerate(msgs):
+            if status[i]:
+                self.send_message(wid, {"type": "reconnect"})
+            elif kind[i] == EV_RESULT:
+                data = m["data"]
+                self.redis_client.hset(data["task_id"], mapping={"status": data["status"], "result": data["result"]})
+                q = int(seq[i])
+                if q >= 0 and self.inflight.get(q, (None, -1))[1] == slot[i]:
+                    tid, _ = self.inflight.pop(q)
+                    self.task_seq.pop(tid, None)
+        # ---- redistribution: orphans (ascending old sequence) go first
+        orphan_tids = []
+        for q in out["orphans"]:
+            tid, _ = self.inflight.pop(int(q))
+            self.task_seq.pop(tid, None)
+            orphan_tids.append(tid)
+        if orphan_tids:
+            self.pending.extendleft(reversed(orphan_tids))
+        # ---- dispatch (:393-419): task k -> slot assign[k], log sequence base + k
+        assign = out["assign"]
+        n = int(res["n_assigned"])
+        base = int(res["log_head"]) - n
+        for k in range(n):
+            tid = self.pending.popleft()
+            s = int(assign[k])
+            task_id, fn_payload, param_payload = self.query_redis({"data": tid.encode("utf-8")})
+            self.send_message(self.identity[s], {"type": "task", "data": {
+                "task_id": task_id, "fn_payload": fn_payload, "param_payload": param_payload}})
+            self.redis_client.hset(task_id, mapping={"status": "RUNNING"})
+            self.inflight[base + k] = (tid, s)
+            self.task_seq[tid] = base + k
+        self.head = int(res["log_head"])
+        # ---- evicted records: their identities become unknown (:246-249)
+        for s in out["evicted"]:
+            self._release(int(s))
+        self.ticks += 1
+        return res
+
+    def start_heartbeat(self, max_ticks=None):
+        """The dispatcher loop (``task_dispatcher.py:324-419``), one tick per pass."""
+        while max_ticks is None or self.ticks < max_ticks:
+            self.tick()
+
+    def purge_workers(self, free_workers=None):
+        """``:241-249`` on its own: a tick at the current clock with no new messages
+        or tasks.  The dead workers' in-flight tasks are redistributed (and already
+        pending tasks dispatched) exactly as in a full tick."""
+        return self._run([])
+
+    # ------------------------------------------------------- state / inspection
+    @property
+    def workers(self):
+        """``self.workers`` of the reference: identity -> PushWorker-like view (device read-back)."""
+        st = self.balancer.read_state(with_log=False)
+        return {wid: WorkerView(st["free"][s], st["hb"][s], self.time_to_expire)
+                for wid, s in self.slot_of.items() if st["reg"][s]}
+
+    @property
+    def free_workers(self):
+        """The LRU queue of the reference (``:327``) as a list of identities, front first."""
+        st = self.balancer.read_state(with_log=False)
+        return [self.identity[s] for s in st["queue"]]
+
+    def compact_log(self):
+        """Renumber the in-flight log densely (completed and redistributed entries
+        dropped); epochs are remapped so every registration keeps exactly its own
+        in-flight entries.  Host O(F), called only when the log would overflow."""
+        st = self.balancer.read_state(with_log=True)
+        keep = np.asarray(sorted(self.inflight), np.int64)
+        log = np.asarray([self.inflight[q][1] for q in keep], np.int32)
+        epoch = np.searchsorted(keep, st["epoch"].astype(np.int64), side="left").astype(np.uint32)
+        self.balancer.load_state(st["reg"], st["free"], st["hb"], epoch, st["queue"], log)
+        remap = {int(q): i for i, q in enumerate(keep)}
+        self.inflight = {remap[q]: v for q, v in self.inflight.items()}
+        self.task_seq = {tid: remap[q] for tid, q in self.task_seq.items()}
+        self.head = len(keep)
+        self.compactions += 1
+
+    def snapshot(self):
+        """Host + device state (checkpoint; the reference keeps none)."""
+        st = self.balancer.read_state(with_log=True)
+        st.update(identity=list(self.identity), inflight=dict(self.inflight), pending=list(self.pending),
+                  free_slots=list(self._free_slots), next_slot=self._next_slot)
+        return st
+
+    def restore(self, st):
+        """Install a snapshot (or a hand-built state: reg/free/hb/epoch/queue/log plus
+        identity[slot] and inflight{seq: (task_id, slot)})."""
+        W = len(st["reg"])
+        if W > self.max_workers:
+            raise FaasbalError(-1, "snapshot has %d slots, table holds %d" % (W, self.max_workers))
+        pad = self.max_workers - W
+        reg = np.concatenate([np.asarray(st["reg"], np.uint8), np.zeros(pad, np.uint8)])
+        free = np.concatenate([np.asarray(st["free"], np.int32), np.zeros(pad, np.int32)])
+        hb = np.concatenate([np.asarray(st["hb"], np.float64), np.zeros(pad, np.float64)])
+        ep = st.get("epoch")
+        ep = np.zeros(W, np.uint32) if ep is None else np.asarray(ep, np.uint32)
+        epoch = np.concatenate([ep, np.zeros(pad, np.uint32)])
+        self.balancer.load_state(reg, free, hb, epoch, st["queue"], st["log"])
+        self._reset_host()
+        ident = list(st["identity"]) + [None] * (self.max_workers - len(st["identity"]))
+        for s, wid in enumerate(ident):
+            if wid is not None:
+                self.slot_of[wid] = s
+                self.identity[s] = wid
+        self._next_slot = int(st.get("next_slot", max((s + 1 for s, w in enumerate(ident) if w is not None),
+                                                      default=0)))
+        used = set(self.slot_of.values())
+        self._free_slots = list(st.get("free_slots", [s for s in range(self._next_slot) if s not in used][::-1]))
+        self.inflight = {int(q): (tid, int(s)) for q, (tid, s) in st.get("inflight", {}).items()}
+        self.task_seq = {tid: q for q, (tid, _) in self.inflight.items()}
+        self.pending = collections.deque(st.get("pending", ()))
+        self.head = len(st["log"])

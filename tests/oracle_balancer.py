@@ -1,0 +1,30 @@
+"""TEST DOUBLE: the oracle (oracle/push_oracle.c) behind GpuBalancer's tick API.
+
+Lets the CPU suite exercise GpuPushDispatcher's host logic (identity -> slot
+mapping, message decoding, reply/Redis ordering, orphan bookkeeping, log
+compaction) without a GPU.  Never imported by the product package; the GPU
+suite runs the same tests against the real HIP library.
+"""
+import numpy as np
+
+from oracle import Oracle
+
+
+class OracleBalancer:
+    def __init__(self, max_workers, max_log, max_events=0, device=0):
+        self.o = Oracle(max_workers, max_log)
+
+    def load_state(self, reg, free, hb, epoch=None, queue=(), log=()):
+        epoch = np.zeros(len(reg), np.uint32) if epoch is None else epoch
+        self.o.load(reg, free, hb, epoch, queue, log)
+
+    def read_state(self, with_log=True):
+        return self.o.export()
+
+    def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0):
+        if ev_seq is None:
+            ev_seq = np.full(len(ev_kind), -1, np.int64)
+        out = self.o.tick(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
+        out["result"] = dict(n_assigned=len(out["assign"]), n_orphans=len(out["orphans"]),
+                             log_head=self.o.export_head())
+        return out

@@ -1,0 +1,208 @@
+"""GpuPushDispatcher end to end: the reference-captured golden ticks replayed as
+real ZMQ-style messages (dill+base64 frames) through fake socket / poller /
+pub-sub / Redis objects.  Checks, per tick, every message the dispatcher sends
+(``reconnect`` replies, then ``task`` messages with their task ids and target
+identities), every Redis write, the LRU queue (as identities) and the worker
+records -- against the expected outputs the reference loop produced
+(tests/golden/*.npz, captured by tests/golden/make_golden.py)."""
+import collections
+import glob
+import os
+
+import numpy as np
+import pytest
+
+from faasbal import codec
+
+GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+KIND_MSG = {0: "register", 1: "reconnect", 2: "heartbeat", 3: "result", 4: "ready"}
+
+
+def wid(s):
+    return b"w%06d" % int(s)
+
+
+class FakeEnv:
+    """ROUTER socket + poller + pub/sub + Redis client + clock, all in memory."""
+
+    def __init__(self):
+        self.inbound = collections.deque()  # (identity, frame bytes, ts)
+        self.tasks = collections.deque()
+        self.sent = []
+        self.hsets = []
+        self.now = 0.0
+        self.t = 0.0
+        self.sock = self
+        self.redis = self
+        self.sub = self
+
+    # poller
+    def poll(self, timeout=None):
+        if self.inbound:
+            return [(self, 1)]
+        self.t = self.now  # inbound drained: the loop's clock moves to the tick's `now`
+        return []
+
+    # socket
+    def recv_multipart(self):
+        w, frame, ts = self.inbound.popleft()
+        self.t = ts
+        return [w, frame]
+
+    def send_multipart(self, parts):
+        self.sent.append((parts[0], codec.deserialize(parts[1].decode("utf-8"))))
+
+    # pub/sub
+    def get_message(self):
+        if not self.tasks:
+            return None
+        return {"type": "message", "data": self.tasks.popleft().encode()}
+
+    # redis
+    def hget(self, key, field):
+        return ("%s:%s" % (field, key)).encode()
+
+    def hset(self, key, mapping=None):
+        self.hsets.append((key, dict(mapping)))
+
+    def clock(self):
+        return self.t
+
+
+def test_codec_matches_reference_format():
+    msg = {"type": "result", "data": {"task_id": "t1", "status": "COMPLETED", "result": "x"}}
+    s = codec.serialize(msg)
+    assert isinstance(s, str) and s.endswith("\n")  # codecs base64 keeps line breaks
+    assert codec.deserialize(s) == msg
+
+
+@pytest.fixture(params=[pytest.param("gpu", marks=pytest.mark.gpu), "host"])
+def dispatcher_cls(request, monkeypatch):
+    """The real dispatcher on the GPU; on the CPU the same host logic over the
+    oracle test double (tests/oracle_balancer.py) in place of libfaasbal."""
+    import faasbal.dispatcher as D
+    if request.param == "host":
+        from oracle_balancer import OracleBalancer
+        monkeypatch.setattr(D, "GpuBalancer", OracleBalancer)
+    return D.GpuPushDispatcher
+
+
+@pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
+def test_dispatcher_replays_reference(path, dispatcher_cls):
+    GpuPushDispatcher = dispatcher_cls
+    z = np.load(path)
+    W = int(z["W"])
+    T = int(z["n_ticks"])
+    max_e = max(1, int(np.diff(z["ev_off"]).max(initial=0)))
+    env = FakeEnv()
+    d = GpuPushDispatcher("127.0.0.1", 0, float(z["tte"]), max_workers=2 * W + max_e, max_events=max_e + 1,
+                          max_inflight=len(z["init_log"]) + len(z["exp_assign"]) + 64,
+                          redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+    reg0 = z["init_reg"].astype(bool)
+    # test-side model of the in-flight records (golden sequence numbering)
+    seq_tid, seq_slot, inflight = {}, {}, set()
+    for q, s in enumerate(z["init_log"]):
+        seq_tid[q] = "init%d" % q
+        seq_slot[q] = int(s)
+        if s >= 0 and reg0[s] and z["init_epoch"][s] == 0:
+            inflight.add(q)
+    d.restore(dict(reg=z["init_reg"], free=z["init_free"], hb=z["init_hb"], epoch=z["init_epoch"],
+                   queue=z["init_queue"], log=z["init_log"],
+                   identity=[wid(s) if reg0[s] else None for s in range(W)],
+                   inflight={q: (seq_tid[q], seq_slot[q]) for q in inflight}))
+    head = len(z["init_log"])
+    carried = []
+    for t in range(T):
+        e0, e1 = int(z["ev_off"][t]), int(z["ev_off"][t + 1])
+        rec = z["exp_reconnect"][e0:e1]
+        exp_sent, exp_hset = [], []
+        for i in range(e0, e1):
+            k, s, v, ts = int(z["ev_kind"][i]), int(z["ev_slot"][i]), int(z["ev_val"][i]), float(z["ev_ts"][i])
+            m = {"type": KIND_MSG[k]}
+            if k == 0:
+                m["data"] = {"num_processes": v}
+            elif k == 1:
+                m["data"] = {"free_processes": v}
+            elif k == 3:
+                q = int(z["ev_seq"][i])
+                live = q >= 0 and q in inflight and seq_slot[q] == s
+                tid = seq_tid[q] if live else "stale-%d-%d" % (t, i)
+                m["data"] = {"task_id": tid, "status": "COMPLETED", "result": "r%d" % i}
+                if not rec[i - e0]:
+                    exp_hset.append((tid, {"status": "COMPLETED", "result": "r%d" % i}))
+                    if live:
+                        inflight.discard(q)
+            env.inbound.append((wid(s), codec.serialize(m).encode("utf-8"), ts))
+            if rec[i - e0]:
+                exp_sent.append((wid(s), {"type": "reconnect"}))
+        new = ["t%d_%d" % (t, j) for j in range(int(z["n_new"][t]))]
+        env.tasks.extend(new)
+        env.now = float(z["now"][t])
+        a0, a1 = int(z["exp_assign_off"][t]), int(z["exp_assign_off"][t + 1])
+        o0, o1 = int(z["exp_orphan_off"][t]), int(z["exp_orphan_off"][t + 1])
+        orph = [int(q) for q in z["exp_orphan"][o0:o1]]
+        for q in orph:
+            inflight.discard(q)
+        pending = [seq_tid[q] for q in orph] + carried + new
+        assign = z["exp_assign"][a0:a1]
+        for k, s in enumerate(assign):
+            tid = pending[k]
+            exp_sent.append((wid(s), {"type": "task", "data": {"task_id": tid, "fn_payload": "fn_payload:" + tid,
+                                                               "param_payload": "param_payload:" + tid}}))
+            exp_hset.append((tid, {"status": "RUNNING"}))
+            seq_tid[head + k] = tid
+            seq_slot[head + k] = int(s)
+            inflight.add(head + k)
+        head += len(assign)
+        carried = pending[len(assign):]
+        env.sent.clear()
+        env.hsets.clear()
+        d.tick()
+        assert env.sent == exp_sent, "tick %d: sent messages differ" % t
+        assert env.hsets == exp_hset, "tick %d: redis writes differ" % t
+        assert list(d.pending) == carried, "tick %d: pending tasks differ" % t
+        q0, q1 = int(z["exp_post_queue_off"][t]), int(z["exp_post_queue_off"][t + 1])
+        assert d.free_workers == [wid(s) for s in z["exp_post_queue"][q0:q1]], "tick %d: LRU queue" % t
+        workers = d.workers
+        exp_reg = np.nonzero(z["exp_post_reg"][t])[0]
+        assert sorted(workers) == sorted(wid(s) for s in exp_reg), "tick %d: registered workers" % t
+        for s in exp_reg:
+            w = workers[wid(s)]
+            assert w.free_processes == int(z["exp_post_free"][t][s]), "tick %d slot %d free" % (t, s)
+            assert w.last_heartbeat == float(z["exp_post_hb"][t][s]), "tick %d slot %d hb" % (t, s)
+
+
+def test_dispatcher_log_compaction_keeps_results(dispatcher_cls):
+    """A tiny in-flight log forces compact_log() every few ticks; assignments must
+    still equal a run with a large log."""
+    GpuPushDispatcher = dispatcher_cls
+
+    runs = []
+    for cap in (1 << 16, 40):
+        env = FakeEnv()
+        d = GpuPushDispatcher("127.0.0.1", 0, 10, max_workers=16, max_events=64, max_inflight=cap,
+                              redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+        sent = []
+        for t in range(16):
+            env.now = 1000.0 + t
+            if t == 0:
+                for w in range(6):
+                    env.inbound.append((wid(w), codec.serialize(
+                        {"type": "register", "data": {"num_processes": 3}}).encode(), env.now))
+            else:
+                # every worker returns one result per tick, worker 5 goes silent after tick 3
+                for (dst, m) in list(prev):
+                    if m["type"] == "task" and not (dst == wid(5) and t > 3):
+                        env.inbound.append((dst, codec.serialize({"type": "result", "data": {
+                            "task_id": m["data"]["task_id"], "status": "COMPLETED", "result": 1}}).encode(),
+                            env.now))
+                env.now += 0.5
+            env.tasks.extend("t%d_%d" % (t, j) for j in range(7))
+            env.sent.clear()
+            d.tick()
+            prev = list(env.sent)
+            sent.append(prev)
+        runs.append(sent)
+        assert (d.compactions > 0) == (cap == 40)
+    assert runs[0] == runs[1]
+    assert sum(len(x) for x in runs[0]) > 50

@@ -1,0 +1,17 @@
+#!/bin/bash
+# GPU-box check: parity tests, smoke, one bench line.  Every GPU step has its own
+# time limit and the chain stops at the first failure.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+mkdir -p gpurun_out
+TAG=${1:-chk}
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread \
+    > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -30 gpurun_out/${TAG}_pytest.log; exit 11; }
+tail -3 gpurun_out/${TAG}_pytest.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
+    || { tail -20 gpurun_out/${TAG}_smoke.log; exit 12; }
+tail -1 gpurun_out/${TAG}_smoke.log
+timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
+    || { tail -20 gpurun_out/${TAG}_bench.err; exit 13; }
+cat gpurun_out/${TAG}_bench.json
