@@ -39,8 +39,7 @@ struct fb_ctx {
     uint8_t *inq[2] = {nullptr, nullptr};
     int32_t *queue[2] = {nullptr, nullptr};
     uint8_t *reg = nullptr;
-    double *hb = nullptr;
-    uint32_t *epoch = nullptr;
+    HbRec *hbe = nullptr;  // {last_heartbeat (NaN: no record), epoch} per slot
     int32_t *log_slot = nullptr;
     int64_t Qn = 0, head = 0;
     uint32_t tick = 1;
@@ -67,6 +66,7 @@ struct fb_ctx {
     uint32_t *fcnt = nullptr, *wcnt = nullptr;
     int64_t *fpre = nullptr, *wpre = nullptr;
     uint32_t *qcnt = nullptr;
+    uint32_t *segcnt = nullptr;  // fused path: per-segment round counts (4 x table)
     int64_t *qpre = nullptr, *A = nullptr;
     size_t table_cap = 0;  // entries of qcnt / qpre
     int R_cap = 0;         // entries of A
@@ -77,6 +77,9 @@ struct fb_ctx {
     unsigned long long *dbg = nullptr;             // diagnostic stamps
     size_t dbg_n = 0;
     int force_plan = 0;
+    int split_slots = 0;
+    int old_emit = 0;
+    int dbg_stop = 0;     // FAASBAL_DBG_STOP=n: timing probe (results invalid)     // FAASBAL_OLD_EMIT=1: 256-thread k_emit on the fused path (A/B switch)  // FAASBAL_SPLIT_SLOTS=1: separate k_slots launch + died bitmap (A/B switch)
     void *arena = nullptr;    // every fixed-size device buffer, carved from one allocation
     size_t arena_bytes = 0;
     bool table_owned = false; // qcnt/qpre grown beyond the arena's reservation
@@ -315,8 +318,7 @@ int enqueue_tick(fb_ctx *c) {
         a.ev_status = evs;
         a.reg = c->reg;
         a.free_in = c->free_[cur];
-        a.hb = c->hb;
-        a.epoch = c->epoch;
+        a.hbe = c->hbe;
         a.inq_in = c->inq[cur];
         a.log_slot = c->log_slot;
         a.post_reg = c->post_reg;
@@ -340,6 +342,8 @@ int enqueue_tick(fb_ctx *c) {
     // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
+    a.slots_in_scan = c->split_slots ? 0 : 1;
+    a.dbg_stop = c->dbg_stop;
     a.tick = c->tick;
     a.now = c->l_now;
     a.tte = c->l_tte;
@@ -349,9 +353,8 @@ int enqueue_tick(fb_ctx *c) {
     a.T = c->l_T;
     a.log_cap = c->log_cap;
     a.reg = c->reg;
-    a.hb = c->hb;
+    a.hbe = c->hbe;
     a.free_in = c->free_[cur];
-    a.epoch = c->epoch;
     a.queue_in = c->queue[cur];
     a.touched = c->touched;
     a.post_reg = c->post_reg;
@@ -367,6 +370,7 @@ int enqueue_tick(fb_ctx *c) {
     a.wcnt = c->wcnt;
     a.fcnt = c->fcnt;
     a.qcnt = c->qcnt;
+    a.segcnt = c->segcnt;
     a.qbmax = c->qbmax;
     a.qbm_raw = c->qbm_raw;
     a.csum = c->csum;
@@ -397,7 +401,7 @@ int enqueue_tick(fb_ctx *c) {
         a.oA = c->oA;
     }
     {
-        const size_t need = (size_t)2 * (nbw + nbf + nbq) * 16 + 16;
+        const size_t need = (size_t)3 * (nbw + nbf + nbq) * 16 + 16;
         if (need > c->dbg_n) {
             hipFree(c->dbg);
             c->dbg = nullptr;
@@ -408,7 +412,7 @@ int enqueue_tick(fb_ctx *c) {
     }
     if (a.shard == 1) {
         // phase 1: own slots' purge, orphan flags and free counts into the exchange buffer
-        {
+        if (!a.slots_in_scan) {
             Timer t(c, "slots");
             launch_slots(a, t.st());
         }
@@ -432,7 +436,7 @@ int enqueue_tick(fb_ctx *c) {
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
-    {
+    if (!a.slots_in_scan) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
     }
@@ -446,7 +450,8 @@ int enqueue_tick(fb_ctx *c) {
     }
     {
         Timer t(c, "emit");
-        launch_emit(a, t.st());
+        if (a.fused) launch_emit2(a, t.st());
+        else launch_emit(a, t.st());
     }
     HIPCHK(c, hipGetLastError());
     return FB_OK;
@@ -496,8 +501,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->queue[i], Wq);
     }
     ap.add(&c->reg, W);
-    ap.add(&c->hb, W);
-    ap.add(&c->epoch, W);
+    ap.add(&c->hbe, W);
     ap.add(&c->touched, W);
     ap.add(&c->post_reg, W);
     ap.add(&c->post_flags, W);
@@ -532,6 +536,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->P, 1);
     const size_t tab = (size_t)128 * (size_t)cdiv(Qlog, kBS);
     ap.add(&c->qcnt, tab);
+    ap.add(&c->segcnt, 4 * tab);
     ap.add(&c->qpre, tab);
     ap.add(&c->A, 128);
     ap.add(&c->log_slot, F);
@@ -552,6 +557,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && hipHostGetDevicePointer((void **)&c->hout_dev, c->hout, 0) != hipSuccess) rc = FB_EHIP;
     if (!rc) memset(c->hout, 0, sizeof(HostOut));
     if (!rc && getenv("FAASBAL_FORCE_PLAN")) c->force_plan = atoi(getenv("FAASBAL_FORCE_PLAN"));
+    if (!rc && getenv("FAASBAL_SPLIT_SLOTS")) c->split_slots = atoi(getenv("FAASBAL_SPLIT_SLOTS"));
+    if (!rc && getenv("FAASBAL_DBG_STOP")) c->dbg_stop = atoi(getenv("FAASBAL_DBG_STOP"));
     if (!rc && hipHostMalloc(&c->h_stage, E * 32, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
@@ -620,16 +627,20 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         if (log_slot[i] < -1 || log_slot[i] >= n_workers)
             return fail(c, FB_EINVAL, "log_slot[%lld] = %d out of range", (long long)i, log_slot[i]);
     std::vector<uint8_t> reg(W ? W : 1, 0);
-    for (size_t s = 0; s < W; ++s) reg[s] = registered[s] ? 1 : 0;
+    std::vector<HbRec> hbv(W ? W : 1);
+    for (size_t s = 0; s < W; ++s) {
+        reg[s] = registered[s] ? 1 : 0;
+        hbv[s].hb = reg[s] ? last_heartbeat[s] : __builtin_nan("");  // no record: NaN (never "dead")
+        hbv[s].epoch = epoch ? epoch[s] : 0u;
+        hbv[s].pad = 0;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->free_[0], free_processes, W * 4, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->hb, last_heartbeat, W * 8, hipMemcpyHostToDevice));
-        if (epoch) HIPCHK(c, hipMemcpy(c->epoch, epoch, W * 4, hipMemcpyHostToDevice));
-        else HIPCHK(c, hipMemset(c->epoch, 0, W * 4));
+        HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
     }
     if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
@@ -652,8 +663,14 @@ int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, doubl
     if (W) {
         if (registered) HIPCHK(c, hipMemcpy(registered, c->reg, W, hipMemcpyDeviceToHost));
         if (free_processes) HIPCHK(c, hipMemcpy(free_processes, c->free_[c->cur], W * 4, hipMemcpyDeviceToHost));
-        if (last_heartbeat) HIPCHK(c, hipMemcpy(last_heartbeat, c->hb, W * 8, hipMemcpyDeviceToHost));
-        if (epoch) HIPCHK(c, hipMemcpy(epoch, c->epoch, W * 4, hipMemcpyDeviceToHost));
+        if (last_heartbeat || epoch) {
+            std::vector<HbRec> hbv(W);
+            HIPCHK(c, hipMemcpy(hbv.data(), c->hbe, W * sizeof(HbRec), hipMemcpyDeviceToHost));
+            for (size_t s = 0; s < W; ++s) {
+                if (last_heartbeat) last_heartbeat[s] = hbv[s].hb;
+                if (epoch) epoch[s] = hbv[s].epoch;
+            }
+        }
     }
     if (queue && c->Qn) HIPCHK(c, hipMemcpy(queue, c->queue[c->cur], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
     if (queue_len) *queue_len = c->Qn;
@@ -698,16 +715,20 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
             return fail(c, FB_EINVAL, "log_seq must ascend below log_head (entry %lld)", (long long)i);
     }
     std::vector<uint8_t> reg(W ? W : 1, 0);
-    for (size_t s = 0; s < W; ++s) reg[s] = registered[s] ? 1 : 0;
+    std::vector<HbRec> hbv(W ? W : 1);
+    for (size_t s = 0; s < W; ++s) {
+        reg[s] = registered[s] ? 1 : 0;
+        hbv[s].hb = reg[s] ? last_heartbeat[s] : __builtin_nan("");  // no record: NaN (never "dead")
+        hbv[s].epoch = epoch ? epoch[s] : 0u;
+        hbv[s].pad = 0;
+    }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->free_[0], free_processes, W * 4, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->hb, last_heartbeat, W * 8, hipMemcpyHostToDevice));
-        if (epoch) HIPCHK(c, hipMemcpy(c->epoch, epoch, W * 4, hipMemcpyHostToDevice));
-        else HIPCHK(c, hipMemset(c->epoch, 0, W * 4));
+        HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
     }
     if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
@@ -880,8 +901,7 @@ int fb_tick_commit(fb_ctx *c) {
         a.post_hb = c->post_hb;
         a.post_epoch = c->post_epoch;
         a.reg = c->reg;
-        a.hb = c->hb;
-        a.epoch = c->epoch;
+        a.hbe = c->hbe;
         Timer t(c, "commit");
         launch_commit(a, (int)cdiv(c->W, kBS), t.st());
         HIPCHK(c, hipGetLastError());
@@ -968,7 +988,8 @@ int fb_tick(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *
 int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     if (!c || !v) return FB_EINVAL;
     v->free_processes = c->free_[c->cur];
-    v->last_heartbeat = c->hb;
+    v->last_heartbeat = &c->hbe->hb;
+    v->last_heartbeat_stride = (int32_t)sizeof(HbRec);
     v->registered = c->reg;
     v->queue = c->queue[c->cur];
     v->log_slot = c->log_slot;

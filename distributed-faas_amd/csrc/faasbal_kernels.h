@@ -28,6 +28,15 @@ constexpr uint8_t kStEvicted = 4;    // record deleted during the tick and not r
 constexpr int kPfDiedStart = 1;
 constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 
+// Committed per-slot heartbeat record: last_heartbeat (NaN when the slot holds no
+// record) and the first log sequence of the current registration, in one 16-byte
+// line so the log scan gets both with a single gather.
+struct alignas(16) HbRec {
+    double hb;
+    uint32_t epoch;
+    uint32_t pad;
+};
+
 // results of a tick, written by k_emit into host-mapped pinned memory
 struct HostOut {
     int64_t O;          // orphans redistributed first
@@ -69,8 +78,7 @@ struct EvArgs {
     uint8_t *ev_status;
     const uint8_t *reg;
     const int32_t *free_in;
-    const double *hb;
-    const uint32_t *epoch;
+    const HbRec *hbe;
     const uint8_t *inq_in;
     int32_t *log_slot;
     uint8_t *post_reg;
@@ -87,14 +95,15 @@ struct TickArgs {
     int W, E, R, nbw, nbf, nbq;
     int fused;       // 1: k_emit derives the cross-block prefixes itself (no k_plan launch)
     int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
+    int slots_in_scan;
+    int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;
     double now, tte;
     int64_t Qn, Qlog, head_in, T, log_cap;
     // committed state
     const uint8_t *reg;
-    const double *hb;
+    const HbRec *hbe;
     const int32_t *free_in;
-    const uint32_t *epoch;
     const int32_t *queue_in;
     // this tick's message results
     const uint32_t *touched;
@@ -108,6 +117,7 @@ struct TickArgs {
     int32_t *c_arr;  // raw free_processes of a live LRU position, INT32_MIN otherwise
     uint8_t *ofl;    // orphan flags, one byte per F-thread (8 log entries)
     uint32_t *wcnt, *fcnt, *qcnt;
+    uint32_t *segcnt;  // [64-position segment][round] counts of c > r (fused path)
     int32_t *qbmax, *qbm_raw;
     unsigned long long *csum;
     int64_t *fpre, *wpre, *qpre, *A;
@@ -143,8 +153,7 @@ struct CommitArgs {
     const double *post_hb;
     const uint32_t *post_epoch;
     uint8_t *reg;
-    double *hb;
-    uint32_t *epoch;
+    HbRec *hbe;
 };
 
 // Host-side launchers (defined in faasbal_kernels.hip; grid sizes are the caller's).
@@ -167,6 +176,7 @@ void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
 void launch_plan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
+void launch_emit2(const TickArgs &a, Stream st);
 void launch_emit_shard(const TickArgs &a, Stream st);
 void launch_commit(const CommitArgs &a, int grid, Stream st);
 

@@ -25,17 +25,21 @@ namespace fb {
 // Diagnostic builds (-DFAASBAL_STAMPS) record s_memtime at phase boundaries of
 // thread 0 of every block into a.dbg[block * 16 + slot]; no output reads them.
 #ifdef FAASBAL_STAMPS
+// slot 0 (entry) and slot 15 (exit) also record s_memrealtime (100 MHz, chip-wide)
+// into slots 13 and 14, so kernel spans can be compared across XCDs.
 #define STAMP(a, kernel_off, slot)                                                                      \
     do {                                                                                                \
         __builtin_amdgcn_sched_barrier(0);                                                              \
-        if (threadIdx.x == 0) (a).dbg[((kernel_off) + blockIdx.x) * 16 + (slot)] = __builtin_amdgcn_s_memtime(); \
+        if (threadIdx.x == 0) {                                                                         \
+            unsigned long long *row_ = (a).dbg + ((kernel_off) + blockIdx.x) * 16;                      \
+            row_[(slot)] = __builtin_amdgcn_s_memtime();                                                \
+            if ((slot) == 0) row_[13] = __builtin_amdgcn_s_memrealtime();                               \
+            if ((slot) == 15) row_[14] = __builtin_amdgcn_s_memrealtime();                              \
+        }                                                                                               \
         __builtin_amdgcn_sched_barrier(0);                                                              \
     } while (0)
-#define STAMPR(a, kernel_off, slot)                                                                     \
-    do {                                                                                                \
-        __builtin_amdgcn_sched_barrier(0);                                                              \
-        if (threadIdx.x == 0) (a).dbg[((kernel_off) + blockIdx.x) * 16 + (slot)] = __builtin_amdgcn_s_memrealtime(); \
-        __builtin_amdgcn_sched_barrier(0);                                                              \
+#define STAMPR(a, kernel_off, slot) \
+    do {                            \
     } while (0)
 #else
 #define STAMPR(a, kernel_off, slot) \
@@ -273,8 +277,8 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
     int reg = a.reg[s];
     int32_t fr = a.free_in[s];
-    double hb = a.hb[s];
-    uint32_t epoch = a.epoch[s];
+    double hb = a.hbe[s].hb;
+    uint32_t epoch = a.hbe[s].epoch;
     int inq = a.inq_in[s];
     int qstat = inq ? kQsKeep : kQsOut;
     int qidx = -1;
@@ -349,7 +353,7 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
         c.flags = a.post_flags[s];
     } else {
         c.reg = c.reg0;
-        c.hb = a.hb[s];
+        c.hb = a.hbe[s].hb;
         c.fr = a.free_in[s];
         c.flags = 0;
     }
@@ -438,13 +442,12 @@ __device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int
     }
 }
 
-// ------------------------------------------------------------ k_slots
+// ------------------------------------------------------------ slot purge
 // Heartbeat purge of every slot (purge_workers, :241-249): liveness, the
 // died-registration bitmap, next free_processes (INT32_MIN = no live record).
-__global__ __launch_bounds__(kBS) void k_slots(TickArgs a) {
-    __shared__ uint32_t l4[kWaves];
-    STAMP(a, 0, 0);
-    const int s = blockIdx.x * kBS + threadIdx.x;
+// Its own launch (k_slots) or the W-role blocks of k_scan (a.slots_in_scan).
+__device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t *l4) {
+    const int s = blk * kBS + threadIdx.x;
     bool died_start = false, evicted = false;
     if (s < a.W) {
         const Cur c = cur_slot(a, s);
@@ -457,12 +460,27 @@ __global__ __launch_bounds__(kBS) void k_slots(TickArgs a) {
         a.inq_out[s] = 0;
     }
     const uint64_t dm = __ballot(died_start);
-    if (lane_id() == 0 && blockIdx.x * kBS + wave_id() * 64 < a.W) a.dmask[(blockIdx.x * kBS) / 64 + wave_id()] = dm;
+    if (!a.slots_in_scan && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
     const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
     if (lane_id() == 0) l4[wave_id()] = ev;
     __syncthreads();
-    if (threadIdx.x == 0) a.wcnt[blockIdx.x] = l4[0] + l4[1] + l4[2] + l4[3];
+    if (threadIdx.x == 0) a.wcnt[blk] = l4[0] + l4[1] + l4[2] + l4[3];
+}
+
+__global__ __launch_bounds__(kBS) void k_slots(TickArgs a) {
+    __shared__ uint32_t l4[kWaves];
+    STAMP(a, 0, 0);
+    slots_body(a, blockIdx.x, l4);
     STAMP(a, 0, 15);
+}
+
+// The registration of slot s alive at tick start died during this tick (read
+// straight from the record: used by k_scan's log role when no bitmap exists).
+// Committed hb is NaN for unregistered slots, so the untouched case is one load.
+__device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
+    if (!a.reg[s]) return false;
+    if (a.post_flags[s] & kPfDiedStart) return true;
+    return a.post_reg[s] && ((a.now - a.post_hb[s]) > a.tte);
 }
 
 // ------------------------------------------------------------ k_scan
@@ -498,6 +516,28 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) v[j] = v[j] < 0 ? -1 : v[j] - a.slot_base;
         }
+        uint32_t died = 0;
+        if (a.slots_in_scan) {
+            // died-at-start straight from the records: 8 independent 16-byte {hb, epoch}
+            // gathers per thread; the epoch rides along, so the orphan test needs no
+            // further load
+            double2 h[kFItems];
+            uint32_t tc[kFItems];
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) {
+                const int sj = v[j] < 0 ? 0 : v[j];
+                h[j] = *reinterpret_cast<const double2 *>(a.hbe + sj);
+                tc[j] = a.E > 0 ? a.touched[sj] : 0u;
+            }
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) {
+                bool d = false;
+                if (v[j] >= 0) d = (a.E > 0 && tc[j] == a.tick) ? died_touched(a, v[j]) : ((a.now - h[j].x) > a.tte);
+                const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
+                const uint32_t ep = (uint32_t)__double_as_longlong(h[j].y);
+                died |= (d && seq >= (uint64_t)ep) ? (1u << j) : 0u;
+            }
+        } else {
         const int nwords = (a.W + 63) >> 6;
         const unsigned long long *dm = a.dmask;
         if (a.lds_bitmap) {
@@ -518,20 +558,22 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
             __syncthreads();
             dm = dyn;
         }
-        uint32_t died = 0;
 #pragma unroll
         for (int j = 0; j < kFItems; ++j) {
             const int sj = v[j] < 0 ? 0 : v[j];
             const unsigned long long wd = dm[sj >> 6];
             died |= (v[j] >= 0 && ((wd >> (sj & 63)) & 1ull)) ? (1u << j) : 0u;
         }
+        }
         uint32_t flags = 0;
-        if (died) {
+        if (a.slots_in_scan) {
+            flags = died;
+        } else if (died) {
 #pragma unroll
             for (int j = 0; j < kFItems; ++j)
                 if ((died >> j) & 1u) {
                     const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
-                    if (seq >= (uint64_t)a.epoch[v[j]]) flags |= 1u << j;
+                    if (seq >= (uint64_t)a.hbe[v[j]].epoch) flags |= 1u << j;
                 }
         }
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
@@ -546,8 +588,15 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
         STAMP(a, SO, 15);
         return;
     }
+    const int nbw = (a.shard == 2 || !a.slots_in_scan) ? 0 : a.nbw;
+    if (bid < nbf + nbw) {
+        // ---- W-role: heartbeat purge of slots [b*256, +256)
+        slots_body(a, bid - nbf, l4);
+        STAMP(a, SO, 15);
+        return;
+    }
     // ---- Q-role: LRU positions [b*256, +256) of fronts ++ queue ++ backs
-    const int b = bid - nbf;
+    const int b = bid - nbf - nbw;
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
     int c = 0, oc = 0;
     if (a.shard == 2) {
@@ -559,7 +608,15 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
     } else if (pos < a.Qlog) {
         const int s = lq_slot(a, pos);
         const int ls = s >= 0 ? own_slot(a, s) : -1;
-        int32_t raw = ls >= 0 ? a.free_out[ls] : INT32_MIN;  // INT32_MIN: no live record (or not mine)
+        int32_t raw = INT32_MIN;  // INT32_MIN: no live record (or not mine)
+        if (ls >= 0) {
+            if (a.slots_in_scan) {
+                const Cur cu = cur_slot(a, ls);
+                raw = (cu.reg && !is_dead(a, cu)) ? cu.fr : INT32_MIN;
+            } else {
+                raw = a.free_out[ls];
+            }
+        }
         // an old queue entry moved to the front, re-appended or removed by this tick's messages
         if (raw != INT32_MIN && a.E > 0 && pos >= a.E && pos < a.E + a.Qn && a.touched[ls] == a.tick &&
             ((a.post_flags[ls] >> 1) & 3) != kQsKeep)
@@ -597,6 +654,9 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
                     cnt = wave_round_counts(cc, r0, k);
                 }
                 wc[wave_id()][g * 64 + lane_id()] = cnt;
+                // per 64-position segment (k_emit2 derives its rank bases from these rows)
+                if (a.fused && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
+                    a.segcnt[(size_t)(4 * b + wave_id()) * a.R + r0 + lane_id()] = cnt;
             }
             __syncthreads();
             uint32_t t = 0;
@@ -715,15 +775,13 @@ struct EmitLds {
 
 __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
     __shared__ EmitLds E_;
-    __shared__ uint32_t part[kWaves * 32][9];    // fused prologue: per-wave class partials
     __shared__ uint32_t red[kWaves][4];
     __shared__ unsigned long long red64[kWaves];
     __shared__ int64_t S_l[kBS + 1];             // S(r) of the current round chunk
     __shared__ int64_t pre_c[kBS];               // this block's prefix of round r (chunk)
-    __shared__ uint32_t tot_f[kRFused];          // fused: A(r)
     __shared__ int32_t misc[8];
     const int bid = blockIdx.x;
-    const int SO = a.nbw + a.nbf + a.nbq;
+    const int SO = a.nbw + a.nbf + a.nbq + (a.slots_in_scan ? a.nbw : 0);
     STAMP(a, SO, 0);
     const int lane = lane_id(), w = wave_id();
     if (bid < a.nbq) {
@@ -736,141 +794,8 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         int rlim;
         int L = 0;
         int64_t S_L = 0, N_eff;
-        if (a.fused) {
-            // ---- every prologue load in flight at once (clamped indices, no branches)
-            const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
-            const int32_t raw0 = a.c_arr[pq];
-            int s0;
-            if (a.E == 0) s0 = a.queue_in[pq];
-            else s0 = lq_slot(a, pq);
-            const int R = a.R;       // 32, 64 or 128
-            const int cls = R >> 2;  // int4 columns per table row
-            const int lcls = 31 - __builtin_clz(cls);
-            const int nq4 = (a.nbq * R) >> 2;
-            const uint4 *tab = reinterpret_cast<const uint4 *>(a.qcnt);
-            uint4 tv[kTabLd];
-#pragma unroll
-            for (int k = 0; k < kTabLd; ++k) {
-                const int q = threadIdx.x + k * kBS;
-                tv[k] = tab[q < nq4 ? q : nq4 - 1];
-            }
-            uint32_t fv[kPeel], wv[kPeel], mv[kPeel], cv[kPeel];
-            const int nbf1 = a.nbf > 0 ? a.nbf - 1 : 0, nbw1 = a.nbw - 1, nbq1 = a.nbq - 1;
-#pragma unroll
-            for (int k = 0; k < kPeel; ++k) {
-                const int i = threadIdx.x + k * kBS;
-                fv[k] = a.fcnt[i < nbf1 ? i : nbf1];
-                wv[k] = a.wcnt[i < nbw1 ? i : nbw1];
-                mv[k] = (uint32_t)a.qbm_raw[i < nbq1 ? i : nbq1];
-                cv[k] = (uint32_t)a.csum[i < nbq1 ? i : nbq1];
-            }
-            // ---- per-thread partials
-            if (threadIdx.x == 0 && (fv[0] + wv[0] + mv[0] + cv[0] + tv[0].x + tv[kTabLd - 1].w + (uint32_t)raw0 + (uint32_t)s0) == 0x7fffffffu)
-                a.c_arr[0] = 0;  // (never true in practice) keeps the stamp below behind the loads
-            STAMP(a, SO, 9);
-            uint32_t fo = 0, wo = 0, mo = 0, co = 0;
-#pragma unroll
-            for (int k = 0; k < kPeel; ++k) {
-                const int i = threadIdx.x + k * kBS;
-                fo += i < a.nbf ? fv[k] : 0u;
-                wo += i < a.nbw ? wv[k] : 0u;
-                mo = (i < a.nbq && mv[k] > mo) ? mv[k] : mo;
-                co += i < a.nbq ? cv[k] : 0u;
-                if (i == b) misc[4] = (int32_t)mv[k];  // this block's max c
-            }
-            for (int i = threadIdx.x + kPeel * kBS; i < a.nbf; i += kBS) fo += a.fcnt[i];
-            for (int i = threadIdx.x + kPeel * kBS; i < a.nbw; i += kBS) wo += a.wcnt[i];
-            for (int i = threadIdx.x + kPeel * kBS; i < a.nbq; i += kBS) {
-                mo = (uint32_t)a.qbm_raw[i] > mo ? (uint32_t)a.qbm_raw[i] : mo;
-                co += (uint32_t)a.csum[i];
-                if (i == b) misc[4] = a.qbm_raw[i];
-            }
-            // table: thread t covers rows r0..r0+3, r0 = 4 (t mod cls), of blocks q / cls
-            uint32_t pp[4] = {0, 0, 0, 0}, tt[4] = {0, 0, 0, 0};
-#pragma unroll
-            for (int k = 0; k < kTabLd; ++k) {
-                const int q = threadIdx.x + k * kBS;
-                const bool in = q < nq4;
-                const bool before = in && (q >> lcls) < b;
-                tt[0] += in ? tv[k].x : 0u; tt[1] += in ? tv[k].y : 0u;
-                tt[2] += in ? tv[k].z : 0u; tt[3] += in ? tv[k].w : 0u;
-                pp[0] += before ? tv[k].x : 0u; pp[1] += before ? tv[k].y : 0u;
-                pp[2] += before ? tv[k].z : 0u; pp[3] += before ? tv[k].w : 0u;
-            }
-            for (int q = threadIdx.x + kTabLd * kBS; q < nq4; q += kBS) {
-                const uint4 v = tab[q];
-                const bool before = (q >> lcls) < b;
-                tt[0] += v.x; tt[1] += v.y; tt[2] += v.z; tt[3] += v.w;
-                pp[0] += before ? v.x : 0u; pp[1] += before ? v.y : 0u;
-                pp[2] += before ? v.z : 0u; pp[3] += before ? v.w : 0u;
-            }
-            // lanes of one class (lane mod cls) hold partials of the same 4 rows
-            for (int d = cls; d < 64; d <<= 1) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    pp[u] += __shfl_xor(pp[u], d, 64);
-                    tt[u] += __shfl_xor(tt[u], d, 64);
-                }
-            }
-            if (lane < cls) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    part[w * 32 + lane][u] = pp[u];
-                    part[w * 32 + lane][4 + u] = tt[u];
-                }
-            }
-            fo = wave_sum_u32(fo);
-            wo = wave_sum_u32(wo);
-            co = wave_sum_u32(co);
-            mo = wave_max_u32(mo);
-            if (lane == 0) {
-                red[w][0] = fo;
-                red[w][1] = wo;
-                red[w][2] = co;
-                red[w][3] = mo;
-            }
-            raw = pos < a.Qlog ? raw0 : INT32_MIN;
-            s = s0;
-            STAMP(a, SO, 10);
-            __syncthreads();
-            STAMP(a, SO, 11);
-            O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-            nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
-            cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
-            maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
-            bm = misc[4];
-            // round-table rows: this block's prefix and the total, summed over the threads of row r's class
-            if ((int)threadIdx.x < R) {
-                const int r = threadIdx.x, c0 = r >> 2, u = r & 3;
-                const uint32_t p = part[c0][u] + part[32 + c0][u] + part[64 + c0][u] + part[96 + c0][u];
-                const uint32_t t = part[c0][4 + u] + part[32 + c0][4 + u] + part[64 + c0][4 + u] + part[96 + c0][4 + u];
-                pre_c[r] = (int64_t)p;
-                tot_f[r] = t;
-            }
-            __syncthreads();
-            STAMP(a, SO, 1);
-            rlim = maxc < R ? maxc : R;
-            if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
-            const int64_t N = O + a.T;
-            N_eff = N < cap ? N : cap;
-            // ---- fill level: one chunk (rlim <= 128); S(r+1) by a block scan of A(r)
-            {
-                const int r = threadIdx.x;
-                const uint32_t v = r < rlim ? tot_f[r] : 0u;
-                uint32_t tot;
-                const uint32_t ex = block_excl_scan_u32(v, (uint32_t *)red, tot);
-                const int64_t S1 = (int64_t)(ex + v);
-                const bool ok = r < rlim && S1 <= N_eff;
-                const int kw = __popcll(__ballot(ok));
-                if (lane == 0) misc[w] = kw;
-                S_l[r + 1] = S1;
-                if (r == 0) S_l[0] = 0;
-                __syncthreads();
-                L = misc[0] + misc[1] + misc[2] + misc[3];
-                S_L = S_l[L];
-            }
-        } else {
-            // ---- large grids: totals and scanned table from k_plan
+        {
+            // ---- totals and the scanned round table from k_plan
             if (pos < a.Qlog) {
                 raw = a.c_arr[pos];
                 s = lq_slot(a, pos);
@@ -909,7 +834,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         if (maxc > a.R && L >= a.R - 1) status = 1;   // rows beyond the table needed: rerun wider
         if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log
         const int64_t p = N_eff - S_L;
-        auto getA = [&](int r) -> int64_t { return r < rlim ? (a.fused ? (int64_t)tot_f[r] : a.A[r]) : (int64_t)0; };
+        auto getA = [&](int r) -> int64_t { return r < rlim ? a.A[r] : (int64_t)0; };
         const int64_t AL = (L < maxc && L < rlim) ? getA(L) : 0;
         STAMP(a, SO, 2);
         if (b == 0 && threadIdx.x == 0) {
@@ -933,7 +858,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         const int wmx = (int)wave_max_u32((uint32_t)c);
         for (int rc = 0; rc <= L + 1; rc += kBS) {
             const int rn = (L + 2 - rc) < kBS ? (L + 2 - rc) : kBS;
-            if (!a.fused) {
+            {
                 // chunk tables from k_plan: pre(r), S(r)
                 const int r = rc + threadIdx.x;
                 int64_t pr = 0, Av = 0;
@@ -947,7 +872,6 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
                 S_l[threadIdx.x] = carryS + (int64_t)ex;
                 carryS += (int64_t)tot;
             }
-            // fused: one chunk, pre_c[r] / S_l[r] from the prologue (rows >= rlim read as 0 / S(rlim))
             STAMP(a, SO, 5);
             // per-wave counts of c > r for the chunk's rounds
 #pragma unroll
@@ -968,14 +892,8 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
             for (int e = threadIdx.x; e < kWaves * rn; e += kBS) {
                 const int ww = e / rn, i = e - ww * rn;
                 const int r = rc + i;
-                int64_t rb, Sr;
-                if (a.fused) {
-                    rb = r < rlim ? pre_c[r] : 0;
-                    Sr = S_l[r < rlim ? r : rlim];
-                } else {
-                    rb = pre_c[i];
-                    Sr = S_l[i];
-                }
+                int64_t rb = pre_c[i];
+                const int64_t Sr = S_l[i];
                 for (int q = 0; q < ww; ++q) rb += E_.wc[q][i];
                 E_.wbase[ww][i] = (int32_t)rb;
                 E_.wpos[ww][i] = (r <= L) ? (int32_t)(Sr + rb) : 0;
@@ -1046,17 +964,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         // ---- orphan compaction, ascending sequence
         const int b = bid - a.nbq;
         const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
-        int64_t off;
-        if (a.fused) {
-            unsigned long long tot, pre;
-            peeled_sum(a.fcnt, b, b, tot, pre);
-            const uint32_t ws = wave_sum_u32((uint32_t)pre);
-            if (lane == 0) red[w][0] = ws;
-            __syncthreads();
-            off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        } else {
-            off = a.fpre[b];
-        }
+        const int64_t off = a.fpre[b];
         uint32_t tot;
         const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tot);
         int64_t o = off + ex;
@@ -1071,20 +979,281 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
     const int b = bid - a.nbq - a.nbf;
     const int s = b * kBS + threadIdx.x;
     const uint32_t e = (s < a.W && (a.st[s] & kStEvicted)) ? 1u : 0u;
-    int64_t off;
-    if (a.fused) {
-        unsigned long long tot, pre;
-        peeled_sum(a.wcnt, b, b, tot, pre);
-        const uint32_t ws = wave_sum_u32((uint32_t)pre);
-        if (lane == 0) red[w][0] = ws;
-        __syncthreads();
-        off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-    } else {
-        off = a.wpre[b];
-    }
+    const int64_t off = a.wpre[b];
     uint32_t tot;
     const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tot);
     if (e) a.evicted[off + ex] = s;
+    STAMP(a, SO, 15);
+}
+
+// ------------------------------------------------------------ k_emit2
+// k_emit for the fused path (round table of at most 8192 entries read as int4
+// [block][round]; no k_plan launch).  Two block barriers in all: per-thread
+// table partials -> barrier -> round rows (this block's prefix, totals) ->
+// barrier; then every wave works alone: S(r) and the fill level L by a wave
+// scan, the task index base of each round in one register (lane i: round
+// 64k + i) from the round prefix plus the earlier segments' counts that k_scan
+// stored per 64-position segment, and the emission.  F / W roles as k_emit's.
+constexpr int kTabLd2 = 8;  // int4 table loads per thread (tail loop beyond 8192 entries)
+constexpr int kRCh = 3;     // 64-round chunks: rounds 0 .. L+1 <= 129
+
+__global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
+    __shared__ uint32_t part[kWaves * 32][9];  // per-wave class partials
+    __shared__ uint32_t red[kWaves][4];
+    __shared__ uint32_t pre_c[kRFused];        // this block's prefix of round r
+    __shared__ uint32_t tot_f[kRFused];        // A(r)
+    __shared__ int32_t misc[8];
+    const int bid = blockIdx.x;
+    const int SO = a.nbw + a.nbf + a.nbq + (a.slots_in_scan ? a.nbw : 0);
+    STAMP(a, SO, 0);
+    const int lane = lane_id(), w = wave_id();
+    if (bid < a.nbq) {
+        const int b = bid;
+        const int64_t pos = (int64_t)b * kBS + threadIdx.x;
+        const int R = a.R;       // 32, 64 or 128
+        const int cls = R >> 2;  // int4 columns per table row
+        const int lcls = 31 - __builtin_clz(cls);
+        const int nq4 = (a.nbq * R) >> 2;
+        // ---- every load in flight at once (clamped indices, no branches)
+        const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
+        const int32_t raw0 = a.c_arr[pq];
+        const int s0 = a.E == 0 ? a.queue_in[pq] : lq_slot(a, pq);
+        const uint4 *tab = reinterpret_cast<const uint4 *>(a.qcnt);
+        uint4 tv[kTabLd2];
+#pragma unroll
+        for (int k = 0; k < kTabLd2; ++k) {
+            const int q = threadIdx.x + k * kBS;
+            tv[k] = tab[q < nq4 ? q : nq4 - 1];
+        }
+        uint32_t fv[kPeel], wv[kPeel], mv[kPeel], cv[kPeel];
+        const int nbf1 = a.nbf > 0 ? a.nbf - 1 : 0, nbw1 = a.nbw - 1, nbq1 = a.nbq - 1;
+#pragma unroll
+        for (int k = 0; k < kPeel; ++k) {
+            const int i = threadIdx.x + k * kBS;
+            fv[k] = a.fcnt[i < nbf1 ? i : nbf1];
+            wv[k] = a.wcnt[i < nbw1 ? i : nbw1];
+            mv[k] = (uint32_t)a.qbm_raw[i < nbq1 ? i : nbq1];
+            cv[k] = (uint32_t)a.csum[i < nbq1 ? i : nbq1];
+        }
+        // counts of c > r in the earlier segments of this block: lane i, round 64 k + i
+        uint32_t segc[kRCh] = {0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k) {
+            const int r = 64 * k + lane;
+            if (r < R) {
+                for (int q = 0; q < w; ++q) segc[k] += a.segcnt[(size_t)(4 * b + q) * R + r];
+            }
+        }
+        STAMP(a, SO, 9);
+        uint32_t fo = 0, wo = 0, mo = 0, co = 0;
+#pragma unroll
+        for (int k = 0; k < kPeel; ++k) {
+            const int i = threadIdx.x + k * kBS;
+            fo += i < a.nbf ? fv[k] : 0u;
+            wo += i < a.nbw ? wv[k] : 0u;
+            mo = (i < a.nbq && mv[k] > mo) ? mv[k] : mo;
+            co += i < a.nbq ? cv[k] : 0u;
+        }
+        for (int i = threadIdx.x + kPeel * kBS; i < a.nbf; i += kBS) fo += a.fcnt[i];
+        for (int i = threadIdx.x + kPeel * kBS; i < a.nbw; i += kBS) wo += a.wcnt[i];
+        for (int i = threadIdx.x + kPeel * kBS; i < a.nbq; i += kBS) {
+            mo = (uint32_t)a.qbm_raw[i] > mo ? (uint32_t)a.qbm_raw[i] : mo;
+            co += (uint32_t)a.csum[i];
+        }
+        // table: thread t covers rows r0..r0+3, r0 = 4 (t mod cls), of blocks q / cls
+        uint32_t pp[4] = {0, 0, 0, 0}, tt[4] = {0, 0, 0, 0};
+#pragma unroll
+        for (int k = 0; k < kTabLd2; ++k) {
+            const int q = threadIdx.x + k * kBS;
+            const uint32_t in = q < nq4 ? ~0u : 0u;
+            const uint32_t before = (q < nq4 && (q >> lcls) < b) ? ~0u : 0u;
+            tt[0] += tv[k].x & in; tt[1] += tv[k].y & in; tt[2] += tv[k].z & in; tt[3] += tv[k].w & in;
+            pp[0] += tv[k].x & before; pp[1] += tv[k].y & before;
+            pp[2] += tv[k].z & before; pp[3] += tv[k].w & before;
+        }
+        for (int q = threadIdx.x + kTabLd2 * kBS; q < nq4; q += kBS) {
+            const uint4 v = tab[q];
+            const uint32_t before = (q >> lcls) < b ? ~0u : 0u;
+            tt[0] += v.x; tt[1] += v.y; tt[2] += v.z; tt[3] += v.w;
+            pp[0] += v.x & before; pp[1] += v.y & before; pp[2] += v.z & before; pp[3] += v.w & before;
+        }
+        // lanes of one class (lane mod cls) hold partials of the same 4 rows
+        for (int d = cls; d < 64; d <<= 1) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                pp[u] += __shfl_xor(pp[u], d, 64);
+                tt[u] += __shfl_xor(tt[u], d, 64);
+            }
+        }
+        if (lane < cls) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                part[w * 32 + lane][u] = pp[u];
+                part[w * 32 + lane][4 + u] = tt[u];
+            }
+        }
+        fo = wave_sum_u32(fo);
+        wo = wave_sum_u32(wo);
+        co = wave_sum_u32(co);
+        mo = wave_max_u32(mo);
+        if (lane == 0) {
+            red[w][0] = fo;
+            red[w][1] = wo;
+            red[w][2] = co;
+            red[w][3] = mo;
+        }
+        __syncthreads();
+        // round rows: this block's prefix and the total, summed over the threads of row r's class
+        if ((int)threadIdx.x < R) {
+            const int r = threadIdx.x, c0 = r >> 2, u = r & 3;
+            pre_c[r] = part[c0][u] + part[32 + c0][u] + part[64 + c0][u] + part[96 + c0][u];
+            tot_f[r] = part[c0][4 + u] + part[32 + c0][4 + u] + part[64 + c0][4 + u] + part[96 + c0][4 + u];
+        }
+        const int64_t O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        const int64_t nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        int64_t cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
+        const int maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
+        __syncthreads();
+        STAMP(a, SO, 1);
+        const int rlim = maxc < R ? maxc : R;
+        if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
+        const int64_t N = O + a.T;
+        const int64_t N_eff = N < cap ? N : cap;
+        // ---- per wave: S(r) (lane i of chunk k: round 64 k + i), fill level L
+        int64_t Sv[kRCh];
+        int L = 0;
+        {
+            int64_t carry = 0;
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k) {
+                const int r = 64 * k + lane;
+                const uint32_t v = r < rlim ? tot_f[r] : 0u;
+                const uint32_t incl = wave_incl_scan_u32(v);
+                const int64_t S1 = carry + (int64_t)incl;  // S(r + 1)
+                Sv[k] = S1 - (int64_t)v;                   // S(r)
+                L += __popcll(__ballot(r < rlim && S1 <= N_eff));
+                carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            }
+        }
+        const int Lc = L >> 6, Ll = L & 63;
+        const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Sv[0] : (Lc == 1 ? Sv[1] : Sv[2])), Ll);
+        int status = 0;
+        if (maxc > R && L >= R - 1) status = 1;   // rows beyond the table needed: rerun wider
+        if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log
+        const int64_t pL = N_eff - S_L;
+        const int64_t AL = (L < maxc && L < rlim) ? (int64_t)tot_f[L] : 0;
+        if (b == 0 && threadIdx.x == 0) {
+            a.hout->O = O;
+            a.hout->n_evicted = nev;
+            a.hout->cap_total = cap;
+            a.hout->maxc = maxc;
+            a.hout->L = L;
+            a.hout->status = status;
+            a.hout->N_eff = status ? 0 : N_eff;
+            a.hout->p = pL;
+            a.hout->AL = AL;
+            if (AL == 0) a.hout->new_qlen = 0;
+        }
+        if (status) return;
+        // ---- rank base (in A_r) and task index base of this wave's segment, per round
+        const int32_t raw = pos < a.Qlog ? raw0 : INT32_MIN;
+        const int s = s0;
+        const int c = raw != INT32_MIN ? (raw > 1 ? raw : 1) : 0;  // free <= 0 still takes one task
+        int32_t rbv[kRCh], basev[kRCh];
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k) {
+            const int r = 64 * k + lane;
+            rbv[k] = (int32_t)((r < rlim ? pre_c[r] : 0u) + segc[k]);
+            basev[k] = (int32_t)Sv[k] + rbv[k];  // valid for r <= rlim
+        }
+        STAMP(a, SO, 2);
+        // ---- full rounds r < min(L, max c of the wave): every active lane takes one task
+        int32_t *const out = a.log_slot + a.head_in;
+        const int wmx = (int)wave_max_u32((uint32_t)c);
+        const int rfull = L < wmx ? L : wmx;
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k) {
+            const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
+            int i = 0;
+            for (; i + 3 < r1; i += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = 64 * k + i + u;
+                    const bool act = c > r;
+                    const uint64_t m = __ballot(act);
+                    const int base = __builtin_amdgcn_readlane(basev[k], i + u);
+                    if (act) out[base + popc_lt(m)] = s;
+                }
+            }
+            for (; i < r1; ++i) {
+                const int r = 64 * k + i;
+                const bool act = c > r;
+                const uint64_t m = __ballot(act);
+                const int base = __builtin_amdgcn_readlane(basev[k], i);
+                if (act) out[base + popc_lt(m)] = s;
+            }
+        }
+        STAMP(a, SO, 3);
+        // ---- round L (partial: ranks < pL) and round L + 1 (ranks for the next queue)
+        const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
+        const int rbL = __builtin_amdgcn_readlane(Lc == 0 ? rbv[0] : (Lc == 1 ? rbv[1] : rbv[2]), Ll);
+        const int rbL1 = __builtin_amdgcn_readlane(L1c == 0 ? rbv[0] : (L1c == 1 ? rbv[1] : rbv[2]), L1l);
+        const uint64_t mL = __ballot(c > L);
+        const int64_t rankL = (int64_t)rbL + popc_lt(mL);
+        if (c > L && rankL < pL) out[S_L + rankL] = s;
+        const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
+        if (c > 0) {
+            int64_t n_q = c < L ? c : L;
+            if (c > L && rankL < pL) n_q += 1;
+            a.free_out[s] = raw - (int32_t)n_q;
+            int64_t np = -1;
+            if (c > L) {
+                if (rankL >= pL) np = rankL - pL;
+                else if (c > L1) np = (AL - pL) + exL1;
+                // the one position of rank pL in A_L knows the next queue's length
+                if (rankL == pL) a.hout->new_qlen = (AL - pL) + exL1;
+            }
+            if (np >= 0) {
+                a.queue_out[np] = s;
+                a.inq_out[s] = 1;
+            }
+        }
+        STAMP(a, SO, 15);
+        return;
+    }
+    if (bid < a.nbq + a.nbf) {
+        // ---- orphan compaction, ascending sequence
+        const int b = bid - a.nbq;
+        const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
+        unsigned long long tot, pre;
+        peeled_sum(a.fcnt, b, b, tot, pre);
+        const uint32_t ws = wave_sum_u32((uint32_t)pre);
+        if (lane == 0) red[w][0] = ws;
+        __syncthreads();
+        const int64_t off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        uint32_t tt;
+        const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tt);
+        int64_t o = off + ex;
+        const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
+#pragma unroll
+        for (int j = 0; j < kFItems; ++j)
+            if (flags & (1u << j)) a.orphans[o++] = base + j;
+        STAMP(a, SO, 15);
+        return;
+    }
+    // ---- evicted compaction, ascending slot
+    const int b = bid - a.nbq - a.nbf;
+    const int sl = b * kBS + threadIdx.x;
+    const uint32_t e = (sl < a.W && (a.st[sl] & kStEvicted)) ? 1u : 0u;
+    unsigned long long tot, pre;
+    peeled_sum(a.wcnt, b, b, tot, pre);
+    const uint32_t ws = wave_sum_u32((uint32_t)pre);
+    if (lane == 0) red[w][0] = ws;
+    __syncthreads();
+    const int64_t off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    uint32_t tt;
+    const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tt);
+    if (e) a.evicted[off + ex] = sl;
     STAMP(a, SO, 15);
 }
 
@@ -1308,12 +1477,18 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
     const int s = blockIdx.x * kBS + threadIdx.x;
     if (s >= a.W) return;
     const uint8_t stt = a.st[s];
+    // committed hb is NaN for slots without a record (k_scan's log role relies on it)
     if (a.touched[s] == a.tick) {
-        a.reg[s] = (stt & kStAlive) ? 1 : 0;
-        a.hb[s] = a.post_hb[s];
-        a.epoch[s] = a.post_epoch[s];
+        const bool alive = (stt & kStAlive) != 0;
+        a.reg[s] = alive ? 1 : 0;
+        HbRec r;
+        r.hb = alive ? a.post_hb[s] : __builtin_nan("");
+        r.epoch = a.post_epoch[s];
+        r.pad = 0;
+        a.hbe[s] = r;
     } else if (stt & kStEvicted) {
         a.reg[s] = 0;
+        a.hbe[s].hb = __builtin_nan("");
     }
 }
 
@@ -1343,14 +1518,18 @@ void launch_slots(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_slots, dim3(a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_scan(const TickArgs &a, Stream st) {
-    const size_t lds = a.lds_bitmap ? (size_t)((a.W + 63) / 64) * 8 : 0;
-    hipExtLaunchKernelGGL(k_scan, dim3((a.shard == 2 ? 0 : a.nbf) + a.nbq), dim3(kBS), a.shard == 2 ? 0 : lds, st.s, st.e0, st.e1, 0, a);
+    const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
+    const int nbw = (a.shard == 2 || !a.slots_in_scan) ? 0 : a.nbw;
+    hipExtLaunchKernelGGL(k_scan, dim3((a.shard == 2 ? 0 : a.nbf) + nbw + a.nbq), dim3(kBS), a.shard == 2 ? 0 : lds, st.s, st.e0, st.e1, 0, a);
 }
 void launch_plan(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_emit(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_emit, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+}
+void launch_emit2(const TickArgs &a, Stream st) {
+    hipExtLaunchKernelGGL(k_emit2, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -59,7 +59,8 @@ typedef struct fb_tick_result {
  * torch tensors built from data_ptr).  Valid until the next fb_tick_commit. */
 typedef struct fb_device_view {
     int32_t *free_processes; /* [n_workers]  PushWorker.free_processes (:205)  */
-    double *last_heartbeat;  /* [n_workers]  PushWorker.last_heartbeat (:206)  */
+    double *last_heartbeat;  /* [n_workers]  PushWorker.last_heartbeat (:206), every
+                              * last_heartbeat_stride bytes; NaN for empty slots */
     uint8_t *registered;     /* [n_workers]  slot present in self.workers      */
     int32_t *queue;          /* [queue_len]  free_workers in LRU order (:327)  */
     int32_t *log_slot;       /* [log_head]   worker slot per task sequence     */
@@ -67,6 +68,7 @@ typedef struct fb_device_view {
     int32_t *evicted;        /* last tick's evicted slots                      */
     int32_t n_workers;
     int64_t queue_len, log_head;
+    int32_t last_heartbeat_stride; /* bytes between consecutive slots' heartbeats */
 } fb_device_view;
 
 /* Context: owns every device buffer.  device = HIP device ordinal. */

@@ -1,8 +1,11 @@
-"""Diagnostic: per-phase cycle breakdown of the tick kernels from in-kernel
-s_memtime stamps (libfaasbal_stamps.so, built with -DFAASBAL_STAMPS).
+"""Diagnostic: per-phase breakdown of the tick kernels from in-kernel stamps
+(libfaasbal_stamps.so, built with -DFAASBAL_STAMPS by tools/build_all.sh).
 
+Slots 0..12 and 15 of a block's row are s_memtime (shader clock, per XCD);
+13 / 14 are s_memrealtime (100 MHz, chip-wide) at block entry / exit.
     python tools/stamps.py [--workers 65536 --tasks 1000000 --reps 50]
-Run on the GPU box; prints median/max cycles per phase and role."""
+Run on the GPU box.  Prints, per kernel, the realtime span and, per role, the
+block entry offset / duration and the phase deltas in time order."""
 import argparse
 import os
 import sys
@@ -25,6 +28,7 @@ def main():
     args = ap.parse_args()
     st = synth.zipf_state(W=args.workers, seed=0)
     W, T = args.workers, args.tasks
+    split = os.environ.get("FAASBAL_SPLIT_SLOTS", "0") == "1"
     g = GpuBalancer(W, 2 * len(st["log"]) + T + 16, max_events=1, lib_path=STAMPS_SO)
     g.load(st)
     nbw = -(-W // 256)
@@ -35,31 +39,43 @@ def main():
     for _ in range(args.reps):
         g.launch(1000.0, 10.0, n_pending=T)
         g.wait()
-        d = g.debug_read()[: 2 * G1 * 16].reshape(2 * G1, 16).astype(np.int64)
+        d = g.debug_read()[: 3 * G1 * 16].reshape(3 * G1, 16).astype(np.int64)
         acc.append(d.copy())
-    d = np.stack(acc)  # reps x blocks x 16
-    roles = {"slots": (0, nbw), "scan.F": (nbw, nbw + nbf), "scan.Q": (nbw + nbf, G1),
-             "emit.Q": (G1, G1 + nbq), "emit.F": (G1 + nbq, G1 + nbq + nbf), "emit.W": (G1 + nbq + nbf, 2 * G1)}
-    for kern, (lo, hi) in (("slots", (0, nbw)), ("scan", (nbw, G1)), ("emit", (G1, 2 * G1))):
-        span = d[:, lo:hi, 15].max(axis=1) - d[:, lo:hi, 0].min(axis=1)
-        start_spread = d[:, lo:hi, 0].max(axis=1) - d[:, lo:hi, 0].min(axis=1)
-        print("%s: kernel span median %d cycles, block start spread %d" % (kern, np.median(span), np.median(start_spread)))
+    d = np.stack(acc)  # reps x rows x 16
+    S = nbw  # k_scan rows start here
+    E0 = G1 if split else G1 + nbw  # k_emit rows start here
+    if split:
+        kernels = {"slots": (0, nbw), "scan": (S, S + nbf + nbq), "emit": (E0, E0 + G1)}
+        roles = {"slots": (0, nbw), "scan.F": (S, S + nbf), "scan.Q": (S + nbf, S + nbf + nbq)}
+    else:
+        kernels = {"scan": (S, S + nbf + nbw + nbq), "emit": (E0, E0 + G1)}
+        roles = {"scan.F": (S, S + nbf), "scan.W": (S + nbf, S + nbf + nbw), "scan.Q": (S + nbf + nbw, S + G1)}
+    roles.update({"emit.Q": (E0, E0 + nbq), "emit.F": (E0 + nbq, E0 + nbq + nbf),
+                  "emit.W": (E0 + nbq + nbf, E0 + G1)})
+    starts = {}
+    for kern, (lo, hi) in kernels.items():
+        ent, ext = d[:, lo:hi, 13], d[:, lo:hi, 14]
+        starts[kern] = ent.min(axis=1)
+        span = (ext.max(axis=1) - ent.min(axis=1)) / 100.0
+        spread = (ent.max(axis=1) - ent.min(axis=1)) / 100.0
+        print("%-6s span %.2f us (median), entry spread %.2f us" % (kern, np.median(span), np.median(spread)))
+    ks = list(kernels)
+    for a, b in zip(ks[:-1], ks[1:]):
+        gap = (starts[b] - d[:, kernels[a][0]:kernels[a][1], 14].max(axis=1)) / 100.0
+        print("gap %s end -> %s first entry: %.2f us" % (a, b, np.median(gap)))
     for name, (lo, hi) in roles.items():
         x = d[:, lo:hi, :]
+        kern = name.split(".")[0]
+        off = (x[..., 13] - starts[kern][:, None]) / 100.0
+        dur = (x[..., 14] - x[..., 13]) / 100.0
+        print("%-7s %4d blocks: entry +%.2f us (p90 %.2f), duration %.2f us (p90 %.2f)" % (
+            name, hi - lo, np.median(off), np.percentile(off, 90), np.median(dur), np.percentile(dur, 90)))
         used = [k for k in range(13) if (x[..., k] > 0).all()] + [15]
-        if (x[..., 13] > 0).all() and (x[..., 14] > 0).all():
-            rt = (x[..., 14] - x[..., 13]).ravel() / 100.0  # s_memrealtime: 100 MHz
-            cy = (x[..., 15] - x[..., 0]).ravel()
-            print("   realtime entry->exit median %.2f us; shader clock %.2f GHz" % (np.median(rt), np.median(cy / rt) / 1e3))
-        print(name, "blocks", hi - lo, "stamps", used)
-        for a, b in zip(used[:-1], used[1:]):
+        med = {k: np.median(x[..., k] - x[..., 0]) for k in used}
+        order = sorted(used, key=lambda k: med[k])
+        for a, b in zip(order[:-1], order[1:]):
             dt = (x[..., b] - x[..., a]).ravel()
-            print("   %2d->%2d  median %7d  p90 %7d  max %7d" % (a, b, np.median(dt), np.percentile(dt, 90), dt.max()))
-        # completion time relative to the kernel's first block start
-        kl, kh = (0, nbw) if name == "slots" else ((nbw, G1) if name.startswith("scan") else (G1, 2 * G1))
-        first = d[:, kl:kh, 0].min(axis=1)[:, None]
-        end = (x[..., 15] - first).ravel()
-        print("   end-from-kernel-start median %d max %d" % (np.median(end), end.max()))
+            print("      %2d->%2d  median %7d cyc  p90 %7d" % (a, b, np.median(dt), np.percentile(dt, 90)))
 
 
 if __name__ == "__main__":
