@@ -38,6 +38,10 @@ struct fb_ctx {
     int32_t *free_[2] = {nullptr, nullptr};
     uint8_t *inq[2] = {nullptr, nullptr};
     int32_t *queue[2] = {nullptr, nullptr};
+    int32_t *qfree[2] = {nullptr, nullptr};  // free_processes by LRU position (one-GPU contexts)
+    double *qhb[2] = {nullptr, nullptr};     // last_heartbeat by LRU position
+    double *c_hb = nullptr;                  // per tick: heartbeat of a live LRU position
+    bool qaos = false;                       // qfree/qhb[cur] describe the committed queue
     uint8_t *reg = nullptr;
     HbRec *hbe = nullptr;  // {last_heartbeat (NaN: no record), epoch} per slot
     int32_t *log_slot = nullptr;
@@ -340,6 +344,7 @@ int enqueue_tick(fb_ctx *c) {
     a.nbf = nbf;
     a.nbq = nbq;
     // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
+    // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
     a.slots_in_scan = c->split_slots ? 0 : 1;
@@ -356,6 +361,9 @@ int enqueue_tick(fb_ctx *c) {
     a.hbe = c->hbe;
     a.free_in = c->free_[cur];
     a.queue_in = c->queue[cur];
+    a.qaos = (!c->shard && c->qaos) ? 1 : 0;
+    a.qfree_in = c->qfree[cur];
+    a.qhb_in = c->qhb[cur];
     a.touched = c->touched;
     a.post_reg = c->post_reg;
     a.post_flags = c->post_flags;
@@ -383,6 +391,9 @@ int enqueue_tick(fb_ctx *c) {
     a.free_out = c->free_[nxt];
     a.inq_out = c->inq[nxt];
     a.queue_out = c->queue[nxt];
+    a.qfree_out = c->qfree[nxt];
+    a.qhb_out = c->qhb[nxt];
+    a.c_hb = c->c_hb;
     a.orphans = c->orphans;
     a.evicted = c->evicted;
     a.hout = c->hout_dev;
@@ -499,6 +510,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->free_[i], W);
         ap.add(&c->inq[i], W);
         ap.add(&c->queue[i], Wq);
+        if (!shard) {
+            ap.add(&c->qfree[i], Wq);
+            ap.add(&c->qhb[i], Wq);
+        }
     }
     ap.add(&c->reg, W);
     ap.add(&c->hbe, W);
@@ -524,6 +539,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
     ap.add(&c->c_arr, Qlog);
+    if (!shard) ap.add(&c->c_hb, Qlog);
     ap.add(&c->qbmax, (size_t)cdiv(Qlog, kBS));
     ap.add(&c->qbm_raw, (size_t)cdiv(Qlog, kBS));
     ap.add(&c->csum, (size_t)cdiv(Qlog, kBS));
@@ -643,7 +659,18 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
     }
-    if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
+    if (queue_len) {
+        HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
+        std::vector<int32_t> qf((size_t)queue_len);
+        std::vector<double> qh((size_t)queue_len);
+        for (int64_t i = 0; i < queue_len; ++i) {
+            qf[i] = free_processes[queue[i]];
+            qh[i] = last_heartbeat[queue[i]];
+        }
+        HIPCHK(c, hipMemcpy(c->qfree[0], qf.data(), (size_t)queue_len * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->qhb[0], qh.data(), (size_t)queue_len * 8, hipMemcpyHostToDevice));
+    }
+    c->qaos = true;
     if (log_len) HIPCHK(c, hipMemcpy(c->log_slot, log_slot, (size_t)log_len * 4, hipMemcpyHostToDevice));
     c->W = n_workers;
     c->Qn = queue_len;

@@ -105,6 +105,11 @@ struct TickArgs {
     const HbRec *hbe;
     const int32_t *free_in;
     const int32_t *queue_in;
+    // free_processes / last_heartbeat of the committed queue, by LRU position
+    // (written by the previous tick's emit; valid when qaos = 1)
+    int qaos;
+    const int32_t *qfree_in;
+    const double *qhb_in;
     // this tick's message results
     const uint32_t *touched;
     const uint8_t *post_reg, *post_flags;
@@ -127,6 +132,9 @@ struct TickArgs {
     int32_t *free_out;  // next free_processes; INT32_MIN for slots without a live record
     uint8_t *inq_out;
     int32_t *queue_out;
+    int32_t *qfree_out;
+    double *qhb_out;
+    double *c_hb;    // last_heartbeat of a live LRU position (k_scan -> emit)
     int64_t *orphans;
     int32_t *evicted;
     HostOut *hout;

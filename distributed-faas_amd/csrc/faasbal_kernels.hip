@@ -57,6 +57,13 @@ __device__ __forceinline__ int popc_lt(uint64_t m) {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0));
 }
 
+// Workgroup barrier for LDS traffic only.  __syncthreads() also waits for every
+// outstanding global store of the wave (vmcnt(0)); no kernel here reads another
+// thread's global stores within a launch, so a barrier need not wait for them.
+__device__ __forceinline__ void lds_barrier() {
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // ---- DPP wave primitives (gfx9 row_shr / row_bcast): no LDS crossbar traffic,
 // unlike __shfl_* which lowers to ds_bpermute.
 template <int CTRL, int ROWM, int BANKM, bool BC>
@@ -87,11 +94,24 @@ __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
     return (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_max_u32(v), 63);
 }
+// Sum over the lanes that share (lane mod cls), cls in {8, 16, 32}; every lane
+// gets its class total.  DPP row_ror:8 pairs lanes i, i^8 inside a 16-lane row;
+// the gfx950 permlane16/32 swaps exchange whole rows / halves without LDS.
+__device__ __forceinline__ uint32_t class_sum_u32(uint32_t v, int cls) {
+    if (cls <= 8) v += dpp<0x128, 0xf, 0xf, false>(v);
+    if (cls <= 16) {
+        const auto q = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+        v = q[0] + q[1];
+    }
+    const auto p = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+    return p[0] + p[1];
+}
+
 // Block-wide exclusive prefix sum (u32), one value per thread.
 __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t *lds4, uint32_t &total) {
     const uint32_t x = wave_incl_scan_u32(v);
     if (lane_id() == 63) lds4[wave_id()] = x;
-    __syncthreads();
+    lds_barrier();
     uint32_t pre = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
@@ -99,7 +119,7 @@ __device__ __forceinline__ uint32_t block_excl_scan_u32(uint32_t v, uint32_t *ld
         pre += (w < wave_id()) ? t : 0u;
         tot += t;
     }
-    __syncthreads();
+    lds_barrier();
     total = tot;
     return pre + x - v;
 }
@@ -138,6 +158,12 @@ __global__ __launch_bounds__(kBS) void k_selftest(uint32_t *err, uint32_t seed) 
     uint32_t tot;
     bad += block_excl_scan_u32(v, l4, tot) != bpre;
     bad += tot != tot_ref;
+    for (int cls = 8; cls <= 32; cls <<= 1) {
+        uint32_t cref = 0;
+        for (int i = wb; i < wb + 64; ++i)
+            if (((i - wb) & (cls - 1)) == (lane_id() & (cls - 1))) cref += vals[i];
+        bad += class_sum_u32(v, cls) != cref;
+    }
     if (bad) atomicAdd(err, bad);
 }
 
@@ -151,7 +177,7 @@ __device__ __forceinline__ T block_excl_scan(T v, T *lds4, T &total) {
         if (lane_id() >= d) x += y;
     }
     if (lane_id() == 63) lds4[wave_id()] = x;
-    __syncthreads();
+    lds_barrier();
     T pre = 0, tot = 0;
 #pragma unroll
     for (int w = 0; w < kWaves; ++w) {
@@ -159,7 +185,7 @@ __device__ __forceinline__ T block_excl_scan(T v, T *lds4, T &total) {
         pre += (w < wave_id()) ? t : (T)0;
         tot += t;
     }
-    __syncthreads();
+    lds_barrier();
     total = tot;
     return pre + x - v;
 }
@@ -172,11 +198,11 @@ __device__ __forceinline__ T block_reduce_max(T v, T *lds4) {
         v = v > y ? v : y;
     }
     if (lane_id() == 0) lds4[wave_id()] = v;
-    __syncthreads();
+    lds_barrier();
     T m = lds4[0];
 #pragma unroll
     for (int w = 1; w < kWaves; ++w) m = m > lds4[w] ? m : lds4[w];
-    __syncthreads();
+    lds_barrier();
     return m;
 }
 
@@ -463,7 +489,7 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
     if (!a.slots_in_scan && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
     const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
     if (lane_id() == 0) l4[wave_id()] = ev;
-    __syncthreads();
+    lds_barrier();
     if (threadIdx.x == 0) a.wcnt[blk] = l4[0] + l4[1] + l4[2] + l4[3];
 }
 
@@ -555,7 +581,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
                 const int i = threadIdx.x + k * kBS;
                 if (i < n4) reinterpret_cast<uint4 *>(dyn)[i] = t[k];
             }
-            __syncthreads();
+            lds_barrier();
             dm = dyn;
         }
 #pragma unroll
@@ -579,7 +605,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
         const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
         if (lane_id() == 0) l4[wave_id()] = wv;
-        __syncthreads();
+        lds_barrier();
         if (threadIdx.x == 0) {
             const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
             a.fcnt[b] = n;
@@ -606,15 +632,27 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
             oc = (c > 0 && own_slot(a, lq_slot(a, pos)) >= 0) ? c : 0;
         }
     } else if (pos < a.Qlog) {
-        const int s = lq_slot(a, pos);
-        const int ls = s >= 0 ? own_slot(a, s) : -1;
+        int s = -1, ls = -1;
         int32_t raw = INT32_MIN;  // INT32_MIN: no live record (or not mine)
-        if (ls >= 0) {
-            if (a.slots_in_scan) {
-                const Cur cu = cur_slot(a, ls);
-                raw = (cu.reg && !is_dead(a, cu)) ? cu.fr : INT32_MIN;
-            } else {
-                raw = a.free_out[ls];
+        double hbq = 0.0;
+        if (a.qaos && a.E == 0 && !a.shard) {
+            // no messages this tick: the committed queue's records ride along by position
+            // (queued slots are registered), one coalesced pass instead of slot gathers
+            hbq = a.qhb_in[pos];
+            const int32_t fq = a.qfree_in[pos];
+            raw = ((a.now - hbq) > a.tte) ? INT32_MIN : fq;
+        } else {
+            s = lq_slot(a, pos);
+            ls = s >= 0 ? own_slot(a, s) : -1;
+            if (ls >= 0) {
+                if (a.slots_in_scan) {
+                    const Cur cu = cur_slot(a, ls);
+                    raw = (cu.reg && !is_dead(a, cu)) ? cu.fr : INT32_MIN;
+                    hbq = cu.hb;
+                } else {
+                    raw = a.free_out[ls];
+                    hbq = a.hbe[ls].hb;
+                }
             }
         }
         // an old queue entry moved to the front, re-appended or removed by this tick's messages
@@ -623,6 +661,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
             raw = INT32_MIN;
         if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
         a.c_arr[pos] = raw;
+        if (!a.shard) a.c_hb[pos] = hbq;
         if (a.shard == 1) a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
     }
     STAMP(a, SO, 1);
@@ -658,7 +697,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
                 if (a.fused && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
                     a.segcnt[(size_t)(4 * b + wave_id()) * a.R + r0 + lane_id()] = cnt;
             }
-            __syncthreads();
+            lds_barrier();
             uint32_t t = 0;
             if ((int)threadIdx.x < rn) {
                 t = wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
@@ -669,10 +708,10 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
                 // sum_r count(c > r) over r < R = sum of min(c, R): the block's capacity when c <= R
                 const uint32_t ts = wave_sum_u32(t);
                 if (lane_id() == 0) l4[wave_id()] = ts;
-                __syncthreads();
+                lds_barrier();
                 csum += (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
             }
-            __syncthreads();
+            lds_barrier();
         }
     }
     if (threadIdx.x == 0) {
@@ -788,6 +827,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         const int b = bid;
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
         int32_t raw = INT32_MIN;
+        double hbp = 0.0;
         int s = -1;
         int64_t O, nev = 0, cap;
         int maxc, bm;
@@ -798,6 +838,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
             // ---- totals and the scanned round table from k_plan
             if (pos < a.Qlog) {
                 raw = a.c_arr[pos];
+                hbp = a.c_hb[pos];
                 s = lq_slot(a, pos);
             }
             bm = a.qbm_raw[b];
@@ -821,11 +862,11 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
                 if (lane == 0) misc[w] = k_w;
                 S_l[threadIdx.x + 1] = S1;
                 if (threadIdx.x == 0) S_l[0] = carry;
-                __syncthreads();
+                lds_barrier();
                 const int k = misc[0] + misc[1] + misc[2] + misc[3];
                 L += k;
                 S_L = S_l[k];
-                __syncthreads();
+                lds_barrier();
                 if (k < kBS) break;
                 carry += (int64_t)tot;
             }
@@ -886,7 +927,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
                 }
                 E_.wc[w][g * 64 + lane] = cnt;
             }
-            __syncthreads();
+            lds_barrier();
             STAMP(a, SO, 6);
             // rank base of every (wave, round) and its task index base
             for (int e = threadIdx.x; e < kWaves * rn; e += kBS) {
@@ -898,7 +939,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
                 E_.wbase[ww][i] = (int32_t)rb;
                 E_.wpos[ww][i] = (r <= L) ? (int32_t)(Sr + rb) : 0;
             }
-            __syncthreads();
+            lds_barrier();
             STAMP(a, SO, 7);
             // full rounds: every active lane takes one task; the wave's task index
             // bases for 64 rounds sit in one register (lane i: round rc + i0 + i)
@@ -937,7 +978,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
                 const int i1 = L + 1 - rc;
                 exL1 = (int64_t)E_.wbase[w][i1] + popc_lt(__ballot(c > L + 1));
             }
-            __syncthreads();
+            lds_barrier();
         }
         STAMP(a, SO, 4);
         if (c > 0) {
@@ -953,6 +994,8 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
             }
             if (np >= 0) {
                 a.queue_out[np] = s;
+                a.qfree_out[np] = raw - (int32_t)n_q;
+                a.qhb_out[np] = hbp;
                 a.inq_out[s] = 1;
             }
         }
@@ -1017,6 +1060,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
         // ---- every load in flight at once (clamped indices, no branches)
         const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
         const int32_t raw0 = a.c_arr[pq];
+        const double hb0 = a.c_hb[pq];
         const int s0 = a.E == 0 ? a.queue_in[pq] : lq_slot(a, pq);
         const uint4 *tab = reinterpret_cast<const uint4 *>(a.qcnt);
         uint4 tv[kTabLd2];
@@ -1078,12 +1122,10 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
             pp[0] += v.x & before; pp[1] += v.y & before; pp[2] += v.z & before; pp[3] += v.w & before;
         }
         // lanes of one class (lane mod cls) hold partials of the same 4 rows
-        for (int d = cls; d < 64; d <<= 1) {
 #pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                pp[u] += __shfl_xor(pp[u], d, 64);
-                tt[u] += __shfl_xor(tt[u], d, 64);
-            }
+        for (int u = 0; u < 4; ++u) {
+            pp[u] = class_sum_u32(pp[u], cls);
+            tt[u] = class_sum_u32(tt[u], cls);
         }
         if (lane < cls) {
 #pragma unroll
@@ -1102,7 +1144,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
             red[w][2] = co;
             red[w][3] = mo;
         }
-        __syncthreads();
+        lds_barrier();
         // round rows: this block's prefix and the total, summed over the threads of row r's class
         if ((int)threadIdx.x < R) {
             const int r = threadIdx.x, c0 = r >> 2, u = r & 3;
@@ -1113,7 +1155,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
         const int64_t nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
         int64_t cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
         const int maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
-        __syncthreads();
+        lds_barrier();
         STAMP(a, SO, 1);
         const int rlim = maxc < R ? maxc : R;
         if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
@@ -1215,6 +1257,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
             }
             if (np >= 0) {
                 a.queue_out[np] = s;
+                a.qfree_out[np] = raw - (int32_t)n_q;
+                a.qhb_out[np] = hb0;
                 a.inq_out[s] = 1;
             }
         }
@@ -1229,7 +1273,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
         peeled_sum(a.fcnt, b, b, tot, pre);
         const uint32_t ws = wave_sum_u32((uint32_t)pre);
         if (lane == 0) red[w][0] = ws;
-        __syncthreads();
+        lds_barrier();
         const int64_t off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
         uint32_t tt;
         const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tt);
@@ -1249,7 +1293,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
     peeled_sum(a.wcnt, b, b, tot, pre);
     const uint32_t ws = wave_sum_u32((uint32_t)pre);
     if (lane == 0) red[w][0] = ws;
-    __syncthreads();
+    lds_barrier();
     const int64_t off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
     uint32_t tt;
     const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tt);
@@ -1310,11 +1354,11 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 if (lane == 0) misc[w] = k_w;
                 S_l[threadIdx.x + 1] = S1;
                 if (threadIdx.x == 0) S_l[0] = carry;
-                __syncthreads();
+                lds_barrier();
                 const int k = misc[0] + misc[1] + misc[2] + misc[3];
                 L += k;
                 S_L = S_l[k];
-                __syncthreads();
+                lds_barrier();
                 if (k < kBS) break;
                 carry += (int64_t)tot;
             }
@@ -1376,7 +1420,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 E_.wc[w][g * 64 + lane] = cnt;
                 E_.owc[w][g * 64 + lane] = ocnt;
             }
-            __syncthreads();
+            lds_barrier();
             for (int e = threadIdx.x; e < kWaves * rn; e += kBS) {
                 const int ww = e / rn, i = e - ww * rn;
                 const int r = rc + i;
@@ -1390,7 +1434,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 E_.wpos[ww][i] = (r <= L) ? (int32_t)(S_l[i] + rb) : 0;
                 E_.opos[ww][i] = (r <= L) ? (int32_t)(So_l[i] + orb) : 0;
             }
-            __syncthreads();
+            lds_barrier();
             int rfull = L < bm ? L : bm;
             rfull = rfull < rc + rn ? rfull : rc + rn;
             int32_t *const lslot = a.log_slot + a.head_local;
@@ -1427,7 +1471,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 const int i1 = L + 1 - rc;
                 exL1 = (int64_t)E_.wbase[w][i1] + popc_lt(__ballot(c > L + 1));
             }
-            __syncthreads();
+            lds_barrier();
         }
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
