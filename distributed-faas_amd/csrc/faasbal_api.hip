@@ -81,7 +81,9 @@ struct fb_ctx {
     unsigned long long *dbg = nullptr;             // diagnostic stamps
     size_t dbg_n = 0;
     int force_plan = 0;
-    int split_slots = 0;
+    int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
+    int ncu = 0, max_lds = 0;
+    int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
     int old_emit = 0;
     int dbg_stop = 0;     // FAASBAL_DBG_STOP=n: timing probe (results invalid)     // FAASBAL_OLD_EMIT=1: 256-thread k_emit on the fused path (A/B switch)  // FAASBAL_SPLIT_SLOTS=1: separate k_slots launch + died bitmap (A/B switch)
     void *arena = nullptr;    // every fixed-size device buffer, carved from one allocation
@@ -347,7 +349,17 @@ int enqueue_tick(fb_ctx *c) {
     // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
-    a.slots_in_scan = c->split_slots ? 0 : 1;
+    // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
+    // (2 MB of records) those gathers miss L2, so k_slots first writes the
+    // died bitmap (W/8 bytes, L2-resident) and the scan tests bits instead
+    a.slots_in_scan = (c->split_slots > 0 || (c->split_slots < 0 && W > kLdsBitmapSlots)) ? 0 : 1;
+    // ... or better, while the bitmap fits in one workgroup's LDS: the W-role of
+    // k_scan writes it and k_logscan tests every entry against an LDS copy
+    const size_t bm_bytes = (size_t)(((W + 63) / 64 + 1) / 2 + 1) * 16;
+    a.f_sep = (head > 0 && (c->logscan > 0 || (c->logscan < 0 && W > kLdsBitmapSlots)) &&
+               bm_bytes <= (size_t)c->max_lds && !(c->shard && c->phase == 2)) ? 1 : 0;
+    if (a.f_sep) a.slots_in_scan = 1;
+    const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
     a.dbg_stop = c->dbg_stop;
     a.tick = c->tick;
     a.now = c->l_now;
@@ -412,7 +424,7 @@ int enqueue_tick(fb_ctx *c) {
         a.oA = c->oA;
     }
     {
-        const size_t need = (size_t)3 * (nbw + nbf + nbq) * 16 + 16;
+        const size_t need = (size_t)4 * (nbw + nbf + nbq) * 16 + 16;
         if (need > c->dbg_n) {
             hipFree(c->dbg);
             c->dbg = nullptr;
@@ -427,8 +439,14 @@ int enqueue_tick(fb_ctx *c) {
             Timer t(c, "slots");
             launch_slots(a, t.st());
         }
-        Timer t(c, "scan");
-        launch_scan(a, t.st());
+        {
+            Timer t(c, "scan");
+            launch_scan(a, t.st());
+        }
+        if (a.f_sep) {
+            Timer t(c, "logscan");
+            launch_logscan(a, ls_grid, t.st());
+        }
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
@@ -454,6 +472,10 @@ int enqueue_tick(fb_ctx *c) {
     {
         Timer t(c, "scan");
         launch_scan(a, t.st());
+    }
+    if (a.f_sep) {
+        Timer t(c, "logscan");
+        launch_logscan(a, ls_grid, t.st());
     }
     if (!a.fused) {
         Timer t(c, "plan");
@@ -573,6 +595,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && hipHostGetDevicePointer((void **)&c->hout_dev, c->hout, 0) != hipSuccess) rc = FB_EHIP;
     if (!rc) memset(c->hout, 0, sizeof(HostOut));
     if (!rc && getenv("FAASBAL_FORCE_PLAN")) c->force_plan = atoi(getenv("FAASBAL_FORCE_PLAN"));
+    if (!rc && getenv("FAASBAL_LOGSCAN")) c->logscan = atoi(getenv("FAASBAL_LOGSCAN"));
+    if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
+                hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
+        rc = FB_EHIP;
     if (!rc && getenv("FAASBAL_SPLIT_SLOTS")) c->split_slots = atoi(getenv("FAASBAL_SPLIT_SLOTS"));
     if (!rc && getenv("FAASBAL_DBG_STOP")) c->dbg_stop = atoi(getenv("FAASBAL_DBG_STOP"));
     if (!rc && hipHostMalloc(&c->h_stage, E * 32, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;

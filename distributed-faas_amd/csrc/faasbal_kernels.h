@@ -15,6 +15,7 @@ constexpr int kRFused = 128;       // fused tick: round table of at most 128 row
 constexpr int kTabLd = 16;         // ... read by at most 16 int4 loads per thread
 constexpr int kPeel = 4;           // fused tick: block-count arrays of at most 4*256 entries
 constexpr int kLdsBitmapSlots = 1 << 17;  // died bitmap staged in LDS up to 128K slots (16 KB)
+constexpr int kLsBS = 1024;        // k_logscan: one 16-wave workgroup per CU
 
 // event kinds / status (include/faasbal.h)
 constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3;
@@ -96,6 +97,7 @@ struct TickArgs {
     int fused;       // 1: k_emit derives the cross-block prefixes itself (no k_plan launch)
     int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
     int slots_in_scan;
+    int f_sep;        // 1: log role in its own launch (k_logscan, died bitmap in LDS); k_scan W-role writes the bitmap
     int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;
     double now, tte;
@@ -182,6 +184,7 @@ void launch_ev_apply(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
+void launch_logscan(const TickArgs &a, int grid, Stream st);
 void launch_plan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);

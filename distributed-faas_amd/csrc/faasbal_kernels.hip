@@ -370,17 +370,26 @@ struct Cur {
 
 __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
     Cur c;
-    c.t = a.E > 0 && a.touched[s] == a.tick;
     c.reg0 = a.reg[s];
-    if (c.t) {
-        c.reg = a.post_reg[s];
-        c.hb = a.post_hb[s];
-        c.fr = a.post_free[s];
-        c.flags = a.post_flags[s];
+    const double hb0 = a.hbe[s].hb;
+    const int32_t fr0 = a.free_in[s];
+    if (a.E > 0) {
+        // message tick: committed and post-message records loaded together and
+        // selected afterwards (a load behind the touched test would wait for it)
+        const uint32_t tk = a.touched[s];
+        const uint8_t pr = a.post_reg[s], pf = a.post_flags[s];
+        const double ph = a.post_hb[s];
+        const int32_t pfr = a.post_free[s];
+        c.t = tk == a.tick;
+        c.reg = c.t ? pr : c.reg0;
+        c.hb = c.t ? ph : hb0;
+        c.fr = c.t ? pfr : fr0;
+        c.flags = c.t ? pf : 0;
     } else {
+        c.t = false;
         c.reg = c.reg0;
-        c.hb = a.hbe[s].hb;
-        c.fr = a.free_in[s];
+        c.hb = hb0;
+        c.fr = fr0;
         c.flags = 0;
     }
     return c;
@@ -391,11 +400,12 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
 __device__ __forceinline__ bool is_dead(const TickArgs &a, const Cur &c) { return c.reg && ((a.now - c.hb) > a.tte); }
 
 // Global slot at logical LRU position pos of fronts ++ queue ++ backs, or -1.
+// One load from the list the position falls in (no branch per list).
 __device__ __forceinline__ int lq_slot(const TickArgs &a, int64_t pos) {
-    if (pos < a.E) return a.front_list[pos] - 1;
-    pos -= a.E;
-    if (pos < a.Qn) return a.queue_in[pos];
-    return a.back_list[pos - a.Qn] - 1;
+    const bool fr = pos < a.E, qu = !fr && pos < a.E + a.Qn;
+    const int32_t *p = fr ? a.front_list : (qu ? a.queue_in : a.back_list);
+    const int64_t i = fr ? pos : (qu ? pos - a.E : pos - a.E - a.Qn);
+    return p[i] - (qu ? 0 : 1);
 }
 // Local index of global slot s if this rank owns it, else -1 (one GPU: s itself).
 __device__ __forceinline__ int own_slot(const TickArgs &a, int s) {
@@ -486,7 +496,8 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         a.inq_out[s] = 0;
     }
     const uint64_t dm = __ballot(died_start);
-    if (!a.slots_in_scan && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
+    if ((!a.slots_in_scan || a.f_sep) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W)
+        a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
     const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
     if (lane_id() == 0) l4[wave_id()] = ev;
     lds_barrier();
@@ -521,7 +532,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
     __shared__ uint32_t wc[kWaves][kBS];
     const int bid = blockIdx.x;
     const int SO = a.nbw;
-    const int nbf = a.shard == 2 ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
+    const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
     STAMP(a, SO, 0);
     if (bid < nbf) {
         // ---- F-role: orphan flags of log entries [b*2048 + t*8, +8)
@@ -595,12 +606,14 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
         if (a.slots_in_scan) {
             flags = died;
         } else if (died) {
+            uint32_t ep[kFItems];  // all gathers in flight (no per-entry branch + wait)
 #pragma unroll
-            for (int j = 0; j < kFItems; ++j)
-                if ((died >> j) & 1u) {
-                    const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
-                    if (seq >= (uint64_t)a.hbe[v[j]].epoch) flags |= 1u << j;
-                }
+            for (int j = 0; j < kFItems; ++j) ep[j] = a.hbe[((died >> j) & 1u) ? v[j] : 0].epoch;
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) {
+                const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
+                flags |= (((died >> j) & 1u) & (uint32_t)(seq >= (uint64_t)ep[j])) << j;
+            }
         }
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
         const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
@@ -723,31 +736,174 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
     STAMP(a, SO, 15);
 }
 
+// ------------------------------------------------------------ k_logscan
+// The log role of k_scan as its own launch for large tables (a.f_sep): past 128K
+// slots a gather per in-flight entry -- into the 16-byte records or the global
+// bitmap -- costs a 64-byte L2 request each.  One 16-wave workgroup per CU
+// instead copies the whole died bitmap (W/8 bytes, <= the 160 KB of LDS) once,
+// then every wave flags the orphans of whole 2048-entry tiles alone (lane: 4
+// groups of 8 consecutive entries, 8 int4 loads in flight), with k_scan's
+// per-tile ofl / fcnt layout so k_emit's orphan compaction is unchanged.
+__global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long bm[];
+    const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows
+    STAMP(a, SO, 0);
+    const int n4 = (((a.W + 63) >> 6) + 1) >> 1;
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
+    for (int i0 = 0; i0 < n4; i0 += kLsBS * 8) {
+        uint4 t[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kLsBS + (int)threadIdx.x;
+            t[k] = src[i < n4 ? i : n4 - 1];
+        }
+        // stores past the bitmap go to one spare slot, not behind a branch: a
+        // guarded store lets the compiler sink its load into the branch, one
+        // round trip per load
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kLsBS + (int)threadIdx.x;
+            reinterpret_cast<uint4 *>(bm)[i < n4 ? i : n4] = t[k];
+        }
+    }
+    __syncthreads();
+    STAMP(a, SO, 1);
+    const int lane = lane_id();
+    constexpr int nw = kLsBS / 64;
+    const int64_t nlog = a.shard ? a.head_local : a.head_in;
+    for (int b = blockIdx.x * nw + (int)(threadIdx.x >> 6); b < a.nbf; b += gridDim.x * nw) {
+        int32_t v[4][kFItems];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int64_t base = (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems;
+            if (base + kFItems <= nlog) {
+                const int4 x0 = *reinterpret_cast<const int4 *>(a.log_slot + base);
+                const int4 x1 = *reinterpret_cast<const int4 *>(a.log_slot + base + 4);
+                v[k][0] = x0.x; v[k][1] = x0.y; v[k][2] = x0.z; v[k][3] = x0.w;
+                v[k][4] = x1.x; v[k][5] = x1.y; v[k][6] = x1.z; v[k][7] = x1.w;
+            } else {
+#pragma unroll
+                for (int j = 0; j < kFItems; ++j) v[k][j] = (base + j < nlog) ? a.log_slot[base + j] : -1;
+            }
+        }
+        // died bits from LDS, then every epoch gather of a died entry in flight at
+        // once (a died slot's entry is an orphan unless it predates the
+        // registration: sequence below its epoch)
+        uint32_t died[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            died[k] = 0;
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) {
+                int sj = v[k][j];
+                if (a.shard && sj >= 0) sj -= a.slot_base;  // log slots are global ids
+                v[k][j] = sj;
+                const int sc = sj < 0 ? 0 : sj;
+                died[k] |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
+            }
+        }
+        uint32_t ep[4][kFItems];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j) ep[k][j] = a.hbe[((died[k] >> j) & 1u) ? v[k][j] : 0].epoch;
+        // sequence numbers: the entry index, or (sharded) the global sequence of
+        // the local entry, loaded as a whole before any use
+        uint32_t sq[4][kFItems];
+        if (a.shard) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int64_t base = (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems;
+#pragma unroll
+                for (int j = 0; j < kFItems; ++j) sq[k][j] = a.lseq[min(base + j, nlog > 0 ? nlog - 1 : 0)];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+#pragma unroll
+                for (int j = 0; j < kFItems; ++j)
+                    sq[k][j] = (uint32_t)((int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems + j);
+        }
+        uint32_t cnt = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t flags = 0;
+#pragma unroll
+            for (int j = 0; j < kFItems; ++j)
+                flags |= (((died[k] >> j) & 1u) & (uint32_t)(sq[k][j] >= ep[k][j])) << j;
+            a.ofl[(size_t)b * kBS + k * 64 + lane] = (uint8_t)flags;
+            cnt += (uint32_t)__popc(flags);
+        }
+        cnt = wave_sum_u32(cnt);
+        if (lane == 0) {
+            a.fcnt[b] = cnt;
+            if (a.shard && cnt) atomicAdd(&a.xrec[a.rank * 4 + 0], (unsigned long long)cnt);
+        }
+    }
+    STAMP(a, SO, 15);
+}
+
 // ------------------------------------------------------------ k_plan (large grids only)
+// Exclusive scan of n counts cnt[i * cs] into pre[i * ps] by one workgroup;
+// returns the total.  Every thread owns a contiguous run of ceil(n / 256)
+// entries and issues its loads 16 at a time, so the whole row costs one block
+// scan instead of one per 256 entries.
+__device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *__restrict__ cnt, size_t cs, int n,
+                                                            int64_t *__restrict__ pre, size_t ps,
+                                                            unsigned long long *l4) {
+    const int per = (n + kBS - 1) / kBS;
+    const int i0 = (int)threadIdx.x * per;
+    unsigned long long sum = 0;
+    for (int j0 = 0; j0 < per; j0 += 16) {
+        // unconditional loads of clamped indices, masked afterwards: a guarded
+        // load compiles to a branch with its own wait, one round trip per entry
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = min(i0 + j0 + j, n - 1);
+            v[j] = cnt[(size_t)i * cs];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += (j0 + j < per && i0 + j0 + j < n) ? v[j] : 0u;
+    }
+    unsigned long long tot;
+    unsigned long long run = block_excl_scan<unsigned long long>(sum, l4, tot);
+    for (int j0 = 0; j0 < per; j0 += 16) {
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = min(i0 + j0 + j, n - 1);
+            v[j] = cnt[(size_t)i * cs];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = i0 + j0 + j;
+            if (j0 + j < per && i < n) {
+                pre[(size_t)i * ps] = (int64_t)run;
+                run += v[j];
+            }
+        }
+    }
+    return tot;
+}
+
 // wg 0: orphan block offsets + O; wg 1: evicted block offsets; wg 2: max c and
 // capacity; wg 3+r: exclusive scan of round r's counts across queue blocks.
 __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     __shared__ unsigned long long l4[kWaves];
     __shared__ int32_t m4[kWaves];
     const int bid = blockIdx.x;
+    const int SO = 3 * (a.nbw + a.nbf + a.nbq) + 512;  // diagnostic stamp rows
+    STAMP(a, SO, 0);
     if (bid <= 1) {
-        const uint32_t *cnt = bid == 0 ? a.fcnt : a.wcnt;
-        int64_t *pre = bid == 0 ? a.fpre : a.wpre;
-        const int n = bid == 0 ? a.nbf : a.nbw;
-        unsigned long long carry = 0;
-        for (int base = 0; base < n; base += kBS) {
-            const int i = base + threadIdx.x;
-            unsigned long long v = i < n ? cnt[i] : 0ull, tot;
-            const unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
-            if (i < n) pre[i] = (int64_t)(carry + ex);
-            carry += tot;
-        }
+        const unsigned long long tot = bid == 0 ? run_excl_scan(a.fcnt, 1, a.nbf, a.fpre, 1, l4)
+                                                : run_excl_scan(a.wcnt, 1, a.nbw, a.wpre, 1, l4);
         if (threadIdx.x == 0) {
             if (bid == 0) {
-                a.P->O_local = (int64_t)carry;
-                if (!a.shard) a.P->O = (int64_t)carry;
+                a.P->O_local = (int64_t)tot;
+                if (!a.shard) a.P->O = (int64_t)tot;
             } else {
-                a.P->n_evicted = (int64_t)carry;
+                a.P->n_evicted = (int64_t)tot;
             }
         }
         return;
@@ -770,9 +926,21 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     if (bid == 2) {
         int32_t mx = 0;
         unsigned long long sum = 0;
-        for (int i = threadIdx.x; i < a.nbq; i += kBS) {
-            mx = a.qbm_raw[i] > mx ? a.qbm_raw[i] : mx;
-            sum += a.csum[i];
+        for (int i0 = 0; i0 < a.nbq; i0 += 8 * kBS) {
+            int32_t m[8];
+            unsigned long long cs[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const int i = i0 + k * kBS + (int)threadIdx.x;
+                m[k] = a.qbm_raw[min(i, a.nbq - 1)];
+                cs[k] = a.csum[min(i, a.nbq - 1)];
+            }
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                const bool ok = i0 + k * kBS + (int)threadIdx.x < a.nbq;
+                mx = (ok && m[k] > mx) ? m[k] : mx;
+                sum += ok ? cs[k] : 0ull;
+            }
         }
         mx = block_reduce_max<int32_t>(mx, m4);
         unsigned long long tot;
@@ -790,16 +958,9 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     if (r >= a.R || (mine && !a.shard)) return;
     const uint32_t *cnt = mine ? a.ocnt : a.qcnt;
     int64_t *pre = mine ? a.opre : a.qpre;
-    unsigned long long carry = 0;
-    for (int base = 0; base < a.nbq; base += kBS) {
-        const int b = base + threadIdx.x;
-        unsigned long long v = 0, tot;
-        if (b < a.nbq) v = cnt[(size_t)b * a.R + r];
-        const unsigned long long ex = block_excl_scan<unsigned long long>(v, l4, tot);
-        if (b < a.nbq) pre[(size_t)b * a.R + r] = (int64_t)(carry + ex);
-        carry += tot;
-    }
-    if (threadIdx.x == 0) (mine ? a.oA : a.A)[r] = (int64_t)carry;
+    const unsigned long long tot = run_excl_scan(cnt + r, (size_t)a.R, a.nbq, pre + r, (size_t)a.R, l4);
+    if (threadIdx.x == 0) (mine ? a.oA : a.A)[r] = (int64_t)tot;
+    STAMP(a, SO, 15);
 }
 
 // ------------------------------------------------------------ k_emit
@@ -1021,7 +1182,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
     // ---- evicted compaction, ascending slot
     const int b = bid - a.nbq - a.nbf;
     const int s = b * kBS + threadIdx.x;
-    const uint32_t e = (s < a.W && (a.st[s] & kStEvicted)) ? 1u : 0u;
+    const uint32_t e = (s < a.W) & ((a.st[min(s, a.W > 0 ? a.W - 1 : 0)] & kStEvicted) != 0);
     const int64_t off = a.wpre[b];
     uint32_t tot;
     const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tot);
@@ -1288,7 +1449,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
     // ---- evicted compaction, ascending slot
     const int b = bid - a.nbq - a.nbf;
     const int sl = b * kBS + threadIdx.x;
-    const uint32_t e = (sl < a.W && (a.st[sl] & kStEvicted)) ? 1u : 0u;
+    const uint32_t e = (sl < a.W) & ((a.st[min(sl, a.W > 0 ? a.W - 1 : 0)] & kStEvicted) != 0);
     unsigned long long tot, pre;
     peeled_sum(a.wcnt, b, b, tot, pre);
     const uint32_t ws = wave_sum_u32((uint32_t)pre);
@@ -1510,7 +1671,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     // ---- own evicted slots, as global ids
     const int b = bid - a.nbq - a.nbf;
     const int s = b * kBS + threadIdx.x;
-    const uint32_t e = (s < a.W && (a.st[s] & kStEvicted)) ? 1u : 0u;
+    const uint32_t e = (s < a.W) & ((a.st[min(s, a.W > 0 ? a.W - 1 : 0)] & kStEvicted) != 0);
     uint32_t tot;
     const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tot);
     if (e) a.evicted[a.wpre[b] + ex] = a.slot_base + s;
@@ -1564,7 +1725,12 @@ void launch_slots(const TickArgs &a, Stream st) {
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
     const int nbw = (a.shard == 2 || !a.slots_in_scan) ? 0 : a.nbw;
-    hipExtLaunchKernelGGL(k_scan, dim3((a.shard == 2 ? 0 : a.nbf) + nbw + a.nbq), dim3(kBS), a.shard == 2 ? 0 : lds, st.s, st.e0, st.e1, 0, a);
+    const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;
+    hipExtLaunchKernelGGL(k_scan, dim3(nbf + nbw + a.nbq), dim3(kBS), nbf ? lds : 0, st.s, st.e0, st.e1, 0, a);
+}
+void launch_logscan(const TickArgs &a, int grid, Stream st) {
+    const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
+    hipExtLaunchKernelGGL(k_logscan, dim3(grid), dim3(kLsBS), lds, st.s, st.e0, st.e1, 0, a);
 }
 void launch_plan(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -248,3 +248,48 @@ def test_golden_plan_path(force_plan):
 def test_device_primitives_selftest():
     g = GpuBalancer(16, 16)
     assert g.selftest() == 0
+
+
+@pytest.fixture
+def logscan(monkeypatch):
+    """Route the log role through k_logscan (died bitmap in LDS), the default past 128K slots."""
+    monkeypatch.setenv("FAASBAL_LOGSCAN", "1")
+
+
+@pytest.fixture
+def split_slots(monkeypatch):
+    """Separate k_slots launch + global died bitmap (tables too large for k_logscan's LDS)."""
+    monkeypatch.setenv("FAASBAL_LOGSCAN", "0")
+    monkeypatch.setenv("FAASBAL_SPLIT_SLOTS", "1")
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_random_multitick_logscan(logscan, seed):
+    test_random_multitick_vs_oracle(seed)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_multitick_logscan_plan(logscan, force_plan, seed):
+    test_random_multitick_vs_oracle(seed + 20)
+
+
+def test_config3_logscan(logscan):
+    test_config3_full_size()
+
+
+def test_churn_logscan(logscan):
+    test_churn_stream_vs_oracle()
+
+
+def test_golden_logscan(logscan):
+    for path in GOLDEN:
+        test_golden_replay(path)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_random_multitick_split_slots(split_slots, seed):
+    test_random_multitick_vs_oracle(seed + 30)
+
+
+def test_config4_split_slots(split_slots):
+    test_config4_single_gpu_full_size()

@@ -145,3 +145,18 @@ def test_sharded_world1_equals_one_gpu():
     a, _ = _group_tick(bals, 1000.0, 10.0, [], [], [], [], [], 60_000)
     b = o.tick(1000.0, 10.0, [], [], [], [], [], 60_000)
     _cmp(bals, o, a, b, 0)
+
+
+@pytest.fixture
+def logscan(monkeypatch):
+    """Phase 1's log role through k_logscan (the default past 128K local slots)."""
+    monkeypatch.setenv("FAASBAL_LOGSCAN", "1")
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_sharded_random_multitick_logscan(logscan, seed):
+    test_sharded_random_multitick(seed)
+
+
+def test_sharded_churn_logscan(logscan):
+    test_sharded_churn()

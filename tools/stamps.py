@@ -28,7 +28,10 @@ def main():
     args = ap.parse_args()
     st = synth.zipf_state(W=args.workers, seed=0)
     W, T = args.workers, args.tasks
-    split = os.environ.get("FAASBAL_SPLIT_SLOTS", "0") == "1"
+    env = os.environ.get("FAASBAL_SPLIT_SLOTS", "-1")
+    split = env == "1" or (env == "-1" and args.workers > (1 << 17))  # the library's auto rule
+    fsep = os.environ.get("FAASBAL_LOGSCAN", "-1") == "1" or (
+        os.environ.get("FAASBAL_LOGSCAN", "-1") == "-1" and args.workers > (1 << 17))
     g = GpuBalancer(W, 2 * len(st["log"]) + T + 16, max_events=1, lib_path=STAMPS_SO)
     g.load(st)
     nbw = -(-W // 256)
@@ -39,12 +42,22 @@ def main():
     for _ in range(args.reps):
         g.launch(1000.0, 10.0, n_pending=T)
         g.wait()
-        d = g.debug_read()[: 3 * G1 * 16].reshape(3 * G1, 16).astype(np.int64)
+        d = g.debug_read()[: 4 * G1 * 16].reshape(4 * G1, 16).astype(np.int64)
         acc.append(d.copy())
     d = np.stack(acc)  # reps x rows x 16
     S = nbw  # k_scan rows start here
     E0 = G1 if split else G1 + nbw  # k_emit rows start here
-    if split:
+    if fsep:
+        # k_scan = W + Q roles, k_logscan (<= 256 rows from 3*G1), k_plan (rows from 3*G1 + 512), k_emit
+        E0 = 2 * nbw + nbf + nbq
+        ls = min(256, -(-nbf // 16))
+        L0, P0 = 3 * G1, 3 * G1 + 512
+        nplan = 3 + 128
+        kernels = {"scan": (S, S + nbw + nbq), "logscan": (L0, L0 + ls), "plan": (P0, P0 + nplan),
+                   "emit": (E0, E0 + G1)}
+        roles = {"scan.W": (S, S + nbw), "scan.Q": (S + nbw, S + nbw + nbq), "logscan": (L0, L0 + ls),
+                 "plan": (P0, P0 + nplan)}
+    elif split:
         kernels = {"slots": (0, nbw), "scan": (S, S + nbf + nbq), "emit": (E0, E0 + G1)}
         roles = {"slots": (0, nbw), "scan.F": (S, S + nbf), "scan.Q": (S + nbf, S + nbf + nbq)}
     else:
@@ -53,7 +66,13 @@ def main():
     roles.update({"emit.Q": (E0, E0 + nbq), "emit.F": (E0 + nbq, E0 + nbq + nbf),
                   "emit.W": (E0 + nbq + nbf, E0 + G1)})
     starts = {}
-    for kern, (lo, hi) in kernels.items():
+    for kern, (lo, hi) in list(kernels.items()):
+        live = (d[:, lo:hi, 13] > 0).all(axis=0)
+        if not live.any():
+            del kernels[kern]
+            continue
+        hi = lo + int(np.nonzero(live)[0].max()) + 1
+        kernels[kern] = (lo, hi)
         ent, ext = d[:, lo:hi, 13], d[:, lo:hi, 14]
         starts[kern] = ent.min(axis=1)
         span = (ext.max(axis=1) - ent.min(axis=1)) / 100.0
@@ -64,6 +83,10 @@ def main():
         gap = (starts[b] - d[:, kernels[a][0]:kernels[a][1], 14].max(axis=1)) / 100.0
         print("gap %s end -> %s first entry: %.2f us" % (a, b, np.median(gap)))
     for name, (lo, hi) in roles.items():
+        live = (d[:, lo:hi, 13] > 0).all(axis=0)
+        if not live.any():
+            continue
+        hi = lo + int(np.nonzero(live)[0].max()) + 1
         x = d[:, lo:hi, :]
         kern = name.split(".")[0]
         off = (x[..., 13] - starts[kern][:, None]) / 100.0
