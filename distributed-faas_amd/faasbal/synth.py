@@ -93,6 +93,69 @@ def random_scenario(seed, W=24, n_ticks=4, max_events=30, max_new=60,
                 ticks=ticks)
 
 
+def random_deque_scenario(seed, W=24, n_ticks=4, max_events=30, max_new=60, t0=1000.0, dup_frac=0.3):
+    """Small adversarial scenario for the loop without heartbeats,
+    ``PushDispatcher.start`` (``task_dispatcher.py:251-322``): the deque holds
+    some ids several times (repeated registers), registers with 0/-1 processes,
+    results that bring a worker back to 1 free process, and message kinds
+    start() ignores.  Results only come from ids with a record (another id's
+    result raises KeyError in the reference, :291)."""
+    rng = _rng(seed + 7919)
+    reg = rng.random(W) < 0.6
+    free = np.where(reg, rng.integers(-1, 6, W), 0).astype(np.int32)
+    hb = np.where(reg, t0 - 0.25 * rng.integers(0, 56, W), 0.0)
+    tok = [s for s in range(W) if reg[s] and (free[s] > 0 and rng.random() < 0.9 or rng.random() < 0.15)]
+    if tok:
+        tok += list(rng.choice(tok, size=int(rng.integers(0, int(dup_frac * len(tok)) + 2))))
+    queue = rng.permutation(np.asarray(tok, np.int32)) if tok else np.zeros(0, np.int32)
+    log = []
+    for s in range(W):
+        if reg[s]:
+            log += [s] * int(rng.integers(0, 4))
+    log += [-1] * int(rng.integers(0, 4))
+    log = list(rng.permutation(np.asarray(log, np.int32))) if log else []
+    known = set(np.nonzero(reg)[0].tolist())
+    ticks = []
+    now = t0
+    for _ in range(n_ticks):
+        prev = now
+        now = prev + 0.25 * int(rng.integers(0, 24))
+        E = int(rng.integers(0, max_events + 1))
+        ts = np.sort(prev + 0.25 * rng.integers(0, int(round((now - prev) / 0.25)) + 1, E)).astype(np.float64)
+        kind = rng.choice(5, size=E, p=[0.25, 0.08, 0.1, 0.5, 0.07]).astype(np.uint8)
+        hot = rng.integers(0, W, max(1, W // 4))
+        slot = np.where(rng.random(E) < 0.6, rng.choice(hot, E), rng.integers(0, W, E)).astype(np.int32)
+        val = rng.integers(-1, 6, E).astype(np.int32)
+        for i in range(E):
+            if kind[i] == EV_REGISTER:
+                known.add(int(slot[i]))
+            elif kind[i] == EV_RESULT and int(slot[i]) not in known:
+                kind[i] = EV_HEARTBEAT  # start() ignores it
+        ticks.append(dict(now=float(now), n_new=int(rng.integers(0, max_new + 1)),
+                          ev_kind=kind, ev_slot=slot, ev_val=val, ev_ts=ts,
+                          ev_pick=rng.integers(0, 2 ** 31, E).astype(np.uint32),
+                          ev_seq=np.full(E, -1, np.int64)))
+    return dict(W=W, tte=float("inf"), t0=float(t0),
+                init_reg=reg.astype(np.uint8), init_free=free, init_hb=hb.astype(np.float64),
+                init_epoch=np.zeros(W, np.uint32),
+                init_queue=np.asarray(queue, np.int32), init_log=np.asarray(log, np.int32),
+                ticks=ticks)
+
+
+def zipf_deque_state(W=65536, seed=0, now=1000.0, cap=32, zipf_a=1.5, dup_frac=0.0):
+    """Config-3 loads for the loop without heartbeats (start(), :251-322): no
+    deaths; the deque holds every worker with free > 0 once, plus ``dup_frac``
+    of them a second time (re-registered while queued)."""
+    st = zipf_state(W=W, seed=seed, now=now, cap=cap, dead_frac=0.0, zipf_a=zipf_a)
+    if dup_frac > 0:
+        rng = _rng(seed + 104729)
+        q = st["queue"]
+        dup = rng.choice(q, size=int(dup_frac * len(q)), replace=False)
+        pos = np.sort(rng.integers(0, len(q) + 1, len(dup)))
+        st["queue"] = np.insert(q, pos, dup).astype(np.int32)
+    return st
+
+
 def uniform_state(W=1000, seed=0, now=1000.0, cap=256):
     """Config 2 (BASELINE.json configs[1]): every worker cap 256, busy ~ U[0,128),
     no deaths (hb = now - U[0, 9.9)), random LRU permutation."""

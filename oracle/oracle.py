@@ -38,6 +38,15 @@ def _lib():
     lib.oracle_tick.restype = C.c_int
     lib.oracle_tick.argtypes = [_P, C.c_double, C.c_double, C.c_int32, _P, _P, _P, _P, _P,
                                 C.c_int64, C.c_int64, _P, _P, _P, _P, _P, _P, _P]
+    lib.dq_oracle_create.restype = _P
+    lib.dq_oracle_create.argtypes = [C.c_int32, C.c_int64]
+    lib.dq_oracle_destroy.argtypes = [_P]
+    lib.dq_oracle_load.restype = C.c_int
+    lib.dq_oracle_load.argtypes = [_P, _P, _P, _P, _P, C.c_int64, _P, C.c_int64]
+    lib.dq_oracle_export.restype = C.c_int64
+    lib.dq_oracle_export.argtypes = [_P] * 7
+    lib.dq_oracle_tick.restype = C.c_int
+    lib.dq_oracle_tick.argtypes = [_P, C.c_int32, _P, _P, _P, _P, _P, C.c_int64, C.c_int64, _P, _P, _P]
     return lib
 
 
@@ -131,6 +140,72 @@ class Oracle:
         head = np.zeros(1, np.int64)
         lib().oracle_export(self.h, None, None, None, None, None, None, _ptr(head))
         return int(head[0])
+
+
+class DequeOracle:
+    """Sequential CPU restatement of the reference's ``PushDispatcher.start``
+    (``task_dispatcher.py:251-322``): no heartbeats, a deque that may repeat ids
+    (``deque_oracle.c``).  Same call shape as :class:`Oracle`; ``now``/``tte``
+    are accepted and unused (start() has no liveness).  Event status in
+    ``reconnect``: 2 = result from an id without a record (KeyError in the
+    reference)."""
+
+    def __init__(self, W, log_cap):
+        self.W = int(W)
+        self.log_cap = int(log_cap)
+        self.h = lib().dq_oracle_create(self.W, self.log_cap)
+        if not self.h:
+            raise MemoryError("dq_oracle_create failed")
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h:
+            lib().dq_oracle_destroy(h)
+            self.h = None
+
+    def load(self, reg, free, hb, epoch, queue, log):
+        del epoch  # no redistribution without heartbeats
+        reg = np.ascontiguousarray(reg, np.uint8)
+        free = np.ascontiguousarray(free, np.int32)
+        hb = np.ascontiguousarray(hb, np.float64)
+        queue = np.ascontiguousarray(queue, np.int32)
+        log = np.ascontiguousarray(log, np.int32)
+        if lib().dq_oracle_load(self.h, _ptr(reg), _ptr(free), _ptr(hb), _ptr(queue), len(queue), _ptr(log),
+                                len(log)) != 0:
+            raise ValueError("inconsistent state")
+
+    def export(self):
+        W = self.W
+        reg = np.zeros(W, np.uint8)
+        free = np.zeros(W, np.int32)
+        hb = np.zeros(W, np.float64)
+        head = np.zeros(1, np.int64)
+        n = lib().dq_oracle_export(self.h, None, None, None, None, None, _ptr(head))
+        queue = np.zeros(max(n, 1), np.int32)
+        log = np.zeros(max(int(head[0]), 1), np.int32)
+        lib().dq_oracle_export(self.h, _ptr(reg), _ptr(free), _ptr(hb), _ptr(queue), _ptr(log), _ptr(head))
+        return dict(reg=reg, free=free, hb=hb, epoch=np.zeros(W, np.uint32), queue=queue[:n],
+                    log=log[: int(head[0])], head=int(head[0]))
+
+    def tick(self, now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending, dispatch_limit=-1):
+        del now, tte
+        E = len(ev_kind)
+        ev_kind = np.ascontiguousarray(ev_kind, np.uint8)
+        ev_slot = np.ascontiguousarray(ev_slot, np.int32)
+        ev_val = np.ascontiguousarray(ev_val, np.int32)
+        ev_ts = np.ascontiguousarray(ev_ts, np.float64)
+        ev_seq = np.ascontiguousarray(ev_seq, np.int64)
+        status = np.zeros(max(E, 1), np.uint8)
+        head = np.zeros(1, np.int64)
+        lib().dq_oracle_export(self.h, None, None, None, None, None, _ptr(head))
+        assign = np.zeros(max(self.log_cap - int(head[0]), 1), np.int32)
+        na = np.zeros(1, np.int64)
+        rc = lib().dq_oracle_tick(self.h, E, _ptr(ev_kind), _ptr(ev_slot), _ptr(ev_val), _ptr(ev_ts), _ptr(ev_seq),
+                                  int(n_pending), int(dispatch_limit), _ptr(status), _ptr(assign), _ptr(na))
+        if rc != 0:
+            raise RuntimeError("deque oracle: log overflow" if rc == -1 else "deque oracle: out of memory")
+        return dict(reconnect=status[:E].copy(), assign=assign[: int(na[0])].copy(),
+                    orphans=np.zeros(0, np.int64), evicted=np.zeros(0, np.int32))
 
 
 def fixture_ticks(z):

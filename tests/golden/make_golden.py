@@ -20,7 +20,11 @@ registrations that died during the tick are put, in ascending original dispatch
 sequence, ahead of the pending tasks.
 
 Only data leaves this script: ``tests/golden/*.npz`` (inputs + expected outputs).
-No reference source is copied.  Usage:  python tests/golden/make_golden.py
+No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque]
+
+The same harness drives the loop without heartbeats, ``PushDispatcher.start``
+(``task_dispatcher.py:251-322``, a deque of ids instead of the OrderedDict) for
+the ``deque_*.npz`` vectors.
 """
 from __future__ import annotations
 
@@ -90,8 +94,9 @@ class RefHarness:
     """Drives the reference loop; also acts as its socket, poller, subscriber
     and redis client."""
 
-    def __init__(self, td, scen, purge_once=False):
+    def __init__(self, td, scen, purge_once=False, loop="start_heartbeat"):
         self.td = td
+        self.loop = loop
         self.scen = scen
         self.clock = [float(scen.get("t0", 0.0))]
         td.time = types.SimpleNamespace(time=lambda: self.clock[0])
@@ -100,11 +105,16 @@ class RefHarness:
         W = int(scen["W"])
         self.W = W
         tte = scen["tte"]
-        q = collections.OrderedDict()
-        for s in scen["init_queue"]:
-            q[wid(int(s))] = None
-        self.queue = q
-        td.OrderedDict = lambda: self.queue
+        if loop == "start":
+            # PushDispatcher.start keeps a collections.deque (:254) that may repeat ids
+            self.queue = collections.deque(wid(int(s)) for s in scen["init_queue"])
+            td.deque = lambda: self.queue
+        else:
+            q = collections.OrderedDict()
+            for s in scen["init_queue"]:
+                q[wid(int(s))] = None
+            self.queue = q
+            td.OrderedDict = lambda: self.queue
         d = td.PushDispatcher.__new__(td.PushDispatcher)
         d.workers = {}
         d.time_to_expire = tte
@@ -325,7 +335,7 @@ class RefHarness:
 
     def run(self):
         try:
-            self.d.start_heartbeat()
+            getattr(self.d, self.loop)()
         except _Stop:
             pass
         return self.out
@@ -367,12 +377,22 @@ def pack(scen, outs, name, note):
     return path
 
 
-def capture(td, scen, purge_once=False):
-    return RefHarness(td, scen, purge_once=purge_once).run()
+def capture(td, scen, purge_once=False, loop="start_heartbeat"):
+    return RefHarness(td, scen, purge_once=purge_once, loop=loop).run()
 
 
-def main():
+def main(which="all"):
     td = load_reference()
+    made = []
+    if which in ("all", "heartbeat"):
+        made += heartbeat_fixtures(td)
+    if which in ("all", "deque"):
+        made += deque_fixtures(td)
+    for p in made:
+        print(p, os.path.getsize(p))
+
+
+def heartbeat_fixtures(td):
     made = []
     # 1) many small adversarial multi-tick scenarios, loop exactly as written
     for seed in range(48):
@@ -401,9 +421,26 @@ def main():
     scen["t0"] = 1000.0
     made.append(pack(scen, capture(td, scen, purge_once=True), "cfg5_w512_churn",
                      "zipf_state(W=512, seed=3) + churn_ticks(14, seed=2), purge once per unchanged clock"))
-    for p in made:
-        print(p, os.path.getsize(p))
+    return made
+
+
+def deque_fixtures(td):
+    made = []
+    # 5) the loop without heartbeats, PushDispatcher.start (:251-322): deque with
+    #    repeated ids, registers with 0/-1, results bringing free back to 1
+    for seed in range(24):
+        W = [6, 12, 24, 48][seed % 4]
+        scen = synth.random_deque_scenario(seed, W=W, n_ticks=1 + seed % 6,
+                                           max_events=[0, 8, 30, 80][(seed // 4) % 4],
+                                           max_new=[0, 10, 60, 200][(seed // 2) % 4])
+        made.append(pack(scen, capture(td, scen, loop="start"), "deque_%02d" % seed,
+                         "random_deque_scenario seed=%d, reference start() loop" % seed))
+    st = synth.zipf_deque_state(W=2048, seed=4, dup_frac=0.05)
+    scen = synth.state_to_scenario(st, [synth.empty_tick(1000.0, 30000)], tte=float("inf"))
+    made.append(pack(scen, capture(td, scen, loop="start"), "deque_cfg3_w2048_t30000",
+                     "zipf_deque_state(W=2048, seed=4, dup_frac=0.05), T=30000, reference start() loop"))
+    return made
 
 
 if __name__ == "__main__":
-    main()
+    main(sys.argv[1] if len(sys.argv) > 1 else "all")

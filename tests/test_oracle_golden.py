@@ -6,9 +6,10 @@ import os
 import numpy as np
 import pytest
 
-from oracle import Oracle, fixture_expect, fixture_ticks
+from oracle import DequeOracle, Oracle, fixture_expect, fixture_ticks
 
-GOLDEN = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz")))
+GOLDEN = sorted(p for p in glob.glob(os.path.join(os.path.dirname(__file__), "golden", "*.npz"))
+                if not os.path.basename(p).startswith("deque_"))  # start_heartbeat vectors
 
 
 def replay(z, purge_mode):
@@ -44,3 +45,47 @@ def test_oracle_matches_reference(path, purge_mode):
         np.testing.assert_array_equal(st["free"][reg], exp["post_free"][reg], err_msg=f"tick {t}")
         np.testing.assert_array_equal(st["hb"][reg], exp["post_hb"][reg], err_msg=f"tick {t}")
         np.testing.assert_array_equal(st["queue"], exp["post_queue"], err_msg=f"tick {t}")
+
+
+DEQUE = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "deque_*.npz")))
+
+
+@pytest.mark.parametrize("path", DEQUE, ids=[os.path.basename(p)[:-4] for p in DEQUE])
+def test_deque_oracle_matches_reference(path):
+    """deque_oracle.c against vectors captured from the reference's start() loop
+    (task_dispatcher.py:251-322): duplicate deque entries, no heartbeats."""
+    z = np.load(path)
+    W = int(z["W"])
+    o = DequeOracle(W, len(z["init_log"]) + len(z["exp_assign"]) + 16)
+    o.load(z["init_reg"], z["init_free"], z["init_hb"], z["init_epoch"], z["init_queue"], z["init_log"])
+    carried = 0
+    for t, tk in enumerate(fixture_ticks(z)):
+        exp = fixture_expect(z, t)
+        n_pending = carried + tk["n_new"]
+        out = o.tick(tk["now"], float(z["tte"]), tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"],
+                     tk["ev_seq"], n_pending)
+        st = o.export()
+        assert n_pending == exp["n_pending"], t
+        assert not exp["reconnect"].any() and not len(exp["orphans"]) and not len(exp["evicted"])
+        np.testing.assert_array_equal(out["reconnect"], exp["reconnect"], err_msg=f"tick {t}")
+        np.testing.assert_array_equal(out["assign"], exp["assign"], err_msg=f"tick {t}")
+        np.testing.assert_array_equal(st["reg"], exp["post_reg"], err_msg=f"tick {t}")
+        reg = exp["post_reg"].astype(bool)
+        np.testing.assert_array_equal(st["free"][reg], exp["post_free"][reg], err_msg=f"tick {t}")
+        np.testing.assert_array_equal(st["hb"][reg], exp["post_hb"][reg], err_msg=f"tick {t}")
+        np.testing.assert_array_equal(st["queue"], exp["post_queue"], err_msg=f"tick {t}")
+        carried = n_pending - len(out["assign"])
+
+
+def test_deque_fixtures_hold_duplicates():
+    """The start() vectors exercise the deque's repeated ids (the case the GPU
+    handles with per-token ranks)."""
+    n = 0
+    for path in DEQUE:
+        z = np.load(path)
+        q = z["exp_post_queue"]
+        off = z["exp_post_queue_off"]
+        for t in range(int(z["n_ticks"])):
+            seg = q[off[t]:off[t + 1]]
+            n += len(seg) - len(np.unique(seg))
+    assert n > 20
