@@ -40,6 +40,14 @@ def emit_bytes(W, Q, F, O, N, Qn_out):
     return 4 * N + 8 * Q + 8 * Q + 4 * Qn_out + 4 * F + 8 * O
 
 
+def emit_deque_bytes(Q, N, Qn_out):
+    """k_emit in deque mode (start()): task writes (4 B/task), per deque entry its
+    c and slot (4+4) and token record {j, m, q, k} (16), its worker's count
+    update (4+4) and K_L (4); next deque entry + rank (4+4) and the per-slot
+    token count (4+4)."""
+    return 4 * N + 36 * Q + 16 * Qn_out
+
+
 def emit_shard_bytes(Q, own_q, F_local, O_local, n_local, Qn_out):
     """Algorithmic bytes of k_emit_shard on one rank: c8 exchange byte + queue
     slot read + next-queue write per LRU position (1+4+4), own tasks (slot and
@@ -82,6 +90,21 @@ def cpu_baseline(st, T, budget_s=10.0):
                                   % len(full["assign"]))
 
 
+def cpu_baseline_deque(st, T, budget_s=10.0):
+    """oracle/deque_oracle.c (the start() loop as written, 1 core) on the whole tick."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    from oracle import DequeOracle
+    W = len(st["reg"])
+    o = DequeOracle(W, len(st["log"]) + T + 16)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    t0 = time.perf_counter()
+    out = o.tick(1000.0, 0.0, [], [], [], [], [], T)
+    dt = time.perf_counter() - t0
+    return dict(value=len(out["assign"]) / dt, unit="assignments/s", cores=1, kind="port",
+                sample="whole tick (%d dispatches), start() loop as written, oracle/deque_oracle.c; host nproc=%d"
+                       % (len(out["assign"]), os.cpu_count()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -92,6 +115,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
+    ap.add_argument("--mode", default="heartbeat", choices=("heartbeat", "deque"),
+                    help="deque: the loop without heartbeats (PushDispatcher.start), one GPU")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", "0"))
@@ -113,11 +138,15 @@ def main():
     # worker-id range and runs the two-phase tick with the RCCL exchange
     # all-reduce every step.
     W, T = args.workers * world, args.tasks * world
-    st = synth.zipf_state(W=W, seed=0)
+    deque = args.mode == "deque"
+    if deque and world > 1:
+        raise SystemExit("--mode deque runs on one GPU (the start() loop has no sharded form)")
+    # deque: same loads without deaths; 2 % of the queued workers hold a second deque entry
+    st = synth.zipf_deque_state(W=W, seed=0, dup_frac=0.02) if deque else synth.zipf_state(W=W, seed=0)
     F = len(st["log"])
     Q = len(st["queue"])
     if world == 1:
-        g = GpuBalancer(W, 2 * F + T + 16, max_events=1, device=0)
+        g = GpuBalancer(W, 2 * F + T + 16, max_events=1, device=0, mode=args.mode)
         g.load(st)
 
         def step():
@@ -186,7 +215,9 @@ def main():
     dom = max((k for k in kern if k != "exchange_allreduce"), key=lambda k: kern[k][0])
     dom_ms = kern[dom][0]
     tick_dev_ms = sum(v[0] for k, v in kern.items() if k != "exchange_allreduce")
-    if dom == "emit" and world == 1:
+    if dom == "emit" and deque:
+        dom_bytes = emit_deque_bytes(Q, n_assigned, int(res["queue_len"]))
+    elif dom == "emit" and world == 1:
         dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]))
     elif dom == "emit":
         dom_bytes = emit_shard_bytes(Q, Q // world, F // world, int(res["n_orphans_local"]), int(res["n_local"]),
@@ -218,7 +249,10 @@ def main():
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (faasbal.synth.zipf_state, seed=0)",
-        "config": {"workload": ("configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
+        "config": {"workload": ("configs[2] loads, start() loop (no heartbeats): one tick, %d pending tasks x %d "
+                                "workers, Zipf(1.5) loads cap 32, deque of %d entries (2%% repeated ids)"
+                                % (T, W, Q)) if deque else
+                               ("configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
                                 "5%% dead -> %d orphans redistributed" % (T, W, O)) if world == 1 else
                                ("configs[2] per GPU, weak: one global tick of %d tasks x %d workers sharded by "
                                 "worker-id range over %d GPUs, exchange all-reduce of %d B per tick (RCCL), "
@@ -235,8 +269,12 @@ def main():
                  "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,
                  "kernels_avg_ms": {k: v[0] for k, v in kern.items()}},
     }
+    if deque:
+        line["metric"] = "task assignments/sec, start() loop (no heartbeats), 1M tasks x 64K workers"
+        line["data"] = "synthetic (faasbal.synth.zipf_deque_state, seed=0, dup_frac=0.02)"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        line["cpu_baseline"] = cpu_baseline(st, T, args.cpu_budget)
+        line["cpu_baseline"] = cpu_baseline_deque(st, T, args.cpu_budget) if deque else \
+            cpu_baseline(st, T, args.cpu_budget)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

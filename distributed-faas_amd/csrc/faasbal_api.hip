@@ -84,8 +84,13 @@ struct fb_ctx {
     int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
     int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
-    int old_emit = 0;
-    int dbg_stop = 0;     // FAASBAL_DBG_STOP=n: timing probe (results invalid)     // FAASBAL_OLD_EMIT=1: 256-thread k_emit on the fused path (A/B switch)  // FAASBAL_SPLIT_SLOTS=1: separate k_slots launch + died bitmap (A/B switch)
+    int dbg_stop = 0;      // FAASBAL_DBG_STOP=n: timing probe (results invalid)
+    // deque contexts (fb_create_deque): PushDispatcher.start, task_dispatcher.py:251-322
+    int deque = 0;
+    int32_t *tokcnt[2] = {nullptr, nullptr}, *xw[2] = {nullptr, nullptr}, *kl[2] = {nullptr, nullptr};
+    uint32_t *qrank[2] = {nullptr, nullptr};
+    int32_t *front_rank = nullptr, *back_rank = nullptr, *post_tok = nullptr, *post_nf = nullptr;
+    int4 *c_tok = nullptr;
     void *arena = nullptr;    // every fixed-size device buffer, carved from one allocation
     size_t arena_bytes = 0;
     bool table_owned = false; // qcnt/qpre grown beyond the arena's reservation
@@ -307,6 +312,12 @@ int enqueue_tick(fb_ctx *c) {
         }
         EvArgs a{};
         a.E = E;
+        a.deque = c->deque;
+        a.tokcnt_in = c->tokcnt[cur];
+        a.front_rank = c->front_rank;
+        a.back_rank = c->back_rank;
+        a.post_tok = c->post_tok;
+        a.post_nf = c->post_nf;
         a.shard = c->shard;
         a.slot_base = c->slot_base;
         a.W = W;
@@ -343,8 +354,23 @@ int enqueue_tick(fb_ctx *c) {
     a.E = E;
     a.R = R;
     a.nbw = nbw;
-    a.nbf = nbf;
+    a.nbf = c->deque ? 0 : nbf;  // start(): nobody dies, no log scan
     a.nbq = nbq;
+    a.deque = c->deque;
+    a.q_cap = c->Wq_cap;
+    a.tokcnt_in = c->tokcnt[cur];
+    a.xw_in = c->xw[cur];
+    a.kl_in = c->kl[cur];
+    a.qrank_in = c->qrank[cur];
+    a.front_rank = c->front_rank;
+    a.back_rank = c->back_rank;
+    a.post_tok = c->post_tok;
+    a.post_nf = c->post_nf;
+    a.c_tok = c->c_tok;
+    a.tokcnt_out = c->tokcnt[nxt];
+    a.xw_out = c->xw[nxt];
+    a.kl_out = c->kl[nxt];
+    a.qrank_out = c->qrank[nxt];
     // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
     // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
@@ -356,7 +382,7 @@ int enqueue_tick(fb_ctx *c) {
     // ... or better, while the bitmap fits in one workgroup's LDS: the W-role of
     // k_scan writes it and k_logscan tests every entry against an LDS copy
     const size_t bm_bytes = (size_t)(((W + 63) / 64 + 1) / 2 + 1) * 16;
-    a.f_sep = (head > 0 && (c->logscan > 0 || (c->logscan < 0 && W > kLdsBitmapSlots)) &&
+    a.f_sep = (head > 0 && !c->deque && (c->logscan > 0 || (c->logscan < 0 && W > kLdsBitmapSlots)) &&
                bm_bytes <= (size_t)c->max_lds && !(c->shard && c->phase == 2)) ? 1 : 0;
     if (a.f_sep) a.slots_in_scan = 1;
     const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
@@ -500,7 +526,7 @@ const char *fb_last_error(const fb_ctx *ctx) { return ctx ? ctx->err.c_str() : "
 
 namespace {
 int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_events, int device, int shard,
-               int rank, int world, int32_t n_workers_global) {
+               int rank, int world, int32_t n_workers_global, int64_t max_tokens = 0) {
     if (!out) return FB_EINVAL;
     *out = nullptr;
     if (max_workers < 1 || max_log < 1 || max_events < 0 || max_log >= ((int64_t)1 << 31) ||
@@ -515,7 +541,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     c->rank = shard ? rank : 0;
     c->world = shard ? world : 1;
     c->W_global = shard ? n_workers_global : max_workers;
-    c->Wq_cap = c->W_global;
+    c->deque = max_tokens > 0 ? 1 : 0;
+    c->Wq_cap = c->deque ? (int32_t)max_tokens : c->W_global;
     c->W_cap = max_workers;
     c->E_cap = std::max(max_events, 1);
     c->log_cap = max_log;
@@ -579,6 +606,19 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->A, 128);
     ap.add(&c->log_slot, F);
     ap.add(&c->orphans, F);
+    if (c->deque) {
+        for (int i = 0; i < 2; ++i) {
+            ap.add(&c->tokcnt[i], W);
+            ap.add(&c->xw[i], W);
+            ap.add(&c->kl[i], W);
+            ap.add(&c->qrank[i], Wq);
+        }
+        ap.add(&c->front_rank, E);
+        ap.add(&c->back_rank, E);
+        ap.add(&c->post_tok, W);
+        ap.add(&c->post_nf, W);
+        ap.add(&c->c_tok, Qlog);
+    }
     if (shard) {
         ap.add(&c->lseq, F);
         ap.add(&c->ocnt, tab);
@@ -619,6 +659,12 @@ int fb_create(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_ev
     return create_ctx(out, max_workers, max_log, max_events, device, 0, 0, 1, max_workers);
 }
 
+int fb_create_deque(fb_ctx **out, int32_t max_workers, int64_t max_tokens, int64_t max_log, int32_t max_events,
+                    int device) {
+    if (max_tokens < 1 || max_tokens >= (1 << 30)) return FB_EINVAL;
+    return create_ctx(out, max_workers, max_log, max_events, device, 0, 0, 1, max_workers, max_tokens);
+}
+
 int fb_create_sharded(fb_ctx **out, int32_t max_workers_local, int32_t n_workers_global, int64_t max_log_local,
                       int32_t max_events, int device, int32_t rank, int32_t world) {
     return create_ctx(out, max_workers_local, max_log_local, max_events, device, 1, rank, world, n_workers_global);
@@ -654,16 +700,20 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
     if (c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_load_shard");
     if (n_workers < 0 || n_workers > c->W_cap) return fail(c, FB_EINVAL, "n_workers %d outside [0, %d]", n_workers, c->W_cap);
     if (log_len < 0 || log_len > c->log_cap) return fail(c, FB_EINVAL, "log_len %lld exceeds capacity", (long long)log_len);
-    if (queue_len < 0 || queue_len > n_workers) return fail(c, FB_EINVAL, "queue_len %lld", (long long)queue_len);
+    if (queue_len < 0 || queue_len > (c->deque ? c->Wq_cap : n_workers))
+        return fail(c, FB_EINVAL, "queue_len %lld", (long long)queue_len);
     const size_t W = (size_t)n_workers;
     std::vector<uint8_t> inq(W ? W : 1, 0);
+    std::vector<int32_t> tokcnt(c->deque ? (W ? W : 1) : 0, 0);
+    std::vector<uint32_t> qrank(c->deque ? (size_t)queue_len : 0);
     int32_t maxc = 1;
     for (int64_t i = 0; i < queue_len; ++i) {
         const int32_t s = queue[i];
-        if (s < 0 || s >= n_workers || !registered[s] || inq[s])
+        if (s < 0 || s >= n_workers || !registered[s] || (inq[s] && !c->deque))
             return fail(c, FB_EINVAL, "queue[%lld] = %d is out of range, unregistered or duplicated", (long long)i, s);
         inq[s] = 1;
         maxc = std::max(maxc, free_processes[s]);
+        if (c->deque) qrank[i] = (uint32_t)(++tokcnt[s]) | kPart2;  // rank among the slot's tokens
     }
     for (int64_t i = 0; i < log_len; ++i)
         if (log_slot[i] < -1 || log_slot[i] >= n_workers)
@@ -696,7 +746,15 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         HIPCHK(c, hipMemcpy(c->qfree[0], qf.data(), (size_t)queue_len * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->qhb[0], qh.data(), (size_t)queue_len * 8, hipMemcpyHostToDevice));
     }
-    c->qaos = true;
+    c->qaos = !c->deque;
+    if (c->deque) {
+        if (W) {
+            HIPCHK(c, hipMemcpy(c->tokcnt[0], tokcnt.data(), W * 4, hipMemcpyHostToDevice));
+            HIPCHK(c, hipMemset(c->xw[0], 0, W * 4));
+            HIPCHK(c, hipMemset(c->kl[0], 0, W * 4));
+        }
+        if (queue_len) HIPCHK(c, hipMemcpy(c->qrank[0], qrank.data(), (size_t)queue_len * 4, hipMemcpyHostToDevice));
+    }
     if (log_len) HIPCHK(c, hipMemcpy(c->log_slot, log_slot, (size_t)log_len * 4, hipMemcpyHostToDevice));
     c->W = n_workers;
     c->Qn = queue_len;
@@ -889,7 +947,7 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
         HIPCHK(c, hipMemcpyAsync(c->ev_seq, hq, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
     }
     c->l_now = now;
-    c->l_tte = tte;
+    c->l_tte = c->deque ? __builtin_inf() : tte;  // start() has no liveness: nobody ever expires
     c->l_E = E;
     c->l_T = n_pending;
     c->l_head = c->head;
@@ -924,6 +982,9 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
         if (rc) return rc;
     }
     const HostOut &p = *c->hout;
+    if (c->deque && p.new_qlen > c->Wq_cap)
+        return fail(c, FB_ENOSPC, "deque of %lld tokens exceeds the context's capacity %d", (long long)p.new_qlen,
+                    c->Wq_cap);
     fb_tick_result r{};
     r.n_assigned = p.N_eff;
     r.n_orphans = p.O;

@@ -21,6 +21,11 @@ constexpr int kLsBS = 1024;        // k_logscan: one 16-wave workgroup per CU
 constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3;
 constexpr uint8_t kEvsApplied = 0, kEvsReconnect = 1;
 
+// deque mode (PushDispatcher.start): a committed token rank with this bit set sat in
+// A_L[p:] of the tick that wrote it (final rank = j - x_w), else in A_L[:p] (K_L - x_w + j)
+constexpr uint32_t kPart2 = 1u << 30;
+constexpr uint8_t kEvsUnknown = 2;  // deque mode: result from an id without a record (KeyError, :291)
+
 // per-slot tick status (st)
 constexpr uint8_t kStAlive = 1;      // registered and alive after the final purge
 constexpr uint8_t kStDiedStart = 2;  // the registration alive at tick start died this tick
@@ -50,6 +55,7 @@ struct HostOut {
     int32_t L;          // fill level
     int32_t maxc;       // max c
     int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
+                        // (deque contexts: new_qlen > token capacity is checked by the host)
     int32_t pad;
     int64_t n_local;    // sharded: tasks appended to this rank's log shard
     int64_t O_local;    // sharded: this rank's orphans
@@ -64,6 +70,10 @@ struct DevTotals {
 
 struct EvArgs {
     int E;
+    int deque;          // 1: PushDispatcher.start semantics (no liveness, deque with repeated ids)
+    const int32_t *tokcnt_in;          // deque: committed tokens per slot
+    int32_t *front_rank, *back_rank;   // deque: rank of a new token among its slot's tokens
+    int32_t *post_tok, *post_nf;       // deque: tokens per slot after the messages; new front tokens
     int shard;          // 0: one GPU; else this rank owns global slots [slot_base, slot_base + W)
     int slot_base, W;
     int64_t head_local; // sharded: local log length (entries carry their global seq in lseq)
@@ -97,6 +107,14 @@ struct TickArgs {
     int fused;       // 1: k_emit derives the cross-block prefixes itself (no k_plan launch)
     int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
     int slots_in_scan;
+    int deque;        // 1: PushDispatcher.start semantics (see EvArgs)
+    int64_t q_cap;    // deque: token capacity of queue_out
+    const int32_t *tokcnt_in, *xw_in, *kl_in;  // deque: committed per-slot token count, x_w, K_L
+    const uint32_t *qrank_in;                  // deque: committed token rank (+ kPart2) per position
+    const int32_t *front_rank, *back_rank, *post_tok, *post_nf;
+    int4 *c_tok;                               // deque: {rank j, m, q, k} per position (k_scan -> emit)
+    int32_t *tokcnt_out, *xw_out, *kl_out;
+    uint32_t *qrank_out;
     int f_sep;        // 1: log role in its own launch (k_logscan, died bitmap in LDS); k_scan W-role writes the bitmap
     int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;

@@ -294,11 +294,72 @@ __device__ __forceinline__ int64_t lseq_find(const uint32_t *lseq, int64_t n, in
     return (lo < n && (int64_t)lseq[lo] == q) ? lo : -1;
 }
 
+// The loop without heartbeats, PushDispatcher.start (task_dispatcher.py:251-322), for
+// one slot's messages: no liveness; every register(n > 0) inserts a new token at the
+// left of the deque (:280-281), a result that brings free to 1 appends one at the
+// right (:294-295) -- both whatever tokens the worker already holds.  Each new
+// token gets its rank among the slot's tokens in deque order: fronts (newest
+// first), then the committed ones, then backs (oldest first).
+__device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
+    int nf = 0;
+    for (int k = j; k < a.E && a.skeys[k] == s; ++k) {
+        const int i = (int)a.svals[k];
+        nf += (a.ev_kind[i] == kEvRegister && a.ev_val[i] > 0) ? 1 : 0;
+    }
+    const int k_old = a.tokcnt_in[s];
+    int reg = a.reg[s];
+    int32_t fr = a.free_in[s];
+    double hb = a.hbe[s].hb;
+    uint32_t epoch = a.hbe[s].epoch;
+    int mf = 0, nb = 0;
+    for (int k = j; k < a.E && a.skeys[k] == s; ++k) {
+        const int i = (int)a.svals[k];
+        const int kind = a.ev_kind[i];
+        uint8_t status = kEvsApplied;
+        if (kind == kEvRegister) {                       // :276-281, a fresh PushWorker
+            if (!reg) { reg = 1; epoch = (uint32_t)a.head_in; }
+            hb = a.ev_ts[i];
+            fr = a.ev_val[i];
+            if (fr > 0) {
+                ++mf;
+                a.front_list[a.E - 1 - i] = (int32_t)s + 1;
+                a.front_rank[a.E - 1 - i] = nf - mf + 1;
+            }
+        } else if (kind == kEvResult) {                  // :284-295
+            if (!reg) {
+                status = kEvsUnknown;                    // KeyError at :291 in the reference
+            } else {
+                fr += 1;
+                const int64_t q = a.ev_seq[i];
+                if (q >= 0 && q < a.head_in && a.log_slot[q] == (int32_t)s) a.log_slot[q] = -1;
+                if (fr == 1) {
+                    ++nb;
+                    a.back_list[i] = (int32_t)s + 1;
+                    a.back_rank[i] = k_old + nf + nb;
+                }
+            }
+        }                                                // other kinds: no branch in start()
+        a.ev_status[i] = status;
+    }
+    a.post_reg[s] = (uint8_t)reg;
+    a.post_free[s] = fr;
+    a.post_hb[s] = hb;
+    a.post_epoch[s] = epoch;
+    a.post_flags[s] = (uint8_t)(kQsKeep << 1);
+    a.touched[s] = a.tick;
+    a.post_tok[s] = k_old + nf + nb;
+    a.post_nf[s] = nf;
+}
+
 __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     const int j = blockIdx.x * kBS + threadIdx.x;
     if (j >= a.E) return;
     const uint32_t gs = a.skeys[j];
     if (j > 0 && a.skeys[j - 1] == gs) return;
+    if (a.deque) {
+        ev_apply_deque(a, j, gs);
+        return;
+    }
     if (a.shard && ((int)gs < a.slot_base || (int)gs >= a.slot_base + a.W)) return;  // another rank's worker
     const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
     int reg = a.reg[s];
@@ -490,10 +551,14 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         const bool dead = is_dead(a, c);
         const bool alive = c.reg && !dead;
         died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
-        evicted = (c.reg0 || c.t) && !alive;
+        evicted = !a.deque && (c.reg0 || c.t) && !alive;  // start() never deletes a record
         a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
         a.free_out[s] = alive ? c.fr : INT32_MIN;
         a.inq_out[s] = 0;
+        if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
+            a.tokcnt_out[s] = 0;
+            a.xw_out[s] = 0;
+        }
     }
     const uint64_t dm = __ballot(died_start);
     if ((!a.slots_in_scan || a.f_sep) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W)
@@ -644,6 +709,43 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
             c = a.xc8[pos];
             oc = (c > 0 && own_slot(a, lq_slot(a, pos)) >= 0) ? c : 0;
         }
+    } else if (a.deque) {
+        // start(): c of every deque token from its worker's free count f, token count k and
+        // the token's rank j (gpu_model.token_c): c = m + 1 + (j <= q), m = max(0, ceil(f/k) - 1),
+        // q = f - m k - 1 (f <= 0: every token is served once)
+        int32_t cc = INT32_MIN;
+        int4 tk = make_int4(0, 0, 0, 0);
+        if (pos < a.Qlog) {
+            const int s = lq_slot(a, pos);
+            if (s >= 0) {
+                const Cur cu = cur_slot(a, s);
+                int jr;
+                if (pos < a.E) {
+                    jr = a.front_rank[pos];
+                } else if (pos < a.E + a.Qn) {
+                    const uint32_t raw = a.qrank_in[pos - a.E];
+                    const int j0 = (int)(raw & (kPart2 - 1)), x = a.xw_in[s];
+                    jr = ((raw & kPart2) ? j0 - x : a.kl_in[s] - x + j0) + (cu.t ? a.post_nf[s] : 0);
+                } else {
+                    jr = a.back_rank[pos - a.E - a.Qn];
+                }
+                const int k = cu.t ? a.post_tok[s] : a.tokcnt_in[s];
+                const int f = cu.fr;
+                // q = f - m k - 1 also for f <= 0 (m = 0): then j <= q never holds and emit
+                // recovers f = q + m k + 1 from the record
+                int m = 0;
+                if (f > 0) {
+                    m = (f + k - 1) / k - 1;
+                    m = m > 0 ? m : 0;
+                }
+                const int q = f - m * k - 1;
+                cc = m + 1 + (jr <= q ? 1 : 0);
+                tk = make_int4(jr, m, q, k);
+            }
+            a.c_arr[pos] = cc;
+            a.c_tok[pos] = tk;
+        }
+        c = cc != INT32_MIN ? cc : 0;
     } else if (pos < a.Qlog) {
         int s = -1, ls = -1;
         int32_t raw = INT32_MIN;  // INT32_MIN: no live record (or not mine)
@@ -963,6 +1065,30 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     STAMP(a, SO, 15);
 }
 
+// Deque mode: the end of a token's tick.  Tokens of one worker share its count
+// (atomic), survivors carry their rank from before the round-L split plus the
+// part they sat in; per slot, x_w = highest rank served in round L and K_L =
+// tokens with c > L let the next tick re-rank them (gpu_model.tick_deque).
+__device__ __forceinline__ void deque_finish(const TickArgs &a, int64_t pos, int s, int c, int L, int64_t n_q,
+                                             bool servedL, int64_t np) {
+    const int4 tk = a.c_tok[pos];  // {j, m, q, k}; f = q + m k + 1
+    if (tk.w == 1) {
+        // the worker's only token: plain stores
+        a.free_out[s] = tk.z + tk.y + 1 - (int32_t)n_q;
+        if (np >= 0) a.tokcnt_out[s] = 1;
+        if (c > L && servedL) a.xw_out[s] = 1;
+    } else {
+        atomicSub(&a.free_out[s], (int32_t)n_q);
+        if (np >= 0) atomicAdd(&a.tokcnt_out[s], 1);
+        if (c > L && servedL) atomicMax(&a.xw_out[s], tk.x);
+    }
+    if (c > L) a.kl_out[s] = L < tk.y + 1 ? tk.w : (L == tk.y + 1 ? tk.z : 0);
+    if (np >= 0 && np < a.q_cap) {
+        a.queue_out[np] = s;
+        a.qrank_out[np] = (uint32_t)tk.x | (servedL ? 0u : kPart2);
+    }
+}
+
 // ------------------------------------------------------------ k_emit
 // Water-filling emission for one queue block once the fill level is known:
 // rounds [0, rfull) in full, round L partially (ranks < p), round L+1 ranks.
@@ -1053,7 +1179,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         }
         if (status) return;
         // ---- water-filling emission, 256 rounds per chunk, rounds 0 .. L+1
-        const int c = raw != INT32_MIN ? (raw > 1 ? raw : 1) : 0;
+        const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
         int32_t *const out = a.log_slot + a.head_in;
         int64_t rankL = -1, exL1 = 0;
         int64_t carryS = 0;  // S(rc)
@@ -1145,7 +1271,6 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
             if (c > L && rankL < p) n_q += 1;
-            a.free_out[s] = raw - (int32_t)n_q;
             int64_t np = -1;
             if (c > L) {
                 if (rankL >= p) np = rankL - p;
@@ -1153,6 +1278,12 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
                 // the one position of rank p in A_L knows the next queue's length
                 if (rankL == p) a.hout->new_qlen = (AL - p) + exL1;
             }
+            if (a.deque) {
+                deque_finish(a, pos, s, c, L, n_q, c > L && rankL < p, np);
+                STAMP(a, SO, 15);
+                return;
+            }
+            a.free_out[s] = raw - (int32_t)n_q;
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
@@ -1361,7 +1492,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
         // ---- rank base (in A_r) and task index base of this wave's segment, per round
         const int32_t raw = pos < a.Qlog ? raw0 : INT32_MIN;
         const int s = s0;
-        const int c = raw != INT32_MIN ? (raw > 1 ? raw : 1) : 0;  // free <= 0 still takes one task
+        // free <= 0 still takes one task; deque mode: c_arr holds the token's c itself
+        const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
         int32_t rbv[kRCh], basev[kRCh];
 #pragma unroll
         for (int k = 0; k < kRCh; ++k) {
@@ -1408,7 +1540,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
             if (c > L && rankL < pL) n_q += 1;
-            a.free_out[s] = raw - (int32_t)n_q;
             int64_t np = -1;
             if (c > L) {
                 if (rankL >= pL) np = rankL - pL;
@@ -1416,6 +1547,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
                 // the one position of rank pL in A_L knows the next queue's length
                 if (rankL == pL) a.hout->new_qlen = (AL - pL) + exL1;
             }
+            if (a.deque) {
+                deque_finish(a, pos, s, c, L, n_q, c > L && rankL < pL, np);
+                STAMP(a, SO, 15);
+                return;
+            }
+            a.free_out[s] = raw - (int32_t)n_q;
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;

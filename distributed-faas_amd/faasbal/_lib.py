@@ -11,6 +11,7 @@ import os
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfaasbal.so")
 
+FB_EVS_APPLIED, FB_EVS_RECONNECT, FB_EVS_UNKNOWN = 0, 1, 2
 FB_OK, FB_EINVAL, FB_ENOMEM, FB_EHIP, FB_ERANGE, FB_ENOSPC, FB_ESTATE = 0, -1, -2, -3, -4, -5, -6
 ERRNAMES = {FB_EINVAL: "FB_EINVAL", FB_ENOMEM: "FB_ENOMEM", FB_EHIP: "FB_EHIP", FB_ERANGE: "FB_ERANGE",
             FB_ENOSPC: "FB_ENOSPC", FB_ESTATE: "FB_ESTATE"}
@@ -21,7 +22,7 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_get_event_status", "fb_tick", "fb_device_view_get", "fb_timing_enable", "fb_timing_read",
            "fb_selftest", "fb_debug_read", "fb_sync", "fb_set_stream", "fb_get_local_assignments",
            "fb_create_sharded", "fb_load_shard", "fb_read_shard_log", "fb_exchange_bytes", "fb_bind_exchange",
-           "fb_tick_continue")
+           "fb_tick_continue", "fb_create_deque")
 
 
 class TickResult(C.Structure):
@@ -91,6 +92,7 @@ def load(path=LIB_PATH):
         "fb_exchange_bytes": (C.c_int, [_P, i32, C.POINTER(i64)]),
         "fb_bind_exchange": (C.c_int, [_P, _P, i64]),
         "fb_tick_continue": (C.c_int, [_P]),
+        "fb_create_deque": (C.c_int, [C.POINTER(_P), i32, i64, i64, i32, C.c_int]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name)

@@ -27,12 +27,31 @@ def _arr(a, dt):
 
 
 class GpuBalancer:
-    """Device-resident worker table + LRU queue + in-flight log on one GPU."""
+    """Device-resident worker table + LRU queue + in-flight log on one GPU.
 
-    def __init__(self, max_workers, max_log, max_events=65536, device=0, lib_path=None):
+    ``mode="heartbeat"`` (default) runs ``PushDispatcher.start_heartbeat``
+    (``task_dispatcher.py:324-419``) per tick; ``mode="deque"`` runs the loop
+    without heartbeats, ``PushDispatcher.start`` (``:251-322``), whose ready
+    queue is a deque that may repeat ids (capacity ``max_tokens``, default
+    ``2 * max_workers + max_events``)."""
+
+    def __init__(self, max_workers, max_log, max_events=65536, device=0, lib_path=None, mode="heartbeat",
+                 max_tokens=None):
+        if mode not in ("heartbeat", "deque"):
+            raise ValueError("mode must be 'heartbeat' or 'deque'")
         self.lib = _lib.load() if lib_path is None else _lib.load(lib_path)
         self.h = C.c_void_p()
-        self._create(max_workers, max_log, max_events, device)
+        self.mode = mode
+        if mode == "deque":
+            self.max_tokens = int(max_tokens if max_tokens is not None else 2 * max_workers + max(max_events, 1))
+            rc = self.lib.fb_create_deque(C.byref(self.h), int(max_workers), self.max_tokens, int(max_log),
+                                          int(max_events), int(device))
+            if rc != 0:
+                raise FaasbalError(rc, "fb_create_deque(max_workers=%d, max_tokens=%d, max_log=%d, max_events=%d, "
+                                       "device=%d) failed" % (max_workers, self.max_tokens, max_log, max_events,
+                                                              device))
+        else:
+            self._create(max_workers, max_log, max_events, device)
         self.device = int(device)
         self.max_workers = int(max_workers)
         self.max_log = int(max_log)

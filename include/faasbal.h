@@ -39,6 +39,8 @@ extern "C" {
 /* Per-event status written by a tick. */
 #define FB_EVS_APPLIED 0
 #define FB_EVS_RECONNECT 1 /* sender unknown: reply {"type":"reconnect"}, payload dropped (:356-358) */
+#define FB_EVS_UNKNOWN 2   /* deque context: result from an id without a record -- the reference
+                            * raises KeyError (:291) and its loop dies; here the message is dropped */
 
 typedef struct fb_ctx fb_ctx;
 
@@ -149,6 +151,21 @@ int fb_set_stream(fb_ctx *ctx, void *stream);
  * pairs, same content as fb_get_assignments.  Sharded contexts: only the tasks
  * given to this rank's workers, in ascending task index. */
 int fb_get_local_assignments(fb_ctx *ctx, int64_t first, int64_t n, int64_t *task, int32_t *slot);
+
+/* ---- Dispatcher without heartbeats (PushDispatcher.start, task_dispatcher.py:251-322) ----
+ * A deque context runs the start() loop per tick: no liveness, no purge, no
+ * orphans (now / tte are unused); the ready queue is a deque that may hold an id
+ * several times.  register(n) creates the record and, for n > 0, inserts the id
+ * at the left even if it is queued already (:276-281); result adds one free
+ * process and appends the id at the right when that makes exactly 1 (:284-295);
+ * other kinds are ignored; dispatch pops the left id, decrements its count and
+ * re-appends it while the count stays > 0 (:298-322).  Replaces, per tick, the
+ * message branches and the dispatch block of many loop iterations.
+ * max_tokens = deque capacity (ids counted with repetition); fb_load_state's
+ * queue may repeat slots; fb_tick_wait fails with FB_ENOSPC if a tick's deque
+ * would outgrow it.  Everything else as for fb_create. */
+int fb_create_deque(fb_ctx **out, int32_t max_workers, int64_t max_tokens, int64_t max_log,
+                    int32_t max_events, int device);
 
 /* ---- Sharded worker table (one process per GPU) ----
  * Rank r owns the global slots [slot_base, slot_base + n_workers): their
