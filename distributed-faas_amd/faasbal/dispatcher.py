@@ -27,6 +27,12 @@ tasks): the assignments are bit-identical to the reference's on it
 (tests/test_dispatcher.py replays the reference-captured goldens through this
 class with fake sockets and Redis).
 
+``start()`` runs the reference's loop without heartbeats
+(``task_dispatcher.py:251-322``) the same way, on a deque-mode balancer: no
+liveness, a ready deque that may repeat identities, results from an identity
+without a record reported instead of crashing the loop (the reference raises
+KeyError at ``:291``, after its ``HSET`` of the result).
+
 There is no CPU path: the balancer is the HIP library, and constructing this
 class without a GPU fails loudly.
 """
@@ -38,7 +44,7 @@ import time
 import numpy as np
 
 from . import codec
-from ._lib import FaasbalError
+from ._lib import FB_EVS_RECONNECT, FaasbalError
 from .balancer import GpuBalancer
 
 EV_REGISTER, EV_RECONNECT, EV_HEARTBEAT, EV_RESULT, EV_OTHER = 0, 1, 2, 3, 4
@@ -102,12 +108,29 @@ class GpuPushDispatcher:
         self.max_workers = int(max_workers)
         self.max_events = int(max_events)
         self.max_inflight = int(max_inflight)
+        self.device = device
+        self.mode = "heartbeat"
         self.balancer = GpuBalancer(self.max_workers, self.max_inflight, max_events=self.max_events, device=device)
         self._reset_host()
         W = self.max_workers
         self.balancer.load_state(np.zeros(W, np.uint8), np.zeros(W, np.int32), np.zeros(W, np.float64))
         self.ticks = 0
         self.compactions = 0
+
+    def use_loop(self, mode):
+        """Select the balancing loop before the first tick: ``"heartbeat"``
+        (``start_heartbeat``, :324-419) or ``"deque"`` (``start``, :251-322).
+        ``start()`` / ``start_heartbeat()`` call this themselves."""
+        if mode == self.mode:
+            return
+        if self.ticks:
+            raise FaasbalError(-6, "cannot switch the dispatcher loop after %d ticks" % self.ticks)
+        self.balancer.close()
+        self.balancer = GpuBalancer(self.max_workers, self.max_inflight, max_events=self.max_events,
+                                    device=self.device, mode=mode)
+        self.mode = mode
+        W = self.max_workers
+        self.balancer.load_state(np.zeros(W, np.uint8), np.zeros(W, np.int32), np.zeros(W, np.float64))
 
     def _reset_host(self):
         self.slot_of = {}                              # ZMQ identity -> slot
@@ -194,16 +217,38 @@ class GpuPushDispatcher:
                 self.pending.append(d.decode("utf-8") if isinstance(d, (bytes, bytearray)) else str(d))
 
     def tick(self):
-        """One tick of the heartbeat loop; returns the balancer's tick result dict."""
+        """One tick of the selected loop; returns the balancer's tick result dict."""
         msgs = self._drain_inbound()
         self._drain_tasks()
         return self._run(msgs)
+
+    def _deque_filter(self, msgs):
+        """start() (:271-295) acts on register and result only; a result from an
+        identity without a record raises KeyError in the reference (after the
+        HSET at :288).  Returns the messages for the balancer and the unknown
+        results (kept out of the table, their HSET done here)."""
+        keep, unknown = [], []
+        known = set(self.slot_of)
+        for wid, m, t in msgs:
+            typ = m.get("type") if isinstance(m, dict) else None
+            if typ == "register":
+                known.add(wid)
+                keep.append((wid, m, t))
+            elif typ == "result":
+                (keep if wid in known else unknown).append((wid, m, t))
+        return keep, unknown
 
     def _run(self, msgs):
         # room for every dispatch this tick can make (orphans + pending) before sequence numbers are taken
         if self.head + len(self.pending) + len(self.inflight) > self.max_inflight:
             self.compact_log()
         now = self._stamp()
+        unknown = []
+        if self.mode == "deque":
+            msgs, unknown = self._deque_filter(msgs)
+            for _, m, _ in unknown:
+                data = m["data"]
+                self.redis_client.hset(data["task_id"], mapping={"status": data["status"], "result": data["result"]})
         E = len(msgs)
         kind = np.empty(E, np.uint8)
         slot = np.empty(E, np.int32)
@@ -228,10 +273,11 @@ class GpuPushDispatcher:
         res = out["result"]
         # ---- per-message replies, in arrival order (:356-358, :374-387)
         status = out["reconnect"]
+        res["unknown_results"] = len(unknown)
         for i, (wid, m, _) in enumerate(msgs):
-            if status[i]:
+            if status[i] == FB_EVS_RECONNECT:
                 self.send_message(wid, {"type": "reconnect"})
-            elif kind[i] == EV_RESULT:
+            elif kind[i] == EV_RESULT and status[i] == 0:
                 data = m["data"]
                 self.redis_client.hset(data["task_id"], mapping={"status": data["status"], "result": data["result"]})
                 q = int(seq[i])
@@ -268,6 +314,13 @@ class GpuPushDispatcher:
 
     def start_heartbeat(self, max_ticks=None):
         """The dispatcher loop (``task_dispatcher.py:324-419``), one tick per pass."""
+        self.use_loop("heartbeat")
+        while max_ticks is None or self.ticks < max_ticks:
+            self.tick()
+
+    def start(self, max_ticks=None):
+        """The loop without heartbeats (``task_dispatcher.py:251-322``), one tick per pass."""
+        self.use_loop("deque")
         while max_ticks is None or self.ticks < max_ticks:
             self.tick()
 
@@ -287,7 +340,8 @@ class GpuPushDispatcher:
 
     @property
     def free_workers(self):
-        """The LRU queue of the reference (``:327``) as a list of identities, front first."""
+        """The LRU queue of the reference (``:327``; ``start()``: the deque of ``:254``,
+        identities possibly repeated) as a list of identities, front first."""
         st = self.balancer.read_state(with_log=False)
         return [self.identity[s] for s in st["queue"]]
 

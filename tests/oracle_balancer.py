@@ -7,12 +7,16 @@ suite runs the same tests against the real HIP library.
 """
 import numpy as np
 
-from oracle import Oracle
+from oracle import DequeOracle, Oracle
 
 
 class OracleBalancer:
-    def __init__(self, max_workers, max_log, max_events=0, device=0):
-        self.o = Oracle(max_workers, max_log)
+    def __init__(self, max_workers, max_log, max_events=0, device=0, mode="heartbeat", max_tokens=None):
+        self.mode = mode
+        self.o = DequeOracle(max_workers, max_log) if mode == "deque" else Oracle(max_workers, max_log)
+
+    def close(self):
+        pass
 
     def load_state(self, reg, free, hb, epoch=None, queue=(), log=()):
         epoch = np.zeros(len(reg), np.uint32) if epoch is None else epoch
@@ -26,5 +30,5 @@ class OracleBalancer:
             ev_seq = np.full(len(ev_kind), -1, np.int64)
         out = self.o.tick(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
         out["result"] = dict(n_assigned=len(out["assign"]), n_orphans=len(out["orphans"]),
-                             log_head=self.o.export_head())
+                             log_head=self.o.export()["head"])
         return out

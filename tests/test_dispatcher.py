@@ -207,3 +207,99 @@ def test_dispatcher_log_compaction_keeps_results(dispatcher_cls):
         assert (d.compactions > 0) == (cap == 40)
     assert runs[0] == runs[1]
     assert sum(len(x) for x in runs[0]) > 50
+
+
+DEQUE = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "deque_*.npz")))
+
+
+@pytest.mark.parametrize("path", DEQUE, ids=[os.path.basename(p)[:-4] for p in DEQUE])
+def test_dispatcher_start_replays_reference(path, dispatcher_cls):
+    """``start()`` (the loop without heartbeats, task_dispatcher.py:251-322) on the
+    vectors captured from the reference's start(): task messages, Redis writes,
+    the deque (identities repeated) and the worker records."""
+    z = np.load(path)
+    W = int(z["W"])
+    max_e = max(1, int(np.diff(z["ev_off"]).max(initial=0)))
+    env = FakeEnv()
+    d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=2 * W + max_e, max_events=max_e + 1,
+                       max_inflight=len(z["init_log"]) + len(z["exp_assign"]) + 64,
+                       redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+    d.use_loop("deque")
+    reg0 = z["init_reg"].astype(bool)
+    seq_tid, seq_slot, inflight = {}, {}, set()
+    for q, s in enumerate(z["init_log"]):
+        seq_tid[q], seq_slot[q] = "init%d" % q, int(s)
+        if s >= 0:
+            inflight.add(q)
+    d.restore(dict(reg=z["init_reg"], free=z["init_free"], hb=z["init_hb"], epoch=z["init_epoch"],
+                   queue=z["init_queue"], log=z["init_log"],
+                   identity=[wid(s) if reg0[s] else None for s in range(W)],
+                   inflight={q: (seq_tid[q], seq_slot[q]) for q in inflight}))
+    head = len(z["init_log"])
+    carried = []
+    for t in range(int(z["n_ticks"])):
+        e0, e1 = int(z["ev_off"][t]), int(z["ev_off"][t + 1])
+        exp_sent, exp_hset = [], []
+        for i in range(e0, e1):
+            k, s, v, ts = int(z["ev_kind"][i]), int(z["ev_slot"][i]), int(z["ev_val"][i]), float(z["ev_ts"][i])
+            m = {"type": KIND_MSG[k]}
+            if k == 0:
+                m["data"] = {"num_processes": v}
+            elif k == 1:
+                m["data"] = {"free_processes": v}
+            elif k == 3:
+                q = int(z["ev_seq"][i])
+                live = q >= 0 and q in inflight and seq_slot[q] == s
+                tid = seq_tid[q] if live else "stale-%d-%d" % (t, i)
+                m["data"] = {"task_id": tid, "status": "COMPLETED", "result": "r%d" % i}
+                exp_hset.append((tid, {"status": "COMPLETED", "result": "r%d" % i}))
+                if live:
+                    inflight.discard(q)
+            env.inbound.append((wid(s), codec.serialize(m).encode("utf-8"), ts))
+        new = ["t%d_%d" % (t, j) for j in range(int(z["n_new"][t]))]
+        env.tasks.extend(new)
+        env.now = float(z["now"][t])
+        a0, a1 = int(z["exp_assign_off"][t]), int(z["exp_assign_off"][t + 1])
+        pending = carried + new
+        assign = z["exp_assign"][a0:a1]
+        for k, s in enumerate(assign):
+            tid = pending[k]
+            exp_sent.append((wid(s), {"type": "task", "data": {"task_id": tid, "fn_payload": "fn_payload:" + tid,
+                                                               "param_payload": "param_payload:" + tid}}))
+            exp_hset.append((tid, {"status": "RUNNING"}))
+            seq_tid[head + k], seq_slot[head + k] = tid, int(s)
+            inflight.add(head + k)
+        head += len(assign)
+        carried = pending[len(assign):]
+        env.sent.clear()
+        env.hsets.clear()
+        d.tick()
+        assert env.sent == exp_sent, "tick %d: sent messages differ" % t
+        assert env.hsets == exp_hset, "tick %d: redis writes differ" % t
+        assert list(d.pending) == carried, "tick %d: pending tasks differ" % t
+        q0, q1 = int(z["exp_post_queue_off"][t]), int(z["exp_post_queue_off"][t + 1])
+        assert d.free_workers == [wid(s) for s in z["exp_post_queue"][q0:q1]], "tick %d: deque" % t
+        workers = d.workers
+        exp_reg = np.nonzero(z["exp_post_reg"][t])[0]
+        assert sorted(workers) == sorted(wid(s) for s in exp_reg), "tick %d: registered workers" % t
+        for s in exp_reg:
+            assert workers[wid(s)].free_processes == int(z["exp_post_free"][t][s]), "tick %d slot %d" % (t, s)
+
+
+def test_dispatcher_start_unknown_result_does_not_kill_the_loop(dispatcher_cls):
+    """The reference's start() HSETs a result from an unknown identity and then
+    raises KeyError (:288-291); the drop-in keeps the HSET and drops the message."""
+    env = FakeEnv()
+    d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=8, max_events=16, max_inflight=64,
+                       redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+    d.use_loop("deque")
+    env.inbound.append((b"ghost", codec.serialize({"type": "result", "data": {
+        "task_id": "tX", "status": "COMPLETED", "result": 1}}).encode(), 0.0))
+    env.inbound.append((b"w1", codec.serialize({"type": "register", "data": {"num_processes": 2}}).encode(), 0.0))
+    env.tasks.extend(["a", "b", "c"])
+    res = d.tick()
+    assert res["unknown_results"] == 1
+    assert env.hsets[0] == ("tX", {"status": "COMPLETED", "result": 1})
+    assert [m["data"]["task_id"] for _, m in env.sent] == ["a", "b"]
+    assert list(d.pending) == ["c"]
+    assert b"ghost" not in d.workers
