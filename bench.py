@@ -105,6 +105,76 @@ def cpu_baseline_deque(st, T, budget_s=10.0):
                        % (len(out["assign"]), os.cpu_count()))
 
 
+def bench_stream(args):
+    """BASELINE.json configs[4] on one GPU: 1M workers, every tick 64K new tasks,
+    64K results of in-flight tasks, 1K re-registrations, 10K heartbeats; the
+    clock advances 10 ms per tick so silent workers expire (churn) and their
+    in-flight tasks are redistributed.  Ticks are committed (state evolves);
+    the timed region holds K whole ticks: host staging of the events, the
+    launch, the wait for the results and the commit."""
+    from faasbal import GpuBalancer, synth
+    W = args.workers if args.workers != 65536 else 1 << 20
+    T = 65536
+    K, Wu = min(args.steps, 50), min(args.warmup, 5)  # 64K distinct results per tick from the initial log
+    st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=Wu + 2 * K, seed=2, tasks_per_tick=T, results_per_tick=T)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g = GpuBalancer(W, len(st["log"]) + (Wu + 2 * K + 2) * 2 * T, max_events=E, device=0)
+    g.load(st)
+    carried = [0]
+    stats = dict(assigned=0, orphans=0, evicted=0, events=0)
+
+    def run(tk):
+        n = carried[0] + tk["n_new"]
+        g.launch(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        r = g.wait()
+        g.commit()
+        carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
+        return r
+
+    for tk in ticks[:Wu]:
+        run(tk)
+    g.sync()
+    t0 = time.perf_counter()
+    for tk in ticks[Wu:Wu + K]:
+        r = run(tk)
+        stats["assigned"] += int(r["n_assigned"])
+        stats["orphans"] += int(r["n_orphans"])
+        stats["evicted"] += int(r["n_evicted"])
+        stats["events"] += len(tk["ev_kind"])
+    g.sync()
+    dt = time.perf_counter() - t0
+    g.timing_enable(True)
+    for tk in ticks[Wu + K:]:
+        run(tk)
+    kt = g.timing_read()
+    g.timing_enable(False)
+    kern = {k: ms / max(n, 1) * 1e3 for k, (ms, n) in kt.items()}  # us per launch
+    per_tick = {k: ms / K * 1e3 for k, (ms, n) in kt.items()}      # us per tick
+    line = {
+        "metric": "streaming task assignments/sec, configs[4] per GPU (64K tasks + churn per tick, 1M workers)",
+        "value": stats["assigned"] / dt,
+        "unit": "assignments/s",
+        "n_gpus": 1,
+        "steps": K,
+        "warmup": Wu,
+        "ms_per_step": dt * 1e3 / K,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32",
+        "data": "synthetic (faasbal.synth.zipf_state(W, seed=0, dead_frac=0) + stream_ticks(seed=2))",
+        "config": {"workload": "configs[4] per GPU: %d workers, %d new tasks + %d results + %d joins + %d heartbeats "
+                               "per tick, 10 ms per tick, committed ticks" % (W, T, T, max(1, W // 1000),
+                                                                                max(1, W // 100)),
+                   "workers": W, "events_per_tick": stats["events"] / K, "assigned_per_tick": stats["assigned"] / K,
+                   "orphans_per_tick": stats["orphans"] / K, "evicted_per_tick": stats["evicted"] / K},
+        "tick": {"device_us_per_tick": sum(per_tick.values()), "kernels_us_per_tick": per_tick,
+                 "kernels_us_per_launch": kern},
+    }
+    print(json.dumps(line), flush=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -117,7 +187,11 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--mode", default="heartbeat", choices=("heartbeat", "deque"),
                     help="deque: the loop without heartbeats (PushDispatcher.start), one GPU")
+    ap.add_argument("--workload", default="tick", choices=("tick", "stream"),
+                    help="stream: configs[4] per GPU -- committed ticks with churn and 64K results each (one GPU)")
     args = ap.parse_args()
+    if args.workload == "stream":
+        return bench_stream(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -588,7 +588,9 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
     ap.add(&c->c_arr, Qlog);
-    if (!shard) ap.add(&c->c_hb, Qlog);
+    if (!shard) {
+        ap.add(&c->c_hb, Qlog);
+    }
     ap.add(&c->qbmax, (size_t)cdiv(Qlog, kBS));
     ap.add(&c->qbm_raw, (size_t)cdiv(Qlog, kBS));
     ap.add(&c->csum, (size_t)cdiv(Qlog, kBS));
@@ -954,6 +956,7 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
     c->l_head_local = c->head_local;
     c->l_Qn = c->Qn;
     c->phase = 1;
+    c->tick += 1;  // per-launch stamp: a relaunch with other messages never sees this launch's marks
     c->l_R = choose_R(std::max(c->maxc_hint, vmax));
     c->reruns = 0;
     c->launched = true;
@@ -1025,7 +1028,6 @@ int fb_tick_commit(fb_ctx *c) {
     c->head_local += c->shard ? c->last.n_local : 0;
     c->Qn = c->last.queue_len;
     c->maxc_hint = std::max(1, c->last.max_free);
-    c->tick += 1;
     c->launched = c->waited = false;
     c->phase = 0;
     return FB_OK;

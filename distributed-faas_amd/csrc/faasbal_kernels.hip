@@ -206,6 +206,50 @@ __device__ __forceinline__ T block_reduce_max(T v, T *lds4) {
     return m;
 }
 
+// Exclusive scan of n counts cnt[i * cs] into pre[i * ps] by one workgroup;
+// returns the total.  Every thread owns a contiguous run of ceil(n / 256)
+// entries and issues its loads 16 at a time, so the whole array costs one block
+// scan instead of one per 256 entries.  In place (pre == cnt) is allowed: a
+// thread reloads a group of its own run before storing into it.
+template <typename TO>
+__device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt, size_t cs, int n, TO *pre,
+                                                            size_t ps, unsigned long long *l4) {
+    const int per = (n + kBS - 1) / kBS;
+    const int i0 = (int)threadIdx.x * per;
+    unsigned long long sum = 0;
+    for (int j0 = 0; j0 < per; j0 += 16) {
+        // unconditional loads of clamped indices, masked afterwards: a guarded
+        // load compiles to a branch with its own wait, one round trip per entry
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = min(i0 + j0 + j, n - 1);
+            v[j] = cnt[(size_t)i * cs];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) sum += (j0 + j < per && i0 + j0 + j < n) ? v[j] : 0u;
+    }
+    unsigned long long tot;
+    unsigned long long run = block_excl_scan<unsigned long long>(sum, l4, tot);
+    for (int j0 = 0; j0 < per; j0 += 16) {
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = min(i0 + j0 + j, n - 1);
+            v[j] = cnt[(size_t)i * cs];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = i0 + j0 + j;
+            if (j0 + j < per && i < n) {
+                pre[(size_t)i * ps] = (TO)run;
+                run += v[j];
+            }
+        }
+    }
+    return tot;
+}
+
 // ---------------------------------------------------------------- radix sort
 // Stable LSD radix sort of (key = slot, val = event index), 8-bit digits.
 __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift,
@@ -214,26 +258,20 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ ke
     cnt[threadIdx.x] = 0;
     __syncthreads();
     const int base = blockIdx.x * kRsTile;
+    uint32_t kk[kRsItems];  // every key load in flight before the first use
 #pragma unroll
-    for (int j = 0; j < kRsItems; ++j) {
-        int e = base + j * kBS + threadIdx.x;
-        if (e < n) atomicAdd(&cnt[(keys[e] >> shift) & 255u], 1u);
-    }
+    for (int j = 0; j < kRsItems; ++j) kk[j] = keys[min(base + j * kBS + (int)threadIdx.x, n - 1)];
+#pragma unroll
+    for (int j = 0; j < kRsItems; ++j)
+        if (base + j * kBS + (int)threadIdx.x < n) atomicAdd(&cnt[(kk[j] >> shift) & 255u], 1u);
     __syncthreads();
     hist[(size_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
 }
 
-// In-place exclusive scan of n entries by one workgroup.
-__global__ __launch_bounds__(kBS) void k_scan_1wg(uint32_t *__restrict__ a, int n) {
-    __shared__ uint32_t l4[kWaves];
-    uint32_t carry = 0;
-    for (int base = 0; base < n; base += kBS) {
-        int i = base + threadIdx.x;
-        uint32_t v = i < n ? a[i] : 0u, tot;
-        uint32_t ex = block_excl_scan<uint32_t>(v, l4, tot);
-        if (i < n) a[i] = carry + ex;
-        carry += tot;
-    }
+// In-place exclusive scan of n entries by one workgroup (runs per thread).
+__global__ __launch_bounds__(kBS) void k_scan_1wg(uint32_t *a, int n) {
+    __shared__ unsigned long long l4[kWaves];
+    run_excl_scan<uint32_t>(a, 1, n, a, 1, l4);
 }
 
 __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
@@ -244,15 +282,23 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
     __shared__ uint32_t wcnt[kWaves][256];
     base[threadIdx.x] = hist[(size_t)threadIdx.x * nblk + blockIdx.x];
     const int tile = blockIdx.x * kRsTile;
-    const int lane = lane_id(), w = wave_id();
+    const int w = wave_id();
+    // the tile's keys and values loaded up front (clamped, all in flight at once)
+    uint32_t kk[kRsItems], vv[kRsItems];
+#pragma unroll
+    for (int j = 0; j < kRsItems; ++j) {
+        const int e = tile + j * kBS + (int)threadIdx.x, ec = min(e, n - 1);
+        kk[j] = kin[ec];
+        vv[j] = identity_vals ? (uint32_t)e : vin[ec];
+    }
+#pragma unroll
     for (int j = 0; j < kRsItems; ++j) {
 #pragma unroll
         for (int q = 0; q < kWaves; ++q) wcnt[q][threadIdx.x] = 0;
         __syncthreads();
         const int e = tile + j * kBS + threadIdx.x;
         const bool valid = e < n;
-        uint32_t key = valid ? kin[e] : 0u;
-        uint32_t val = valid ? (identity_vals ? (uint32_t)e : vin[e]) : 0u;
+        const uint32_t key = kk[j], val = vv[j];
         uint32_t d = (key >> shift) & 255u;
         uint64_t peers = __ballot(valid);
 #pragma unroll
@@ -276,7 +322,6 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
         base[threadIdx.x] += add;
         __syncthreads();
     }
-    (void)lane;
 }
 
 // ------------------------------------------------------------ event apply
@@ -461,10 +506,14 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
 __device__ __forceinline__ bool is_dead(const TickArgs &a, const Cur &c) { return c.reg && ((a.now - c.hb) > a.tte); }
 
 // Global slot at logical LRU position pos of fronts ++ queue ++ backs, or -1.
-// One load from the list the position falls in (no branch per list).
+// One load from the list the position falls in (no branch per list).  The list
+// pointers go through registers first: a select between the fields' addresses
+// would keep the kernels' argument copy in scratch.
 __device__ __forceinline__ int lq_slot(const TickArgs &a, int64_t pos) {
     const bool fr = pos < a.E, qu = !fr && pos < a.E + a.Qn;
-    const int32_t *p = fr ? a.front_list : (qu ? a.queue_in : a.back_list);
+    const int32_t *pf = a.front_list, *pq = a.queue_in, *pb = a.back_list;
+    asm("" : "+s"(pf), "+s"(pq), "+s"(pb));
+    const int32_t *p = fr ? pf : (qu ? pq : pb);
     const int64_t i = fr ? pos : (qu ? pos - a.E : pos - a.E - a.Qn);
     return p[i] - (qu ? 0 : 1);
 }
@@ -539,6 +588,22 @@ __device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int
     }
 }
 
+// ------------------------------------------------------------ specialisations
+// The tick kernels are instantiated per tick kind: idle (no messages -- every
+// message path folds away, the benchmark's headline tick), message ticks, and
+// the deque loop (PushDispatcher.start).  The launcher picks the instance that
+// matches the argument block; each kernel works on a copy with those fields
+// fixed, so the inlined helpers constant-fold on them -- and the copy loads the
+// whole block once at entry instead of one scalar fetch (and wait) per field at
+// its first use.
+constexpr int kModeIdle = 0, kModeEvents = 1, kModeDeque = 2;
+template <int MODE>
+__device__ __forceinline__ TickArgs specialise(TickArgs a) {
+    if (MODE == kModeIdle) a.E = 0;
+    a.deque = MODE == kModeDeque ? 1 : 0;
+    return a;
+}
+
 // ------------------------------------------------------------ slot purge
 // Heartbeat purge of every slot (purge_workers, :241-249): liveness, the
 // died-registration bitmap, next free_processes (INT32_MIN = no live record).
@@ -569,7 +634,9 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
     if (threadIdx.x == 0) a.wcnt[blk] = l4[0] + l4[1] + l4[2] + l4[3];
 }
 
-__global__ __launch_bounds__(kBS) void k_slots(TickArgs a) {
+template <int MODE>
+__global__ __launch_bounds__(kBS) void k_slots(TickArgs a_) {
+    const TickArgs a = specialise<MODE>(a_);
     __shared__ uint32_t l4[kWaves];
     STAMP(a, 0, 0);
     slots_body(a, blockIdx.x, l4);
@@ -589,7 +656,9 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
 // F-blocks flag orphaned log entries (died bitmap in LDS); Q-blocks compute the
 // effective free count c of every LRU position and the block's count of c > r
 // for every round r (table laid out [block][round]).
-__global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
+template <int MODE>
+__global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
+    const TickArgs a = specialise<MODE>(a_);
     extern __shared__ __attribute__((aligned(16))) unsigned long long dyn[];
     __shared__ uint32_t l4[kWaves];
     __shared__ int32_t m4[kWaves];
@@ -750,11 +819,14 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
         int s = -1, ls = -1;
         int32_t raw = INT32_MIN;  // INT32_MIN: no live record (or not mine)
         double hbq = 0.0;
-        if (a.qaos && a.E == 0 && !a.shard) {
-            // no messages this tick: the committed queue's records ride along by position
-            // (queued slots are registered), one coalesced pass instead of slot gathers
-            hbq = a.qhb_in[pos];
-            const int32_t fq = a.qfree_in[pos];
+        const int64_t q = pos - a.E;  // committed queue position (fronts come first)
+        const int64_t qc = q < 0 ? 0 : (q < a.Qn ? q : (a.Qn > 0 ? a.Qn - 1 : 0));
+        if (a.qaos && q >= 0 && q < a.Qn && (a.E == 0 || a.touched[a.queue_in[qc]] != a.tick)) {
+            // a committed entry whose slot got no message this tick: its record rides
+            // along by position (queued slots are registered) -- one coalesced pass
+            // plus one 4-byte stamp gather instead of the slot's record gathers
+            hbq = a.qhb_in[q];
+            const int32_t fq = a.qfree_in[q];
             raw = ((a.now - hbq) > a.tte) ? INT32_MIN : fq;
         } else {
             s = lq_slot(a, pos);
@@ -766,7 +838,9 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a) {
                     hbq = cu.hb;
                 } else {
                     raw = a.free_out[ls];
-                    hbq = a.hbe[ls].hb;
+                    // the heartbeat after this tick's messages rides along into the next queue
+                    const double h0 = a.hbe[ls].hb, h1 = a.post_hb[ls];
+                    hbq = (a.E > 0 && a.touched[ls] == a.tick) ? h1 : h0;
                 }
             }
         }
@@ -946,49 +1020,6 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
 }
 
 // ------------------------------------------------------------ k_plan (large grids only)
-// Exclusive scan of n counts cnt[i * cs] into pre[i * ps] by one workgroup;
-// returns the total.  Every thread owns a contiguous run of ceil(n / 256)
-// entries and issues its loads 16 at a time, so the whole row costs one block
-// scan instead of one per 256 entries.
-__device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *__restrict__ cnt, size_t cs, int n,
-                                                            int64_t *__restrict__ pre, size_t ps,
-                                                            unsigned long long *l4) {
-    const int per = (n + kBS - 1) / kBS;
-    const int i0 = (int)threadIdx.x * per;
-    unsigned long long sum = 0;
-    for (int j0 = 0; j0 < per; j0 += 16) {
-        // unconditional loads of clamped indices, masked afterwards: a guarded
-        // load compiles to a branch with its own wait, one round trip per entry
-        uint32_t v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int i = min(i0 + j0 + j, n - 1);
-            v[j] = cnt[(size_t)i * cs];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) sum += (j0 + j < per && i0 + j0 + j < n) ? v[j] : 0u;
-    }
-    unsigned long long tot;
-    unsigned long long run = block_excl_scan<unsigned long long>(sum, l4, tot);
-    for (int j0 = 0; j0 < per; j0 += 16) {
-        uint32_t v[16];
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int i = min(i0 + j0 + j, n - 1);
-            v[j] = cnt[(size_t)i * cs];
-        }
-#pragma unroll
-        for (int j = 0; j < 16; ++j) {
-            const int i = i0 + j0 + j;
-            if (j0 + j < per && i < n) {
-                pre[(size_t)i * ps] = (int64_t)run;
-                run += v[j];
-            }
-        }
-    }
-    return tot;
-}
-
 // wg 0: orphan block offsets + O; wg 1: evicted block offsets; wg 2: max c and
 // capacity; wg 3+r: exclusive scan of round r's counts across queue blocks.
 __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
@@ -1099,7 +1130,9 @@ struct EmitLds {
     int32_t wpos[kWaves][kBS];  // S(r) + rank base (task index base), r <= L
 };
 
-__global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
+template <int MODE>
+__global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
+    const TickArgs a = specialise<MODE>(a_);
     __shared__ EmitLds E_;
     __shared__ uint32_t red[kWaves][4];
     __shared__ unsigned long long red64[kWaves];
@@ -1332,7 +1365,9 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a) {
 constexpr int kTabLd2 = 8;  // int4 table loads per thread (tail loop beyond 8192 entries)
 constexpr int kRCh = 3;     // 64-round chunks: rounds 0 .. L+1 <= 129
 
-__global__ __launch_bounds__(kBS) void k_emit2(TickArgs a) {
+template <int MODE>
+__global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
+    const TickArgs a = specialise<MODE>(a_);
     __shared__ uint32_t part[kWaves * 32][9];  // per-wave class partials
     __shared__ uint32_t red[kWaves][4];
     __shared__ uint32_t pre_c[kRFused];        // this block's prefix of round r
@@ -1856,14 +1891,23 @@ void launch_ev_apply(const EvArgs &a, Stream st) {
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
     hipExtLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st.s, st.e0, st.e1, 0, err, seed);
 }
+static int tick_mode(const TickArgs &a) { return a.deque ? kModeDeque : (a.E == 0 ? kModeIdle : kModeEvents); }
+#define FB_LAUNCH_MODE(K, grid, lds, st, a)                                                              \
+    do {                                                                                             \
+        switch (tick_mode(a)) {                                                                      \
+        case kModeIdle: hipExtLaunchKernelGGL(K<kModeIdle>, grid, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;    \
+        case kModeEvents: hipExtLaunchKernelGGL(K<kModeEvents>, grid, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break; \
+        default: hipExtLaunchKernelGGL(K<kModeDeque>, grid, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;           \
+        }                                                                                            \
+    } while (0)
 void launch_slots(const TickArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_slots, dim3(a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    FB_LAUNCH_MODE(k_slots, dim3(a.nbw), 0, st, a);
 }
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
     const int nbw = (a.shard == 2 || !a.slots_in_scan) ? 0 : a.nbw;
     const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;
-    hipExtLaunchKernelGGL(k_scan, dim3(nbf + nbw + a.nbq), dim3(kBS), nbf ? lds : 0, st.s, st.e0, st.e1, 0, a);
+    FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
 }
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
     const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
@@ -1873,10 +1917,10 @@ void launch_plan(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_emit(const TickArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_emit, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
 }
 void launch_emit2(const TickArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_emit2, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    FB_LAUNCH_MODE(k_emit2, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

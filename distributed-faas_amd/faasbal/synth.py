@@ -227,3 +227,41 @@ def churn_ticks(st, n_ticks, seed=2, tasks_per_tick=1024, join_frac=0.001,
                           ev_pick=rng.integers(0, 2 ** 31, E).astype(np.uint32),
                           ev_seq=np.full(E, -1, np.int64)))
     return ticks
+
+
+def stream_ticks(st, n_ticks, seed=2, tasks_per_tick=65536, results_per_tick=65536, join_frac=0.001,
+                 hb_frac=0.01, now0=1000.0, dt=0.01):
+    """Config 5 (BASELINE.json configs[4]) per GPU: every tick ``tasks_per_tick``
+    new tasks, ``results_per_tick`` results of distinct in-flight tasks of the
+    initial log (their ``ev_seq`` resolved here, so no host model of the GPU's
+    assignments is needed), ``join_frac`` re-registrations and ``hb_frac``
+    heartbeats; the clock advances ``dt`` per tick, so workers that send
+    nothing age towards the timeout and die (churn)."""
+    rng = _rng(seed)
+    W = int(st["W"])
+    log = st["log"]
+    inflight = np.nonzero(log >= 0)[0]
+    order = rng.permutation(inflight)
+    need = n_ticks * results_per_tick
+    if need > len(order):
+        raise ValueError("initial log holds %d in-flight tasks, %d results requested" % (len(order), need))
+    ticks = []
+    now = now0
+    nj, nh = max(1, int(join_frac * W)), max(1, int(hb_frac * W))
+    for t in range(n_ticks):
+        prev = now
+        now = prev + dt
+        seq = order[t * results_per_tick:(t + 1) * results_per_tick].astype(np.int64)
+        joins = rng.integers(0, W, nj)
+        hbs = rng.integers(0, W, nh)
+        kinds = np.concatenate([np.full(nj, EV_REGISTER), np.full(nh, EV_HEARTBEAT),
+                                np.full(len(seq), EV_RESULT)]).astype(np.uint8)
+        slots = np.concatenate([joins, hbs, log[seq]]).astype(np.int32)
+        vals = np.concatenate([rng.integers(1, 33, nj), np.zeros(nh + len(seq), int)]).astype(np.int32)
+        seqs = np.concatenate([np.full(nj + nh, -1, np.int64), seq])
+        perm = rng.permutation(len(kinds))
+        E = len(kinds)
+        ts = np.sort(prev + dt * rng.random(E))
+        ticks.append(dict(now=float(now), n_new=int(tasks_per_tick), ev_kind=kinds[perm], ev_slot=slots[perm],
+                          ev_val=vals[perm], ev_ts=ts, ev_seq=seqs[perm]))
+    return ticks

@@ -294,3 +294,40 @@ def test_random_multitick_split_slots(split_slots, seed):
 
 def test_config4_split_slots(split_slots):
     test_config4_single_gpu_full_size()
+
+
+def test_relaunch_with_other_messages_is_clean():
+    """A launched-but-abandoned tick (no commit) must leave no marks: the next
+    launch, with other messages, equals the oracle run without the first."""
+    for seed in range(4):
+        scen = synth.random_scenario(4100 + seed, W=300, n_ticks=3, max_events=300, max_new=500)
+        g, o = _pair(_state(scen), len(scen["init_log"]) + 40000)
+        carried = 0
+        for t, tk in enumerate(scen["ticks"]):
+            n = carried + tk["n_new"]
+            # an abandoned launch with the events of a different slot mapping
+            g.launch(tk["now"], scen["tte"], tk["ev_kind"], (tk["ev_slot"] * 7 + 3) % scen["W"], tk["ev_val"],
+                     tk["ev_ts"], None, n)
+            g.wait()
+            args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"],
+                    np.full(len(tk["ev_kind"]), -1, np.int64), n)
+            a, b = g.tick(*args), o.tick(*args)
+            _cmp_out(a, b, t)
+            _cmp_state(g, o, t)
+            carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def test_stream_ticks_vs_oracle():
+    """configs[4] event mix (results of in-flight tasks, joins, heartbeats,
+    expiry by clock) at reduced size, committed ticks."""
+    st = synth.zipf_state(W=8192, seed=0, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=6, seed=2, tasks_per_tick=4096, results_per_tick=4096, dt=1.5)
+    g, o = _pair(st, len(st["log"]) + 6 * 8192 + 16, max_events=8192)
+    carried = 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp_out(a, b, t)
+        _cmp_state(g, o, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])

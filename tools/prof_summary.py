@@ -20,7 +20,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short(name):
     """Kernel symbol -> the timer name bench.py reports (k_emit2 is the fused 'emit')."""
-    n = name.split("(")[0].split("::")[-1].replace("k_", "", 1)
+    n = name.split("(")[0].split("<")[0].split("::")[-1].replace("k_", "", 1)
     return "emit" if n == "emit2" else n
 
 
