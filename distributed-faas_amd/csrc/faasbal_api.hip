@@ -267,6 +267,7 @@ int choose_R(int32_t maxc) {
 
 // Enqueue every kernel of the tick described by c->l_* (events already on device).
 int enqueue_tick(fb_ctx *c) {
+
     const int E = c->l_E;
     const int W = c->W;
     const int R = c->l_R;
@@ -449,16 +450,22 @@ int enqueue_tick(fb_ctx *c) {
         a.opre = c->opre;
         a.oA = c->oA;
     }
+#ifdef FAASBAL_STAMPS
     {
+        // diagnostic stamp rows (stamps builds only); grown geometrically -- hipFree
+        // synchronises the device
         const size_t need = (size_t)4 * (nbw + nbf + nbq) * 16 + 16;
         if (need > c->dbg_n) {
+            HIPCHK(c, hipStreamSynchronize(c->stream));
             hipFree(c->dbg);
             c->dbg = nullptr;
-            if ((rc = dalloc(c, &c->dbg, need))) return rc;
-            c->dbg_n = need;
+            const size_t cap = std::max(need, 2 * c->dbg_n);
+            if ((rc = dalloc(c, &c->dbg, cap))) return rc;
+            c->dbg_n = cap;
         }
         a.dbg = c->dbg;
     }
+#endif
     if (a.shard == 1) {
         // phase 1: own slots' purge, orphan flags and free counts into the exchange buffer
         if (!a.slots_in_scan) {
@@ -916,18 +923,13 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
     if (n_events && (!kind || !slot || !val || !ts))
         return fail(c, FB_EINVAL, "event arrays must be non-NULL");
     const int E = n_events;
+    // One pass over the caller's arrays: validate (branch-free; the per-event loop
+    // below runs only to name the first offending event) while staging them into
+    // pinned memory, then one async copy per array.
+    const uint32_t Wv = (uint32_t)(c->shard ? c->W_global : c->W);
     int32_t vmax = 0;
-    for (int i = 0; i < E; ++i) {
-        const int32_t Wv = c->shard ? c->W_global : c->W;
-        if (slot[i] < 0 || slot[i] >= Wv) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %d)", i, slot[i], Wv);
-        if (kind[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, kind[i]);
-        if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
-            return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
-        if (kind[i] == FB_EV_REGISTER || kind[i] == FB_EV_RECONNECT) vmax = std::max(vmax, val[i]);
-    }
     HIPCHK(c, hipSetDevice(c->device));
     if (E) {
-        // stage into pinned memory, then one async copy per array
         char *h = (char *)c->h_stage;
         const size_t ecap = (size_t)c->E_cap;
         uint8_t *hk = (uint8_t *)h;
@@ -936,12 +938,28 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
         double *ht = (double *)(h + ecap * 9);
         int64_t *hq = (int64_t *)(h + ecap * 17);
         HIPCHK(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
-        memcpy(hk, kind, E);
-        memcpy(hs, slot, (size_t)E * 4);
-        memcpy(hv, val, (size_t)E * 4);
-        memcpy(ht, ts, (size_t)E * 8);
-        if (seq) memcpy(hq, seq, (size_t)E * 8);
-        else for (int i = 0; i < E; ++i) hq[i] = -1;
+        uint32_t bad = 0;
+        double prev = ts[0];
+        for (int i = 0; i < E; ++i) {
+            const uint8_t k = kind[i];
+            const int32_t sl = slot[i], v = val[i];
+            const double t = ts[i];
+            bad |= (uint32_t)((uint32_t)sl >= Wv) | (uint32_t)(k > FB_EV_OTHER) | (uint32_t)!(t <= now) |
+                   (uint32_t)(t < prev);
+            prev = t;
+            vmax = std::max(vmax, k <= FB_EV_RECONNECT ? v : 0);
+            hk[i] = k;
+            hs[i] = sl;
+            hv[i] = v;
+            ht[i] = t;
+            hq[i] = seq ? seq[i] : -1;
+        }
+        for (int i = 0; bad && i < E; ++i) {
+            if ((uint32_t)slot[i] >= Wv) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %u)", i, slot[i], Wv);
+            if (kind[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, kind[i]);
+            if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
+                return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
+        }
         HIPCHK(c, hipMemcpyAsync(c->ev_kind, hk, E, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->ev_slot, hs, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
         HIPCHK(c, hipMemcpyAsync(c->ev_val, hv, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
