@@ -292,10 +292,7 @@ int enqueue_tick(fb_ctx *c) {
         if (c->phase != 2) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
     }
     if (E > 0 && !(c->shard && c->phase == 2)) {
-        if (!c->shard) {
-            HIPCHK(c, hipMemsetAsync(front, 0, sizeof(int32_t) * E, c->stream));
-            HIPCHK(c, hipMemsetAsync(back, 0, sizeof(int32_t) * E, c->stream));
-        }
+
         // stable radix sort of events by slot
         int bits = 1;
         while ((1ll << bits) < (int64_t)(c->shard ? c->W_global : W)) ++bits;
@@ -305,8 +302,9 @@ int enqueue_tick(fb_ctx *c) {
         for (int ps = 0; ps < passes; ++ps) {
             Timer t(c, "rs_sort");
             uint32_t *kout = c->keys[ps & 1], *vout = c->vals[ps & 1];
-            launch_rs_hist(kin, E, 8 * ps, c->rs_hist, nb, t.first());
-            launch_scan_1wg(c->rs_hist, 256 * nb, t.mid());
+            // pass 0 also clears the one-GPU front / back lists (sharded: zeroed with the exchange buffer)
+            const bool z = ps == 0 && !c->shard;
+            launch_rs_hist(kin, E, 8 * ps, c->rs_hist, nb, z ? front : nullptr, z ? back : nullptr, t.first());
             launch_rs_scatter(kin, vin, kout, vout, E, 8 * ps, c->rs_hist, nb, ps == 0 ? 1 : 0, t.last());
             kin = kout;
             vin = vout;

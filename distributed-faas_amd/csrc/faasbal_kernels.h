@@ -194,8 +194,8 @@ struct Stream {
     Stream(hipStream_t s_) : s(s_) {}
     Stream(hipStream_t s_, hipEvent_t a, hipEvent_t b) : s(s_), e0(a), e1(b) {}
 };
-void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, Stream st);
-void launch_scan_1wg(uint32_t *a, int n, Stream st);
+void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1,
+                    Stream st);
 void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,
                        int shift, const uint32_t *hist, int nblk, int identity_vals, Stream st);
 void launch_ev_apply(const EvArgs &a, Stream st);

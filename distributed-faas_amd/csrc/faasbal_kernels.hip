@@ -1,7 +1,7 @@
 // faasbal_kernels.hip -- CDNA4 (gfx950) kernels of one balancer tick.
 //
 // Tick pipeline, every kernel 256 threads = 4 wave64:
-//   [E>0]  k_rs_hist / k_rs_scan / k_rs_scatter   stable LSD radix sort of events by slot
+//   [E>0]  k_rs_hist / k_rs_scatter   stable LSD radix sort of events by slot (8-bit digits)
 //   [E>0]  k_ev_apply     per-slot sequential message semantics (task_dispatcher.py:347-387)
 //          k_slots        heartbeat purge of every slot (is_alive :209-212, purge_workers :241-249)
 //          k_scan         log role: orphan flags per block; queue role: effective free count c
@@ -252,12 +252,24 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 
 // ---------------------------------------------------------------- radix sort
 // Stable LSD radix sort of (key = slot, val = event index), 8-bit digits.
+// (pass 0 also clears the tick's front / back lists, which k_ev_apply fills)
 __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift,
-                                                 uint32_t *__restrict__ hist, int nblk) {
+                                                 uint32_t *__restrict__ hist, int nblk, int32_t *__restrict__ zero0,
+                                                 int32_t *__restrict__ zero1) {
     __shared__ uint32_t cnt[256];
     cnt[threadIdx.x] = 0;
     __syncthreads();
     const int base = blockIdx.x * kRsTile;
+    if (zero0) {
+#pragma unroll
+        for (int j = 0; j < kRsItems; ++j) {
+            const int e = base + j * kBS + (int)threadIdx.x;
+            if (e < n) {
+                zero0[e] = 0;
+                zero1[e] = 0;
+            }
+        }
+    }
     uint32_t kk[kRsItems];  // every key load in flight before the first use
 #pragma unroll
     for (int j = 0; j < kRsItems; ++j) kk[j] = keys[min(base + j * kBS + (int)threadIdx.x, n - 1)];
@@ -268,19 +280,33 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ ke
     hist[(size_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
 }
 
-// In-place exclusive scan of n entries by one workgroup (runs per thread).
-__global__ __launch_bounds__(kBS) void k_scan_1wg(uint32_t *a, int n) {
-    __shared__ unsigned long long l4[kWaves];
-    run_excl_scan<uint32_t>(a, 1, n, a, 1, l4);
-}
-
 __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                     uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int n,
                                                     int shift, const uint32_t *__restrict__ hist, int nblk,
                                                     int identity_vals) {
     __shared__ uint32_t base[256];
     __shared__ uint32_t wcnt[kWaves][256];
-    base[threadIdx.x] = hist[(size_t)threadIdx.x * nblk + blockIdx.x];
+    __shared__ uint32_t l4[kWaves];
+    {
+        // this block's base per digit straight from the raw [digit][block] counts
+        // (no separate scan launch): thread d sums digit d over all blocks and over
+        // the blocks before this one, then one block scan over the digit totals
+        const int d = threadIdx.x;
+        uint32_t tot = 0, pre = 0;
+        for (int j0 = 0; j0 < nblk; j0 += 32) {
+            uint32_t v[32];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) v[j] = hist[(size_t)d * nblk + min(j0 + j, nblk - 1)];
+#pragma unroll
+            for (int j = 0; j < 32; ++j) {
+                const uint32_t x = (j0 + j < nblk) ? v[j] : 0u;
+                tot += x;
+                pre += (j0 + j < (int)blockIdx.x) ? x : 0u;
+            }
+        }
+        uint32_t all;
+        base[d] = block_excl_scan_u32(tot, l4, all) + pre;
+    }
     const int tile = blockIdx.x * kRsTile;
     const int w = wave_id();
     // the tile's keys and values loaded up front (clamped, all in flight at once)
@@ -1874,11 +1900,10 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
 // ------------------------------------------------------------ launchers
 namespace fb {
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
-void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, Stream st) {
-    hipExtLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kBS), 0, st.s, st.e0, st.e1, 0, keys, n, shift, hist, nblk);
-}
-void launch_scan_1wg(uint32_t *a, int n, Stream st) {
-    hipExtLaunchKernelGGL(k_scan_1wg, dim3(1), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a, n);
+void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1,
+                    Stream st) {
+    hipExtLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kBS), 0, st.s, st.e0, st.e1, 0, keys, n, shift, hist, nblk,
+                          zero0, zero1);
 }
 void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,
                        int shift, const uint32_t *hist, int nblk, int identity_vals, Stream st) {
