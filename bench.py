@@ -31,13 +31,33 @@ def tick_bytes(W, Q, F, O, N, E=0):
     return 16 * W + 8 * W + 4 * (N - O) + 4 * F + 8 * O + 17 * E
 
 
-def emit_bytes(W, Q, F, O, N, Qn_out):
-    """Algorithmic bytes of k_emit: assignment log writes (4 B/task), the
-    c-array and queue reads (4+4 B per LRU position), free_processes
-    read-modify-write (8 B per queued worker), next queue (4 B/entry),
-    in-flight log re-read for orphan compaction (4 B/entry) and orphan ids
-    (8 B each)."""
-    return 4 * N + 8 * Q + 8 * Q + 4 * Qn_out + 4 * F + 8 * O
+def emit_bytes(W, Q, F, O, N, Qn_out, n_evicted):
+    """Algorithmic bytes of one k_emit launch.  Queue role, per LRU
+    position: its c, heartbeat and slot (4+8+4 B read), next free count and
+    queued flag of its worker (4+1 B written); per task its slot (4 B); per
+    next-queue entry slot, free count and heartbeat (4+4+8 B).  Log role: the
+    orphan flags (1 bit per in-flight entry) and the orphan ids (8 B each).
+    Slot role: the slot status byte and the evicted ids (4 B each)."""
+    return 4 * N + 21 * Q + 16 * Qn_out + F // 8 + 8 * O + W + 4 * n_evicted
+
+
+def scan_bytes(W, Q, F, logscan=False):
+    """Algorithmic bytes of one k_scan launch: slot role per slot its record
+    (registered 1 + {hb, epoch} 16 + free 4 B) in, status byte, next free count
+    and queued flag (1+4+1 B) out; queue role per LRU position its ride-along
+    free count and heartbeat (4+8 B) in, c and heartbeat (4+8 B) out; log role
+    (unless k_logscan runs it) per in-flight entry its slot (4 B), its worker's
+    16-byte record and 1 bit of orphan flags."""
+    b = 27 * W + 24 * Q
+    if not logscan:
+        b += 20 * F + F // 8
+    return b
+
+
+def logscan_bytes(W, F):
+    """k_logscan: per in-flight entry its slot (4 B) and 1 bit of orphan flags; the
+    died bitmap (W/8 B) once."""
+    return 4 * F + F // 8 + W // 8
 
 
 def emit_deque_bytes(Q, N, Qn_out):
@@ -292,10 +312,14 @@ def main():
     if dom == "emit" and deque:
         dom_bytes = emit_deque_bytes(Q, n_assigned, int(res["queue_len"]))
     elif dom == "emit" and world == 1:
-        dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]))
+        dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]), int(res["n_evicted"]))
     elif dom == "emit":
         dom_bytes = emit_shard_bytes(Q, Q // world, F // world, int(res["n_orphans_local"]), int(res["n_local"]),
                                      int(res["queue_len"]))
+    elif dom == "scan" and world == 1:
+        dom_bytes = scan_bytes(W, Q, F, logscan="logscan" in kern)
+    elif dom == "logscan":
+        dom_bytes = logscan_bytes(W, F)
     else:
         dom_bytes = tick_bytes(W // world, Q, F // world, O // world, n_assigned // world)
     achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
