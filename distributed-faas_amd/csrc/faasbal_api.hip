@@ -35,8 +35,7 @@ struct fb_ctx {
     // committed state
     int32_t W = 0;
     int cur = 0;  // index of the committed dense buffers
-    int32_t *free_[2] = {nullptr, nullptr};
-    uint8_t *inq[2] = {nullptr, nullptr};
+    int2 *free_[2] = {nullptr, nullptr};  // {free_processes, queued} per slot
     int32_t *queue[2] = {nullptr, nullptr};
     int32_t *qfree[2] = {nullptr, nullptr};  // free_processes by LRU position (one-GPU contexts)
     double *qhb[2] = {nullptr, nullptr};     // last_heartbeat by LRU position
@@ -335,7 +334,6 @@ int enqueue_tick(fb_ctx *c) {
         a.reg = c->reg;
         a.free_in = c->free_[cur];
         a.hbe = c->hbe;
-        a.inq_in = c->inq[cur];
         a.log_slot = c->log_slot;
         a.post_reg = c->post_reg;
         a.post_free = c->post_free;
@@ -426,7 +424,6 @@ int enqueue_tick(fb_ctx *c) {
     a.P = c->P;
     a.log_slot = c->log_slot;
     a.free_out = c->free_[nxt];
-    a.inq_out = c->inq[nxt];
     a.queue_out = c->queue[nxt];
     a.qfree_out = c->qfree[nxt];
     a.qhb_out = c->qhb[nxt];
@@ -562,7 +559,6 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ArenaPlan ap;
     for (int i = 0; i < 2; ++i) {
         ap.add(&c->free_[i], W);
-        ap.add(&c->inq[i], W);
         ap.add(&c->queue[i], Wq);
         if (!shard) {
             ap.add(&c->qfree[i], Wq);
@@ -738,9 +734,10 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
     c->cur = 0;
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->free_[0], free_processes, W * 4, hipMemcpyHostToDevice));
+        std::vector<int2> fq(W);
+        for (size_t s = 0; s < W; ++s) fq[s] = make_int2(free_processes[s], inq[s]);
+        HIPCHK(c, hipMemcpy(c->free_[0], fq.data(), W * sizeof(int2), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
     }
     if (queue_len) {
         HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
@@ -780,7 +777,11 @@ int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, doubl
     const size_t W = (size_t)c->W;
     if (W) {
         if (registered) HIPCHK(c, hipMemcpy(registered, c->reg, W, hipMemcpyDeviceToHost));
-        if (free_processes) HIPCHK(c, hipMemcpy(free_processes, c->free_[c->cur], W * 4, hipMemcpyDeviceToHost));
+        if (free_processes) {
+            std::vector<int2> fq(W);
+            HIPCHK(c, hipMemcpy(fq.data(), c->free_[c->cur], W * sizeof(int2), hipMemcpyDeviceToHost));
+            for (size_t s = 0; s < W; ++s) free_processes[s] = fq[s].x;
+        }
         if (last_heartbeat || epoch) {
             std::vector<HbRec> hbv(W);
             HIPCHK(c, hipMemcpy(hbv.data(), c->hbe, W * sizeof(HbRec), hipMemcpyDeviceToHost));
@@ -845,9 +846,10 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
     c->cur = 0;
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->free_[0], free_processes, W * 4, hipMemcpyHostToDevice));
+        std::vector<int2> fq(W);
+        for (size_t s = 0; s < W; ++s) fq[s] = make_int2(free_processes[s], inq[s]);
+        HIPCHK(c, hipMemcpy(c->free_[0], fq.data(), W * sizeof(int2), hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->inq[0], inq.data(), W, hipMemcpyHostToDevice));
     }
     if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
     if (log_len) {
@@ -1119,7 +1121,8 @@ int fb_tick(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *
 
 int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     if (!c || !v) return FB_EINVAL;
-    v->free_processes = c->free_[c->cur];
+    v->free_processes = &c->free_[c->cur]->x;
+    v->free_processes_stride = (int32_t)sizeof(int2);
     v->last_heartbeat = &c->hbe->hb;
     v->last_heartbeat_stride = (int32_t)sizeof(HbRec);
     v->registered = c->reg;

@@ -88,9 +88,8 @@ struct EvArgs {
     const int64_t *ev_seq;
     uint8_t *ev_status;
     const uint8_t *reg;
-    const int32_t *free_in;
+    const int2 *free_in;  // {free_processes, queued} per slot
     const HbRec *hbe;
-    const uint8_t *inq_in;
     int32_t *log_slot;
     uint8_t *post_reg;
     int32_t *post_free;
@@ -123,7 +122,7 @@ struct TickArgs {
     // committed state
     const uint8_t *reg;
     const HbRec *hbe;
-    const int32_t *free_in;
+    const int2 *free_in;  // {free_processes, queued} per slot: one 8-byte record per worker
     const int32_t *queue_in;
     // free_processes / last_heartbeat of the committed queue, by LRU position
     // (written by the previous tick's emit; valid when qaos = 1)
@@ -149,8 +148,7 @@ struct TickArgs {
     DevTotals *P;
     // outputs
     int32_t *log_slot;
-    int32_t *free_out;  // next free_processes; INT32_MIN for slots without a live record
-    uint8_t *inq_out;
+    int2 *free_out;     // next {free_processes (INT32_MIN: no live record), queued}
     int32_t *queue_out;
     int32_t *qfree_out;
     double *qhb_out;

@@ -379,7 +379,7 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
     }
     const int k_old = a.tokcnt_in[s];
     int reg = a.reg[s];
-    int32_t fr = a.free_in[s];
+    int32_t fr = a.free_in[s].x;
     double hb = a.hbe[s].hb;
     uint32_t epoch = a.hbe[s].epoch;
     int mf = 0, nb = 0;
@@ -434,10 +434,11 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     if (a.shard && ((int)gs < a.slot_base || (int)gs >= a.slot_base + a.W)) return;  // another rank's worker
     const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
     int reg = a.reg[s];
-    int32_t fr = a.free_in[s];
+    const int2 fq = a.free_in[s];
+    int32_t fr = fq.x;
     double hb = a.hbe[s].hb;
     uint32_t epoch = a.hbe[s].epoch;
-    int inq = a.inq_in[s];
+    int inq = fq.y;
     int qstat = inq ? kQsKeep : kQsOut;
     int qidx = -1;
     int cur_is_start = reg, died_start = 0;
@@ -504,7 +505,7 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
     Cur c;
     c.reg0 = a.reg[s];
     const double hb0 = a.hbe[s].hb;
-    const int32_t fr0 = a.free_in[s];
+    const int32_t fr0 = a.free_in[s].x;
     if (a.E > 0) {
         // message tick: committed and post-message records loaded together and
         // selected afterwards (a load behind the touched test would wait for it)
@@ -644,8 +645,7 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
         evicted = !a.deque && (c.reg0 || c.t) && !alive;  // start() never deletes a record
         a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
-        a.free_out[s] = alive ? c.fr : INT32_MIN;
-        a.inq_out[s] = 0;
+        a.free_out[s] = make_int2(alive ? c.fr : INT32_MIN, 0);
         if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
             a.tokcnt_out[s] = 0;
             a.xw_out[s] = 0;
@@ -863,7 +863,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                     raw = (cu.reg && !is_dead(a, cu)) ? cu.fr : INT32_MIN;
                     hbq = cu.hb;
                 } else {
-                    raw = a.free_out[ls];
+                    raw = a.free_out[ls].x;
                     // the heartbeat after this tick's messages rides along into the next queue
                     const double h0 = a.hbe[ls].hb, h1 = a.post_hb[ls];
                     hbq = (a.E > 0 && a.touched[ls] == a.tick) ? h1 : h0;
@@ -1131,11 +1131,11 @@ __device__ __forceinline__ void deque_finish(const TickArgs &a, int64_t pos, int
     const int4 tk = a.c_tok[pos];  // {j, m, q, k}; f = q + m k + 1
     if (tk.w == 1) {
         // the worker's only token: plain stores
-        a.free_out[s] = tk.z + tk.y + 1 - (int32_t)n_q;
+        a.free_out[s].x = tk.z + tk.y + 1 - (int32_t)n_q;
         if (np >= 0) a.tokcnt_out[s] = 1;
         if (c > L && servedL) a.xw_out[s] = 1;
     } else {
-        atomicSub(&a.free_out[s], (int32_t)n_q);
+        atomicSub(&a.free_out[s].x, (int32_t)n_q);
         if (np >= 0) atomicAdd(&a.tokcnt_out[s], 1);
         if (c > L && servedL) atomicMax(&a.xw_out[s], tk.x);
     }
@@ -1342,12 +1342,12 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
                 STAMP(a, SO, 15);
                 return;
             }
-            a.free_out[s] = raw - (int32_t)n_q;
+            // the worker's next {free, queued}: one 8-byte store
+            a.free_out[s] = make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0);
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
                 a.qhb_out[np] = hbp;
-                a.inq_out[s] = 1;
             }
         }
         STAMPR(a, SO, 14);
@@ -1613,12 +1613,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 STAMP(a, SO, 15);
                 return;
             }
-            a.free_out[s] = raw - (int32_t)n_q;
+            // the worker's next {free, queued}: one 8-byte store
+            a.free_out[s] = make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0);
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
                 a.qhb_out[np] = hb0;
-                a.inq_out[s] = 1;
             }
         }
         STAMP(a, SO, 15);
@@ -1835,7 +1835,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
             if (c > L && rankL < p) n_q += 1;
-            if (own) a.free_out[ls] = raw - (int32_t)n_q;
+            if (own) a.free_out[ls].x = raw - (int32_t)n_q;
             int64_t np = -1;
             if (c > L) {
                 if (rankL >= p) np = rankL - p;
@@ -1848,7 +1848,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             }
             if (np >= 0) {
                 a.queue_out[np] = s;  // the next queue is replicated on every rank
-                if (own) a.inq_out[ls] = 1;
+                if (own) a.free_out[ls].y = 1;
             }
         }
         return;

@@ -39,7 +39,8 @@ class DeviceView(C.Structure):
     _fields_ = [("free_processes", C.c_void_p), ("last_heartbeat", C.c_void_p), ("registered", C.c_void_p),
                 ("queue", C.c_void_p), ("log_slot", C.c_void_p), ("orphans", C.c_void_p),
                 ("evicted", C.c_void_p), ("n_workers", C.c_int32), ("queue_len", C.c_int64),
-                ("log_head", C.c_int64), ("last_heartbeat_stride", C.c_int32)]
+                ("log_head", C.c_int64), ("last_heartbeat_stride", C.c_int32),
+                ("free_processes_stride", C.c_int32)]
 
 
 class FaasbalError(RuntimeError):

@@ -60,7 +60,8 @@ typedef struct fb_tick_result {
 /* Device pointers of the context's state (for zero-copy consumers, e.g.
  * torch tensors built from data_ptr).  Valid until the next fb_tick_commit. */
 typedef struct fb_device_view {
-    int32_t *free_processes; /* [n_workers]  PushWorker.free_processes (:205)  */
+    int32_t *free_processes; /* [n_workers]  PushWorker.free_processes (:205), every
+                              * free_processes_stride bytes                    */
     double *last_heartbeat;  /* [n_workers]  PushWorker.last_heartbeat (:206), every
                               * last_heartbeat_stride bytes; NaN for empty slots */
     uint8_t *registered;     /* [n_workers]  slot present in self.workers      */
@@ -71,6 +72,7 @@ typedef struct fb_device_view {
     int32_t n_workers;
     int64_t queue_len, log_head;
     int32_t last_heartbeat_stride; /* bytes between consecutive slots' heartbeats */
+    int32_t free_processes_stride; /* bytes between consecutive slots' free counts */
 } fb_device_view;
 
 /* Context: owns every device buffer.  device = HIP device ordinal. */
