@@ -1433,13 +1433,22 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             cv[k] = (uint32_t)a.csum[i < nbq1 ? i : nbq1];
         }
         // counts of c > r in the earlier segments of this block: lane i, round 64 k + i
+        // (all three earlier segments loaded unconditionally, clamped, then masked:
+        // a loop bounded by the wave id would issue one load and wait per segment)
         uint32_t segc[kRCh] = {0, 0, 0};
+        {
+            uint32_t sv[kRCh][kWaves - 1];
 #pragma unroll
-        for (int k = 0; k < kRCh; ++k) {
-            const int r = 64 * k + lane;
-            if (r < R) {
-                for (int q = 0; q < w; ++q) segc[k] += a.segcnt[(size_t)(4 * b + q) * R + r];
-            }
+            for (int k = 0; k < kRCh; ++k)
+#pragma unroll
+                for (int q = 0; q < kWaves - 1; ++q) {
+                    const int r = min(64 * k + lane, R - 1);
+                    sv[k][q] = a.segcnt[(size_t)(4 * b + q) * R + r];
+                }
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k)
+#pragma unroll
+                for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
         }
         STAMP(a, SO, 9);
         uint32_t fo = 0, wo = 0, mo = 0, co = 0;
