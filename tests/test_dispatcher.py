@@ -23,14 +23,42 @@ def wid(s):
     return b"w%06d" % int(s)
 
 
+class FakePipe:
+    """redis-py pipeline stand-in: commands queue up, ``execute`` runs them in order."""
+
+    def __init__(self, env):
+        self.env, self.cmds = env, []
+
+    def hget(self, key, field):
+        self.cmds.append(("hget", key, field))
+
+    def hset(self, key, mapping=None):
+        self.cmds.append(("hset", key, mapping))
+
+    def execute(self):
+        self.env.round_trips += 1
+        out = []
+        for op, key, arg in self.cmds:
+            if op == "hget":
+                out.append(("%s:%s" % (arg, key)).encode())
+            else:
+                self.env.hsets.append((key, dict(arg)))
+                out.append(1)
+        self.cmds = []
+        return out
+
+
 class FakeEnv:
     """ROUTER socket + poller + pub/sub + Redis client + clock, all in memory."""
 
-    def __init__(self):
+    def __init__(self, pipelines=True):
         self.inbound = collections.deque()  # (identity, frame bytes, ts)
         self.tasks = collections.deque()
         self.sent = []
         self.hsets = []
+        self.round_trips = 0
+        if pipelines:
+            self.pipeline = lambda transaction=True: FakePipe(self)
         self.now = 0.0
         self.t = 0.0
         self.sock = self
@@ -61,9 +89,11 @@ class FakeEnv:
 
     # redis
     def hget(self, key, field):
+        self.round_trips += 1
         return ("%s:%s" % (field, key)).encode()
 
     def hset(self, key, mapping=None):
+        self.round_trips += 1
         self.hsets.append((key, dict(mapping)))
 
     def clock(self):
@@ -88,14 +118,20 @@ def dispatcher_cls(request, monkeypatch):
     return D.GpuPushDispatcher
 
 
+@pytest.fixture(params=[True, False], ids=["pipelined", "per-call"])
+def pipelines(request):
+    """Redis client with pipelines (batched host I/O) or without (one round trip per command)."""
+    return request.param
+
+
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
-def test_dispatcher_replays_reference(path, dispatcher_cls):
+def test_dispatcher_replays_reference(path, dispatcher_cls, pipelines):
     GpuPushDispatcher = dispatcher_cls
     z = np.load(path)
     W = int(z["W"])
     T = int(z["n_ticks"])
     max_e = max(1, int(np.diff(z["ev_off"]).max(initial=0)))
-    env = FakeEnv()
+    env = FakeEnv(pipelines)
     d = GpuPushDispatcher("127.0.0.1", 0, float(z["tte"]), max_workers=2 * W + max_e, max_events=max_e + 1,
                           max_inflight=len(z["init_log"]) + len(z["exp_assign"]) + 64,
                           redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
@@ -213,14 +249,14 @@ DEQUE = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "dequ
 
 
 @pytest.mark.parametrize("path", DEQUE, ids=[os.path.basename(p)[:-4] for p in DEQUE])
-def test_dispatcher_start_replays_reference(path, dispatcher_cls):
+def test_dispatcher_start_replays_reference(path, dispatcher_cls, pipelines):
     """``start()`` (the loop without heartbeats, task_dispatcher.py:251-322) on the
     vectors captured from the reference's start(): task messages, Redis writes,
     the deque (identities repeated) and the worker records."""
     z = np.load(path)
     W = int(z["W"])
     max_e = max(1, int(np.diff(z["ev_off"]).max(initial=0)))
-    env = FakeEnv()
+    env = FakeEnv(pipelines)
     d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=2 * W + max_e, max_events=max_e + 1,
                        max_inflight=len(z["init_log"]) + len(z["exp_assign"]) + 64,
                        redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
@@ -303,3 +339,77 @@ def test_dispatcher_start_unknown_result_does_not_kill_the_loop(dispatcher_cls):
     assert [m["data"]["task_id"] for _, m in env.sent] == ["a", "b"]
     assert list(d.pending) == ["c"]
     assert b"ghost" not in d.workers
+
+
+def test_batched_io_round_trips(dispatcher_cls):
+    """Pipelined host I/O: 2 Redis round trips for a tick's dispatches (+1 for its
+    results) instead of 3 per task (+1 per result); same messages and writes."""
+    runs = []
+    for pipelines in (True, False):
+        env = FakeEnv(pipelines)
+        d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=16, max_events=64, max_inflight=4096,
+                           redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+        for w in range(4):
+            env.inbound.append((wid(w), codec.serialize({"type": "register", "data": {"num_processes": 8}}).encode(),
+                                0.0))
+        env.tasks.extend("t%d" % j for j in range(20))
+        env.now = 1.0
+        d.tick()
+        trips0 = env.round_trips
+        env.inbound.append((wid(0), codec.serialize({"type": "result", "data": {
+            "task_id": "t0", "status": "COMPLETED", "result": 1}}).encode(), 1.5))
+        env.tasks.extend("u%d" % j for j in range(5))
+        env.now = 2.0
+        d.tick()
+        runs.append((env.sent, env.hsets, trips0, env.round_trips - trips0))
+    (s1, h1, a1, b1), (s2, h2, a2, b2) = runs
+    assert s1 == s2 and h1 == h2
+    assert (a1, b1) == (2, 3) and (a2, b2) == (3 * 20, 1 + 3 * 5)
+
+
+def _dill_wire(obj):
+    import codecs as _c
+    import dill
+    return _c.encode(dill.dumps(obj), "base64").decode()  # helper_functions.py:5-6
+
+
+def test_codec_bytes_equal_dill_for_messages():
+    """The C-pickler path writes exactly dill's bytes for every message shape the
+    dispatcher and workers exchange."""
+    msgs = [{"type": "task", "data": {"task_id": "0f8fad5b-d9cb-469f-a165-70867728950e",
+                                      "fn_payload": "gASV" * 60, "param_payload": "gAS" * 30}},
+            {"type": "reconnect"}, {"type": "wait"}, {"type": "heartbeat"},
+            {"type": "register", "data": {"num_processes": 8}},
+            {"type": "reconnect", "data": {"free_processes": -1}},
+            {"type": "result", "data": {"task_id": "t1", "status": "COMPLETED", "result": "gASVBQ=="}},
+            {"type": "result", "data": {"task_id": "t1", "status": "FAILED", "result": None}}]
+    for m in msgs:
+        assert codec.serialize(m) == _dill_wire(m), m
+        assert codec.deserialize(codec.serialize(m)) == m
+
+
+def test_codec_random_plain_data_matches_dill():
+    hypothesis = pytest.importorskip("hypothesis")
+    st = hypothesis.strategies
+    leaves = st.one_of(st.none(), st.booleans(), st.integers(-2 ** 70, 2 ** 70),
+                       st.floats(allow_nan=False), st.text(max_size=40), st.binary(max_size=40))
+    data = st.recursive(leaves, lambda ch: st.one_of(st.lists(ch, max_size=5), st.tuples(ch, ch),
+                                                     st.dictionaries(st.text(max_size=8), ch, max_size=5)),
+                        max_leaves=20)
+
+    @hypothesis.settings(max_examples=300, deadline=None)
+    @hypothesis.given(data)
+    def check(obj):
+        assert codec.serialize(obj) == _dill_wire(obj)
+
+    check()
+
+
+def test_codec_non_plain_objects_go_through_dill():
+    import dill
+
+    def double(x):
+        return 2 * x
+    s = codec.serialize(double)
+    assert codec.deserialize(s)(21) == 42
+    assert dill.loads(__import__("codecs").decode(s.encode(), "base64"))(4) == 8
