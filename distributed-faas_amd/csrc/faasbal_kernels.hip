@@ -880,17 +880,15 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         if (a.shard == 1) a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
     }
     STAMP(a, SO, 1);
-    const uint32_t wmx = wave_max_u32((uint32_t)c);
     if (a.shard == 1) {
-        // phase 1: this rank's capacity and max c go to its exchange record (exact values)
-        const uint32_t ws = wave_sum_u32((uint32_t)c);
-        if (lane_id() == 0) {
-            atomicAdd(&a.xrec[a.rank * 4 + 1], (unsigned long long)ws);
-            atomicMax(&a.xrec[a.rank * 4 + 2], (unsigned long long)wmx);
-        }
+        // phase 1 ends with the c bytes: phase 2 re-derives capacity and max c from
+        // them (exact: sharded ticks keep every c <= 128 < 255, the byte's clamp).
+        // Per-wave atomics on one exchange word cost ~10 ns each, serialised --
+        // 14 K of them per tick at 8 ranks.
         STAMP(a, SO, 15);
         return;
     }
+    const uint32_t wmx = wave_max_u32((uint32_t)c);
     if (lane_id() == 0) m4[wave_id()] = (int32_t)wmx;
     unsigned long long csum = 0;
     for (int rc = 0; rc < a.R; rc += kBS) {
@@ -1067,22 +1065,9 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
         }
         return;
     }
-    if (bid == 2 && a.shard) {
-        // sharded: exact totals from every rank's exchange record
-        if (threadIdx.x == 0) {
-            unsigned long long O = 0, cap = 0, mx = 0;
-            for (int g = 0; g < a.world; ++g) {
-                O += a.xrec[g * 4 + 0];
-                cap += a.xrec[g * 4 + 1];
-                mx = a.xrec[g * 4 + 2] > mx ? a.xrec[g * 4 + 2] : mx;
-            }
-            a.P->O = (int64_t)O;
-            a.P->cap_total = (int64_t)cap;
-            a.P->maxc = (int32_t)mx;
-        }
-        return;
-    }
     if (bid == 2) {
+        // capacity and max c from the queue blocks (sharded phase 2: of the exchanged
+        // c bytes); sharded: every rank's orphan count from the exchange records
         int32_t mx = 0;
         unsigned long long sum = 0;
         for (int i0 = 0; i0 < a.nbq; i0 += 8 * kBS) {
@@ -1107,6 +1092,11 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
         if (threadIdx.x == 0) {
             a.P->maxc = mx;
             a.P->cap_total = (int64_t)tot;
+            if (a.shard) {
+                unsigned long long O = 0;
+                for (int g = 0; g < a.world; ++g) O += a.xrec[g * 4 + 0];
+                a.P->O = (int64_t)O;
+            }
         }
         return;
     }
