@@ -481,7 +481,7 @@ int enqueue_tick(fb_ctx *c) {
     if (a.shard == 2) {
         if (R > kRFused) return fail(c, FB_ERANGE, "sharded tick: free counts need %d rounds (limit %d)", R, kRFused);
         {
-            Timer t(c, "scan");
+            Timer t(c, "scan2");
             launch_scan(a, t.st());
         }
         {

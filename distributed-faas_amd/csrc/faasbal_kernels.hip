@@ -591,6 +591,22 @@ __device__ __forceinline__ uint32_t wave_round_counts(int c, int r0, int rn) {
     return m0 | m1 | m2 | m3;  // each lane is set by exactly one chain (others stay 0)
 }
 
+// wave_round_counts for two predicates at once: lane i gets the counts of
+// c > r0 + i over all lanes and over the lanes in own (one ballot per round).
+__device__ __forceinline__ void wave_round_counts2(int c, uint64_t own, int r0, int rn, uint32_t &all,
+                                                   uint32_t &mine) {
+    uint32_t a0 = 0, m0 = 0;
+    const int lane = lane_id();
+    for (int i = 0; i < rn; ++i) {
+        const uint64_t m = __ballot(c > r0 + i);
+        const uint32_t na = (uint32_t)__popcll(m), nm = (uint32_t)__popcll(m & own);
+        a0 = (lane == i) ? na : a0;
+        m0 = (lane == i) ? nm : m0;
+    }
+    all = a0;
+    mine = m0;
+}
+
 // Sum of cnt[i] over i < n with all loads in flight at once (n <= kPeel*256 on
 // the fused path; a tail loop covers larger n); also the sum over i < lim.
 __device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int n, int lim,
@@ -800,9 +816,13 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     int c = 0, oc = 0;
     if (a.shard == 2) {
         // phase 2 of a sharded tick: every rank's effective free counts arrived in the exchange
+        // both loads issued together (a guarded slot load would wait for the c byte first)
+        const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
+        const int cq = a.xc8[pq];
+        const int sq = lq_slot(a, pq);
         if (pos < a.Qlog) {
-            c = a.xc8[pos];
-            oc = (c > 0 && own_slot(a, lq_slot(a, pos)) >= 0) ? c : 0;
+            c = cq;
+            oc = (c > 0 && own_slot(a, sq) >= 0) ? c : 0;
         }
     } else if (a.deque) {
         // start(): c of every deque token from its worker's free count f, token count k and
@@ -891,9 +911,40 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     const uint32_t wmx = wave_max_u32((uint32_t)c);
     if (lane_id() == 0) m4[wave_id()] = (int32_t)wmx;
     unsigned long long csum = 0;
+    if (a.shard == 2) {
+        // phase 2: the round counts of all positions and of this rank's, one ballot per
+        // round for both (rounds < R <= 128: two 64-round groups at most)
+        __shared__ uint32_t owc[kWaves][kBS];
+        const uint64_t own = __ballot(oc > 0);
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+            const int r0 = g * 64;
+            uint32_t cnt = 0, ocnt = 0;
+            if (r0 < a.R && r0 < (int)wmx) {
+                int k = a.R - r0;
+                k = k < 64 ? k : 64;
+                k = k < (int)wmx - r0 ? k : (int)wmx - r0;
+                wave_round_counts2(c, own, r0, k, cnt, ocnt);
+            }
+            wc[wave_id()][g * 64 + lane_id()] = cnt;
+            owc[wave_id()][g * 64 + lane_id()] = ocnt;
+        }
+        lds_barrier();
+        uint32_t t = 0;
+        if ((int)threadIdx.x < a.R) {
+            const int r = threadIdx.x;
+            t = wc[0][r] + wc[1][r] + wc[2][r] + wc[3][r];
+            a.qcnt[(size_t)b * a.R + r] = t;
+            a.ocnt[(size_t)b * a.R + r] = owc[0][r] + owc[1][r] + owc[2][r] + owc[3][r];
+        }
+        const uint32_t ts = wave_sum_u32(t);
+        if (lane_id() == 0) l4[wave_id()] = ts;
+        lds_barrier();
+        csum = (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
+    } else
     for (int rc = 0; rc < a.R; rc += kBS) {
         const int rn = (a.R - rc) < kBS ? (a.R - rc) : kBS;
-        for (int tab = 0; tab < (a.shard == 2 ? 2 : 1); ++tab) {
+        for (int tab = 0; tab < 1; ++tab) {
             const int cc = tab ? oc : c;
 #pragma unroll
             for (int g = 0; g < kBS / 64; ++g) {
