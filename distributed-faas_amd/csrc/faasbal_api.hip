@@ -113,7 +113,7 @@ struct fb_ctx {
     int32_t slot_base = 0, W_global = 0, Wq_cap = 0;  // Wq_cap: LRU queue capacity (global slots)
     int64_t head_local = 0, l_head_local = 0;
     uint32_t *lseq = nullptr;                         // global sequence of each local log entry
-    uint32_t *ocnt = nullptr;
+    uint32_t *ocnt = nullptr, *osegcnt = nullptr;
     int64_t *opre = nullptr, *oA = nullptr;
     uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
     int64_t xcap = 0;
@@ -442,6 +442,7 @@ int enqueue_tick(fb_ctx *c) {
         a.xc8 = c->xbuf + xl.c8;
         a.xrec = (unsigned long long *)(c->xbuf + xl.rec);
         a.ocnt = c->ocnt;
+        a.osegcnt = c->osegcnt;
         a.opre = c->opre;
         a.oA = c->oA;
     }
@@ -625,6 +626,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (shard) {
         ap.add(&c->lseq, F);
         ap.add(&c->ocnt, tab);
+        ap.add(&c->osegcnt, 4 * tab);
         ap.add(&c->opre, tab);
         ap.add(&c->oA, 128);
     }

@@ -167,6 +167,7 @@ struct TickArgs {
     uint8_t *xc8;                  // exchange: min(c, 255) per LRU position (single contributor per byte)
     unsigned long long *xrec;      // exchange: per rank {O, sum c, max c, -}
     uint32_t *ocnt;                // [block][round] counts of this rank's positions
+    uint32_t *osegcnt;             // [64-position segment][round] counts of this rank's positions
     int64_t *opre, *oA;
 };
 

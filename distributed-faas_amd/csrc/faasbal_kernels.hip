@@ -928,6 +928,12 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             }
             wc[wave_id()][g * 64 + lane_id()] = cnt;
             owc[wave_id()][g * 64 + lane_id()] = ocnt;
+            // per 64-position segment: k_emit_shard's in-block rank bases
+            if (g * 64 + lane_id() < a.R) {
+                const size_t si = (size_t)(4 * b + wave_id()) * a.R + g * 64 + lane_id();
+                a.segcnt[si] = cnt;
+                a.osegcnt[si] = ocnt;
+            }
         }
         lds_barrier();
         uint32_t t = 0;
@@ -1715,65 +1721,86 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 // the exchanged counts (identical on all ranks), writes the whole next LRU queue,
 // and appends only its own workers' tasks to its log shard -- in ascending global
 // sequence, because own tasks are placed round-major by their own rank.
-struct EmitShardLds {
-    uint32_t wc[kWaves][kBS], owc[kWaves][kBS];
-    int32_t wbase[kWaves][kBS], wpos[kWaves][kBS], obase[kWaves][kBS], opos[kWaves][kBS];
-};
-
+// k_emit2's scheme with two rank systems: per wave and round, the global task
+// index base S(r) + block prefix + earlier segments (for the sequence number)
+// and the own-log base So(r) + own block prefix + own earlier segments (for the
+// log position), one register per 64 rounds, read with readlane in the round
+// loop; block prefixes from k_plan, segment counts from the phase-2 k_scan.
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
-    __shared__ EmitShardLds E_;
-    __shared__ unsigned long long red64[kWaves];
-    __shared__ int64_t S_l[kBS + 1], So_l[kBS + 1];
-    __shared__ int64_t pre_c[kBS], opre_c[kBS];
     __shared__ int32_t misc[8];
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
     if (bid < a.nbq) {
         const int b = bid;
+        const int R = a.R;
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
-        int c = 0, s = -1, ls = -1;
-        int32_t raw = INT32_MIN;
-        if (pos < a.Qlog) {
-            c = a.xc8[pos];
-            s = lq_slot(a, pos);
-            ls = s >= 0 ? own_slot(a, s) : -1;
-            if (ls >= 0) raw = a.c_arr[pos];
+        // ---- every load in flight at once (clamped indices, no branches)
+        const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
+        const int cq = a.xc8[pq];
+        const int sq = lq_slot(a, pq);
+        const int32_t rawq = a.c_arr[pq];
+        int64_t Av[kRCh], oAv[kRCh], pv[kRCh], opv[kRCh];
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k) {
+            const int r = min(64 * k + lane, R - 1);
+            Av[k] = a.A[r];
+            oAv[k] = a.oA[r];
+            pv[k] = a.qpre[(size_t)b * R + r];
+            opv[k] = a.opre[(size_t)b * R + r];
         }
-        const bool own = c > 0 && ls >= 0;
-        const int bm = a.qbm_raw[b];
+        uint32_t segc[kRCh] = {0, 0, 0}, osegc[kRCh] = {0, 0, 0};
+        {
+            uint32_t sv[kRCh][kWaves - 1], osv[kRCh][kWaves - 1];
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k)
+#pragma unroll
+                for (int q = 0; q < kWaves - 1; ++q) {
+                    const size_t si = (size_t)(4 * b + q) * R + min(64 * k + lane, R - 1);
+                    sv[k][q] = a.segcnt[si];
+                    osv[k][q] = a.osegcnt[si];
+                }
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k)
+#pragma unroll
+                for (int q = 0; q < kWaves - 1; ++q) {
+                    const bool in = q < w && 64 * k + lane < R;
+                    segc[k] += in ? sv[k][q] : 0u;
+                    osegc[k] += in ? osv[k][q] : 0u;
+                }
+        }
         const int64_t O = a.P->O;
         int64_t cap = a.P->cap_total;
         const int maxc = a.P->maxc;
-        const int rlim = maxc < a.R ? maxc : a.R;
-        if (maxc > a.R) cap = INT64_MAX;
+        const int rlim = maxc < R ? maxc : R;
+        if (maxc > R) cap = INT64_MAX;
         const int64_t N = O + a.T;
         const int64_t N_eff = N < cap ? N : cap;
-        // fill level L = max{ r in [0, maxc] : S(r) <= N_eff }
+        // ---- per wave: S(r) and So(r) (lane i of chunk k: round 64 k + i), fill level L
+        int64_t Sv[kRCh], Sov[kRCh];
         int L = 0;
-        int64_t S_L = 0;
         {
-            int64_t carry = 0;
-            for (int rc = 0; rc < rlim; rc += kBS) {
-                const int r = rc + threadIdx.x;
-                const unsigned long long v = r < rlim ? (unsigned long long)a.A[r] : 0ull;
-                unsigned long long tot;
-                const unsigned long long ex = block_excl_scan<unsigned long long>(v, red64, tot);
-                const int64_t S1 = carry + (int64_t)(ex + v);
-                const int k_w = __popcll(__ballot(r < rlim && S1 <= N_eff));
-                if (lane == 0) misc[w] = k_w;
-                S_l[threadIdx.x + 1] = S1;
-                if (threadIdx.x == 0) S_l[0] = carry;
-                lds_barrier();
-                const int k = misc[0] + misc[1] + misc[2] + misc[3];
-                L += k;
-                S_L = S_l[k];
-                lds_barrier();
-                if (k < kBS) break;
-                carry += (int64_t)tot;
+            int64_t carry = 0, ocarry = 0;
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k) {
+                const int r = 64 * k + lane;
+                const uint32_t v = r < rlim ? (uint32_t)Av[k] : 0u;
+                const uint32_t ov = r < rlim ? (uint32_t)oAv[k] : 0u;
+                const uint32_t incl = wave_incl_scan_u32(v);
+                const uint32_t oincl = wave_incl_scan_u32(ov);
+                const int64_t S1 = carry + (int64_t)incl;  // S(r + 1)
+                Sv[k] = S1 - (int64_t)v;                   // S(r)
+                Sov[k] = ocarry + (int64_t)oincl - (int64_t)ov;
+                L += __popcll(__ballot(r < rlim && S1 <= N_eff));
+                carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+                ocarry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)oincl, 63);
             }
         }
+        const int Lc = L >> 6, Ll = L & 63;
+        const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Sv[0] : (Lc == 1 ? Sv[1] : Sv[2])), Ll);
+        const int64_t oSL =
+            (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Sov[0] : (Lc == 1 ? Sov[1] : Sov[2])), Ll);
         int status = 0;
-        if (maxc > a.R && L >= a.R - 1) status = 1;
+        if (maxc > R && L >= R - 1) status = 1;
         if (a.head_local + N_eff > a.log_cap) status = 2;
         const int64_t p = N_eff - S_L;
         const int64_t AL = (L < maxc && L < rlim) ? a.A[L] : 0;
@@ -1788,108 +1815,72 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             a.hout->N_eff = status ? 0 : N_eff;
             a.hout->p = p;
             a.hout->AL = AL;
+            if (!status && AL == 0) {
+                a.hout->new_qlen = 0;
+                a.hout->n_local = oSL;  // every worker saturated: all own capacity used
+            }
         }
         if (status) return;
-        int64_t rankL = -1, orankL = 0, exL1 = 0, oSL = 0;
-        int64_t carryS = 0, carryO = 0;
-        const int wmx = (int)wave_max_u32((uint32_t)c);
+        const int c = pos < a.Qlog ? cq : 0;
+        const int s = sq;
+        const int ls = s >= 0 ? own_slot(a, s) : -1;
+        const bool own = c > 0 && ls >= 0;
         const int oc = own ? c : 0;
-        for (int rc = 0; rc <= L + 1; rc += kBS) {
-            const int rn = (L + 2 - rc) < kBS ? (L + 2 - rc) : kBS;
-            {
-                const int r = rc + threadIdx.x;
-                int64_t pr = 0, opr = 0, Av = 0, oAv = 0;
-                if ((int)threadIdx.x < rn && r < rlim) {
-                    pr = a.qpre[(size_t)b * a.R + r];
-                    opr = a.opre[(size_t)b * a.R + r];
-                    Av = a.A[r];
-                    oAv = a.oA[r];
-                }
-                unsigned long long tot, otot;
-                const unsigned long long ex = block_excl_scan<unsigned long long>((unsigned long long)Av, red64, tot);
-                const unsigned long long oex = block_excl_scan<unsigned long long>((unsigned long long)oAv, red64, otot);
-                pre_c[threadIdx.x] = pr;
-                opre_c[threadIdx.x] = opr;
-                S_l[threadIdx.x] = carryS + (int64_t)ex;
-                So_l[threadIdx.x] = carryO + (int64_t)oex;
-                carryS += (int64_t)tot;
-                carryO += (int64_t)otot;
-            }
+        // rank bases in A_r (global and own) and the task / own-log index bases per round
+        int32_t rbv[kRCh], orbv[kRCh], basev[kRCh], obasev[kRCh];
 #pragma unroll
-            for (int g = 0; g < kBS / 64; ++g) {
-                const int r0 = rc + g * 64;
-                uint32_t cnt = 0, ocnt = 0;
-                if (r0 < rc + rn && r0 < wmx) {
-                    int k = rc + rn - r0;
-                    k = k < 64 ? k : 64;
-                    k = k < wmx - r0 ? k : wmx - r0;
-                    cnt = wave_round_counts(c, r0, k);
-                    ocnt = wave_round_counts(oc, r0, k);
-                }
-                E_.wc[w][g * 64 + lane] = cnt;
-                E_.owc[w][g * 64 + lane] = ocnt;
-            }
-            lds_barrier();
-            for (int e = threadIdx.x; e < kWaves * rn; e += kBS) {
-                const int ww = e / rn, i = e - ww * rn;
-                const int r = rc + i;
-                int64_t rb = pre_c[i], orb = opre_c[i];
-                for (int q = 0; q < ww; ++q) {
-                    rb += E_.wc[q][i];
-                    orb += E_.owc[q][i];
-                }
-                E_.wbase[ww][i] = (int32_t)rb;
-                E_.obase[ww][i] = (int32_t)orb;
-                E_.wpos[ww][i] = (r <= L) ? (int32_t)(S_l[i] + rb) : 0;
-                E_.opos[ww][i] = (r <= L) ? (int32_t)(So_l[i] + orb) : 0;
-            }
-            lds_barrier();
-            int rfull = L < bm ? L : bm;
-            rfull = rfull < rc + rn ? rfull : rc + rn;
-            int32_t *const lslot = a.log_slot + a.head_local;
-            uint32_t *const lseq = a.lseq_out + a.head_local;
-            const uint32_t hin = (uint32_t)a.head_in;
-            for (int i = 0; rc + i < rfull; ++i) {
-                const int r = rc + i;
+        for (int k = 0; k < kRCh; ++k) {
+            const int r = 64 * k + lane;
+            rbv[k] = (int32_t)((r < rlim ? pv[k] : 0) + segc[k]);
+            orbv[k] = (int32_t)((r < rlim ? opv[k] : 0) + osegc[k]);
+            basev[k] = (int32_t)Sv[k] + rbv[k];
+            obasev[k] = (int32_t)Sov[k] + orbv[k];
+        }
+        int32_t *const lslot = a.log_slot + a.head_local;
+        uint32_t *const lseq = a.lseq_out + a.head_local;
+        const uint32_t hin = (uint32_t)a.head_in;
+        // ---- full rounds r < min(L, max own c of the wave): own lanes append their task
+        const int owmx = (int)wave_max_u32((uint32_t)oc);
+        const int rfull = L < owmx ? L : owmx;
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k) {
+            const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
+            for (int i = 0; i < r1; ++i) {
+                const int r = 64 * k + i;
                 const uint64_t m = __ballot(c > r);
                 const uint64_t om = __ballot(oc > r);
+                const int base = __builtin_amdgcn_readlane(basev[k], i);
+                const int obase = __builtin_amdgcn_readlane(obasev[k], i);
                 if (oc > r) {
-                    const int lp = E_.opos[w][i] + popc_lt(om);
+                    const int lp = obase + popc_lt(om);
                     lslot[lp] = s;
-                    lseq[lp] = hin + (uint32_t)(E_.wpos[w][i] + popc_lt(m));
+                    lseq[lp] = hin + (uint32_t)(base + popc_lt(m));
                 }
             }
-            if (L >= rc && L < rc + rn) {
-                const int iL = L - rc;
-                const uint64_t m = __ballot(c > L);
-                const uint64_t om = __ballot(oc > L);
-                rankL = (int64_t)E_.wbase[w][iL] + popc_lt(m);
-                orankL = (int64_t)E_.obase[w][iL] + popc_lt(om);
-                oSL = So_l[iL];
-                if (oc > L && rankL < p) {
-                    const int lp = E_.opos[w][iL] + popc_lt(om);
-                    lslot[lp] = s;
-                    lseq[lp] = hin + (uint32_t)(E_.wpos[w][iL] + popc_lt(m));
-                }
-                if (b == 0 && threadIdx.x == 0 && AL == 0) {
-                    a.hout->new_qlen = 0;
-                    a.hout->n_local = oSL;  // every worker saturated: all own capacity used
-                }
-            }
-            if (L + 1 >= rc && L + 1 < rc + rn) {
-                const int i1 = L + 1 - rc;
-                exL1 = (int64_t)E_.wbase[w][i1] + popc_lt(__ballot(c > L + 1));
-            }
-            lds_barrier();
         }
+        // ---- round L (partial: ranks < p) and round L + 1 (ranks for the next queue)
+        const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
+        const int rbL = __builtin_amdgcn_readlane(Lc == 0 ? rbv[0] : (Lc == 1 ? rbv[1] : rbv[2]), Ll);
+        const int orbL = __builtin_amdgcn_readlane(Lc == 0 ? orbv[0] : (Lc == 1 ? orbv[1] : orbv[2]), Ll);
+        const int rbL1 = __builtin_amdgcn_readlane(L1c == 0 ? rbv[0] : (L1c == 1 ? rbv[1] : rbv[2]), L1l);
+        const uint64_t mL = __ballot(c > L);
+        const uint64_t omL = __ballot(oc > L);
+        const int64_t rankL = (int64_t)rbL + popc_lt(mL);
+        const int64_t orankL = (int64_t)orbL + popc_lt(omL);
+        if (oc > L && rankL < p) {
+            const int64_t lp = oSL + orankL;
+            lslot[lp] = s;
+            lseq[lp] = hin + (uint32_t)(S_L + rankL);
+        }
+        const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
             if (c > L && rankL < p) n_q += 1;
-            if (own) a.free_out[ls].x = raw - (int32_t)n_q;
+            if (own) a.free_out[ls].x = rawq - (int32_t)n_q;
             int64_t np = -1;
             if (c > L) {
                 if (rankL >= p) np = rankL - p;
-                else if (c > L + 1) np = (AL - p) + exL1;
+                else if (c > L1) np = (AL - p) + exL1;
                 if (rankL == p) {
                     // first position of round L left without a task: both queue and own-log lengths
                     a.hout->new_qlen = (AL - p) + exL1;
