@@ -273,7 +273,8 @@ int enqueue_tick(fb_ctx *c) {
     const int64_t head = c->l_head, Qn = c->l_Qn;
     const int64_t Qlog = Qn + 2 * (int64_t)E;
     const int nbw = (int)std::max<int64_t>(1, cdiv(W, kBS));
-    const int nbf = (int)cdiv(head, kFTile);
+    // sharded: the log shard holds head_local entries (head is the global sequence)
+    const int nbf = (int)cdiv(c->shard ? c->l_head_local : head, kFTile);
     const int nbq = (int)std::max<int64_t>(1, cdiv(Qlog, kBS));
     int rc;
     if ((rc = ensure_table(c, R, nbq))) return rc;
