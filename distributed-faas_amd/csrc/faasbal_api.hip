@@ -372,6 +372,8 @@ int enqueue_tick(fb_ctx *c) {
     // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
     // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
+    // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
+    a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
     // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
     // (2 MB of records) those gathers miss L2, so k_slots first writes the
@@ -513,7 +515,7 @@ int enqueue_tick(fb_ctx *c) {
     }
     {
         Timer t(c, "emit");
-        if (a.fused) launch_emit2(a, t.st());
+        if (a.segw) launch_emit2(a, t.st());
         else launch_emit(a, t.st());
     }
     HIPCHK(c, hipGetLastError());

@@ -964,7 +964,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 }
                 wc[wave_id()][g * 64 + lane_id()] = cnt;
                 // per 64-position segment (k_emit2 derives its rank bases from these rows)
-                if (a.fused && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
+                if (a.segw && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
                     a.segcnt[(size_t)(4 * b + wave_id()) * a.R + r0 + lane_id()] = cnt;
             }
             lds_barrier();
@@ -1438,7 +1438,10 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
 constexpr int kTabLd2 = 8;  // int4 table loads per thread (tail loop beyond 8192 entries)
 constexpr int kRCh = 3;     // 64-round chunks: rounds 0 .. L+1 <= 129
 
-template <int MODE>
+// PLAN: large tables (round table beyond the fused limit, R <= 128) -- the same
+// emission with this block's prefixes and the totals from k_plan instead of an
+// in-block reduction of the whole table.
+template <int MODE, bool PLAN>
 __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const TickArgs a = specialise<MODE>(a_);
     __shared__ uint32_t part[kWaves * 32][9];  // per-wave class partials
@@ -1462,6 +1465,36 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int32_t raw0 = a.c_arr[pq];
         const double hb0 = a.c_hb[pq];
         const int s0 = a.E == 0 ? a.queue_in[pq] : lq_slot(a, pq);
+        // counts of c > r in the earlier segments of this block: lane i, round 64 k + i
+        // (all three earlier segments loaded unconditionally, clamped, then masked:
+        // a loop bounded by the wave id would issue one load and wait per segment)
+        uint32_t segc[kRCh] = {0, 0, 0};
+        uint32_t sv[kRCh][kWaves - 1];
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k)
+#pragma unroll
+            for (int q = 0; q < kWaves - 1; ++q) {
+                const int r = min(64 * k + lane, R - 1);
+                sv[k][q] = a.segcnt[(size_t)(4 * b + q) * R + r];
+            }
+        int64_t O, nev, cap;
+        int maxc;
+        if constexpr (PLAN) {
+            // this block's prefix and the total of every round, scanned by k_plan
+            if ((int)threadIdx.x < R) {
+                pre_c[threadIdx.x] = (uint32_t)a.qpre[(size_t)b * R + threadIdx.x];
+                tot_f[threadIdx.x] = (uint32_t)a.A[threadIdx.x];
+            }
+            O = a.P->O;
+            nev = a.P->n_evicted;
+            cap = a.P->cap_total;
+            maxc = a.P->maxc;
+#pragma unroll
+        for (int k = 0; k < kRCh; ++k)
+#pragma unroll
+            for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
+            lds_barrier();
+        } else {
         const uint4 *tab = reinterpret_cast<const uint4 *>(a.qcnt);
         uint4 tv[kTabLd2];
 #pragma unroll
@@ -1479,24 +1512,10 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             mv[k] = (uint32_t)a.qbm_raw[i < nbq1 ? i : nbq1];
             cv[k] = (uint32_t)a.csum[i < nbq1 ? i : nbq1];
         }
-        // counts of c > r in the earlier segments of this block: lane i, round 64 k + i
-        // (all three earlier segments loaded unconditionally, clamped, then masked:
-        // a loop bounded by the wave id would issue one load and wait per segment)
-        uint32_t segc[kRCh] = {0, 0, 0};
-        {
-            uint32_t sv[kRCh][kWaves - 1];
 #pragma unroll
-            for (int k = 0; k < kRCh; ++k)
+        for (int k = 0; k < kRCh; ++k)
 #pragma unroll
-                for (int q = 0; q < kWaves - 1; ++q) {
-                    const int r = min(64 * k + lane, R - 1);
-                    sv[k][q] = a.segcnt[(size_t)(4 * b + q) * R + r];
-                }
-#pragma unroll
-            for (int k = 0; k < kRCh; ++k)
-#pragma unroll
-                for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
-        }
+            for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
         STAMP(a, SO, 9);
         uint32_t fo = 0, wo = 0, mo = 0, co = 0;
 #pragma unroll
@@ -1560,11 +1579,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             pre_c[r] = part[c0][u] + part[32 + c0][u] + part[64 + c0][u] + part[96 + c0][u];
             tot_f[r] = part[c0][4 + u] + part[32 + c0][4 + u] + part[64 + c0][4 + u] + part[96 + c0][4 + u];
         }
-        const int64_t O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        const int64_t nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
-        int64_t cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
-        const int maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
+        O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
+        maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
         lds_barrier();
+        }
         STAMP(a, SO, 1);
         const int rlim = maxc < R ? maxc : R;
         if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
@@ -1684,12 +1704,17 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         // ---- orphan compaction, ascending sequence
         const int b = bid - a.nbq;
         const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
-        unsigned long long tot, pre;
-        peeled_sum(a.fcnt, b, b, tot, pre);
-        const uint32_t ws = wave_sum_u32((uint32_t)pre);
-        if (lane == 0) red[w][0] = ws;
-        lds_barrier();
-        const int64_t off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        int64_t off;
+        if constexpr (PLAN) {
+            off = a.fpre[b];
+        } else {
+            unsigned long long tot, pre;
+            peeled_sum(a.fcnt, b, b, tot, pre);
+            const uint32_t ws = wave_sum_u32((uint32_t)pre);
+            if (lane == 0) red[w][0] = ws;
+            lds_barrier();
+            off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        }
         uint32_t tt;
         const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tt);
         int64_t o = off + ex;
@@ -1704,12 +1729,17 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const int b = bid - a.nbq - a.nbf;
     const int sl = b * kBS + threadIdx.x;
     const uint32_t e = (sl < a.W) & ((a.st[min(sl, a.W > 0 ? a.W - 1 : 0)] & kStEvicted) != 0);
-    unsigned long long tot, pre;
-    peeled_sum(a.wcnt, b, b, tot, pre);
-    const uint32_t ws = wave_sum_u32((uint32_t)pre);
-    if (lane == 0) red[w][0] = ws;
-    lds_barrier();
-    const int64_t off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    int64_t off;
+    if constexpr (PLAN) {
+        off = a.wpre[b];
+    } else {
+        unsigned long long tot, pre;
+        peeled_sum(a.wcnt, b, b, tot, pre);
+        const uint32_t ws = wave_sum_u32((uint32_t)pre);
+        if (lane == 0) red[w][0] = ws;
+        lds_barrier();
+        off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    }
     uint32_t tt;
     const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tt);
     if (e) a.evicted[off + ex] = sl;
@@ -1985,8 +2015,18 @@ void launch_plan(const TickArgs &a, Stream st) {
 void launch_emit(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
 }
+template <bool PLAN>
+static void launch_emit2_t(const TickArgs &a, Stream st) {
+    const dim3 g(a.nbq + a.nbf + a.nbw);
+    switch (tick_mode(a)) {
+    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    }
+}
 void launch_emit2(const TickArgs &a, Stream st) {
-    FB_LAUNCH_MODE(k_emit2, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
+    if (a.fused) launch_emit2_t<false>(a, st);
+    else launch_emit2_t<true>(a, st);
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -151,3 +151,9 @@ def test_deque_random_plan_path(force_plan, seed):
 
 def test_deque_config3_plan_path(force_plan):
     test_deque_config3_with_duplicates()
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_deque_random_chunked_emit(monkeypatch, seed):
+    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "2")
+    test_deque_random_multitick_vs_oracle(seed + 20)

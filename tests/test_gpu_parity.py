@@ -246,6 +246,22 @@ def test_golden_plan_path(force_plan):
         test_golden_replay(path)
 
 
+@pytest.fixture
+def force_chunked_emit(monkeypatch):
+    """The 3-launch path with the chunked k_emit (used when R > 128) instead of
+    k_emit2 after k_plan."""
+    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "2")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_multitick_chunked_emit(force_chunked_emit, seed):
+    test_random_multitick_vs_oracle(seed)
+
+
+def test_config3_chunked_emit(force_chunked_emit):
+    test_config3_full_size()
+
+
 def test_device_primitives_selftest():
     g = GpuBalancer(16, 16)
     assert g.selftest() == 0
