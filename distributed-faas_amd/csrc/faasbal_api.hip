@@ -80,6 +80,7 @@ struct fb_ctx {
     unsigned long long *dbg = nullptr;             // diagnostic stamps
     size_t dbg_n = 0;
     int force_plan = 0;
+    int emit_cfirst = 0;  // FAASBAL_EMIT_CFIRST: k_emit2 grid order (A/B knob)
     int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
     int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
@@ -374,6 +375,7 @@ int enqueue_tick(fb_ctx *c) {
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
     // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
     a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
+    a.cfirst = c->emit_cfirst;
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
     // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
     // (2 MB of records) those gathers miss L2, so k_slots first writes the
@@ -643,6 +645,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && hipHostGetDevicePointer((void **)&c->hout_dev, c->hout, 0) != hipSuccess) rc = FB_EHIP;
     if (!rc) memset(c->hout, 0, sizeof(HostOut));
     if (!rc && getenv("FAASBAL_FORCE_PLAN")) c->force_plan = atoi(getenv("FAASBAL_FORCE_PLAN"));
+    if (!rc && getenv("FAASBAL_EMIT_CFIRST")) c->emit_cfirst = atoi(getenv("FAASBAL_EMIT_CFIRST"));
     if (!rc && getenv("FAASBAL_LOGSCAN")) c->logscan = atoi(getenv("FAASBAL_LOGSCAN"));
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))

@@ -105,6 +105,7 @@ struct TickArgs {
     int W, E, R, nbw, nbf, nbq;
     int fused;       // 1: k_emit derives the cross-block prefixes itself (no k_plan launch)
     int segw;        // 1: k_scan stores per-64-position segment counts (k_emit2, fused or after k_plan)
+    int cfirst;      // 1: k_emit2's compaction blocks come first in the grid
     int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
     int slots_in_scan;
     int deque;        // 1: PushDispatcher.start semantics (see EvArgs)

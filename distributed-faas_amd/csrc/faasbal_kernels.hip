@@ -1453,8 +1453,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const int SO = a.nbw + a.nbf + a.nbq + (a.slots_in_scan ? a.nbw : 0);
     STAMP(a, SO, 0);
     const int lane = lane_id(), w = wave_id();
-    if (bid < a.nbq) {
-        const int b = bid;
+    // grid: queue blocks then compaction blocks, or (a.cfirst) compaction first
+    const int nbf4 = (a.nbf + 3) >> 2, nbw4 = (a.nbw + 3) >> 2;
+    const int qb0 = a.cfirst ? nbf4 + nbw4 : 0;  // first queue block
+    const int cb0 = a.cfirst ? 0 : a.nbq;        // first compaction block
+    if (bid >= qb0 && bid < qb0 + a.nbq) {
+        const int b = bid - qb0;
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
         const int R = a.R;       // 32, 64 or 128
         const int cls = R >> 2;  // int4 columns per table row
@@ -1700,49 +1704,50 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         STAMP(a, SO, 15);
         return;
     }
-    if (bid < a.nbq + a.nbf) {
-        // ---- orphan compaction, ascending sequence
-        const int b = bid - a.nbq;
-        const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
-        int64_t off;
-        if constexpr (PLAN) {
-            off = a.fpre[b];
-        } else {
-            unsigned long long tot, pre;
-            peeled_sum(a.fcnt, b, b, tot, pre);
-            const uint32_t ws = wave_sum_u32((uint32_t)pre);
-            if (lane == 0) red[w][0] = ws;
-            lds_barrier();
-            off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        }
-        uint32_t tt;
-        const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tt);
-        int64_t o = off + ex;
-        const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
-#pragma unroll
-        for (int j = 0; j < kFItems; ++j)
-            if (flags & (1u << j)) a.orphans[o++] = base + j;
-        STAMP(a, SO, 15);
-        return;
-    }
-    // ---- evicted compaction, ascending slot
-    const int b = bid - a.nbq - a.nbf;
-    const int sl = b * kBS + threadIdx.x;
-    const uint32_t e = (sl < a.W) & ((a.st[min(sl, a.W > 0 ? a.W - 1 : 0)] & kStEvicted) != 0);
-    int64_t off;
+    // ---- compaction roles: one wave per tile (a k_scan block's 2048 log entries or
+    // 256 slots), four tiles per workgroup -- a quarter of the blocks of one
+    // thread per flag byte / slot, so they do not queue behind the queue role
+    const bool frole = bid < cb0 + nbf4;
+    const int t0 = 4 * (frole ? bid - cb0 : bid - cb0 - nbf4);
+    const int t = t0 + w;
+    const int ntile = frole ? a.nbf : a.nbw;
+    const uint32_t *cnt = frole ? a.fcnt : a.wcnt;
+    int64_t off;  // entries of the tiles before t
     if constexpr (PLAN) {
-        off = a.wpre[b];
+        const int64_t *pre = frole ? a.fpre : a.wpre;
+        off = pre[t < ntile ? t : ntile - 1];
     } else {
         unsigned long long tot, pre;
-        peeled_sum(a.wcnt, b, b, tot, pre);
+        peeled_sum(cnt, t0, t0, tot, pre);
         const uint32_t ws = wave_sum_u32((uint32_t)pre);
         if (lane == 0) red[w][0] = ws;
         lds_barrier();
         off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        for (int q = 0; q < w; ++q) off += t0 + q < ntile ? cnt[t0 + q] : 0u;
     }
-    uint32_t tt;
-    const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tt);
-    if (e) a.evicted[off + ex] = sl;
+    if (t >= ntile) return;
+    if (frole) {
+        // orphans, ascending sequence: lane l holds flag bytes 4l .. 4l+3 of tile t
+        // (k_scan's thread j flagged entries t*2048 + 8j .. +8)
+        const uint32_t f4 = reinterpret_cast<const uint32_t *>(a.ofl + (size_t)t * kBS)[lane];
+        const uint32_t n = (uint32_t)__popc(f4);
+        int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
+        const int64_t base = (int64_t)t * kFTile + (int64_t)lane * 4 * kFItems;
+        for (uint32_t m = f4; m; m &= m - 1) a.orphans[o++] = base + __builtin_ctz(m);
+    } else {
+        // evicted slots, ascending: lane l holds slots t*256 + 4l .. +4
+        const int s0 = t * kBS + 4 * lane;
+        const int wl = a.W > 0 ? a.W - 1 : 0;
+        uint32_t e = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint8_t sv = a.st[min(s0 + q, wl)];
+            e |= ((s0 + q < a.W) && (sv & kStEvicted)) ? (1u << q) : 0u;
+        }
+        const uint32_t n = (uint32_t)__popc(e);
+        int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
+        for (uint32_t m = e; m; m &= m - 1) a.evicted[o++] = s0 + __builtin_ctz(m);
+    }
     STAMP(a, SO, 15);
 }
 
@@ -2017,7 +2022,7 @@ void launch_emit(const TickArgs &a, Stream st) {
 }
 template <bool PLAN>
 static void launch_emit2_t(const TickArgs &a, Stream st) {
-    const dim3 g(a.nbq + a.nbf + a.nbw);
+    const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
     switch (tick_mode(a)) {
     case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
     case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;

@@ -63,8 +63,9 @@ def main():
     else:
         kernels = {"scan": (S, S + nbf + nbw + nbq), "emit": (E0, E0 + G1)}
         roles = {"scan.F": (S, S + nbf), "scan.W": (S + nbf, S + nbf + nbw), "scan.Q": (S + nbf + nbw, S + G1)}
-    roles.update({"emit.Q": (E0, E0 + nbq), "emit.F": (E0 + nbq, E0 + nbq + nbf),
-                  "emit.W": (E0 + nbq + nbf, E0 + G1)})
+    nbf4, nbw4 = -(-nbf // 4), -(-nbw // 4)  # k_emit2: one wave per compaction tile
+    roles.update({"emit.Q": (E0, E0 + nbq), "emit.F": (E0 + nbq, E0 + nbq + nbf4),
+                  "emit.W": (E0 + nbq + nbf4, E0 + nbq + nbf4 + nbw4)})
     starts = {}
     for kern, (lo, hi) in list(kernels.items()):
         live = (d[:, lo:hi, 13] > 0).all(axis=0)
