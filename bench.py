@@ -259,6 +259,11 @@ def main():
     res = g.wait()
     n_assigned = int(res["n_assigned"])
     O = int(res["n_orphans"])
+    n_evicted = int(res["n_evicted"])  # sharded: this rank's evicted slots; summed below
+    if world > 1:
+        t = torch.tensor([n_evicted], device="cuda", dtype=torch.int64)
+        dist.all_reduce(t)
+        n_evicted = int(t.item())
 
     def barrier():
         if dist is not None:
@@ -356,7 +361,7 @@ def main():
                                 "worker-id range over %d GPUs, exchange all-reduce of %d B per tick (RCCL), "
                                 "%d orphans redistributed" % (T, W, world, kt_x_bytes, O)),
                    "tasks_per_tick": T, "workers": W, "in_flight": F, "queue": Q,
-                   "assigned_per_tick": n_assigned, "evicted": int(res["n_evicted"]),
+                   "assigned_per_tick": n_assigned, "evicted": n_evicted,
                    "fill_level": int(res["fill_level"]),
                    "parallelism": "dp1" if world == 1 else "worker-table shards x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
