@@ -217,6 +217,30 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
     const int per = (n + kBS - 1) / kBS;
     const int i0 = (int)threadIdx.x * per;
     unsigned long long sum = 0;
+    if (per <= 16) {
+        // one load pass: the run stays in registers across the block scan (a second
+        // pass would be another dependent round trip to memory the producer just wrote)
+        uint32_t v[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = min(i0 + j, n - 1);
+            v[j] = cnt[(size_t)i * cs];
+        }
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            v[j] = (j < per && i0 + j < n) ? v[j] : 0u;
+            sum += v[j];
+        }
+        unsigned long long tot;
+        unsigned long long run = block_excl_scan<unsigned long long>(sum, l4, tot);
+#pragma unroll
+        for (int j = 0; j < 16; ++j) {
+            const int i = i0 + j;
+            if (j < per && i < n) pre[(size_t)i * ps] = (TO)run;
+            run += v[j];
+        }
+        return tot;
+    }
     for (int j0 = 0; j0 < per; j0 += 16) {
         // unconditional loads of clamped indices, masked afterwards: a guarded
         // load compiles to a branch with its own wait, one round trip per entry
