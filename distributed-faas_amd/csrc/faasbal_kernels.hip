@@ -759,18 +759,28 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             // gathers per thread; the epoch rides along, so the orphan test needs no
             // further load
             double2 h[kFItems];
-            uint32_t tc[kFItems];
+            uint32_t tc[kFItems], sq[kFItems];
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) {
                 const int sj = v[j] < 0 ? 0 : v[j];
                 h[j] = *reinterpret_cast<const double2 *>(a.hbe + sj);
                 tc[j] = a.E > 0 ? a.touched[sj] : 0u;
             }
+            if (a.shard) {
+                // the entries' global sequence numbers, in flight with the gathers
+                // (loaded per entry inside the test below they cost one more round trip)
+                const int64_t lb = base + kFItems <= nlog ? base : (nlog > kFItems ? nlog - kFItems : 0);
+                const uint4 s0 = *reinterpret_cast<const uint4 *>(a.lseq + (lb & ~(int64_t)3));
+                const uint4 s1 = *reinterpret_cast<const uint4 *>(a.lseq + (lb & ~(int64_t)3) + 4);
+                sq[0] = s0.x; sq[1] = s0.y; sq[2] = s0.z; sq[3] = s0.w;
+                sq[4] = s1.x; sq[5] = s1.y; sq[6] = s1.z; sq[7] = s1.w;
+            }
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) {
                 bool d = false;
                 if (v[j] >= 0) d = (a.E > 0 && tc[j] == a.tick) ? died_touched(a, v[j]) : ((a.now - h[j].x) > a.tte);
-                const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
+                const uint64_t seq = a.shard ? (uint64_t)(base + kFItems <= nlog ? sq[j] : a.lseq[base + j])
+                                             : (uint64_t)(base + j);
                 const uint32_t ep = (uint32_t)__double_as_longlong(h[j].y);
                 died |= (d && seq >= (uint64_t)ep) ? (1u << j) : 0u;
             }
