@@ -1796,7 +1796,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 // log position), one register per 64 rounds, read with readlane in the round
 // loop; block prefixes from k_plan, segment counts from the phase-2 k_scan.
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
-    __shared__ int32_t misc[8];
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
     if (bid < a.nbq) {
@@ -1963,26 +1962,34 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         }
         return;
     }
-    if (bid < a.nbq + a.nbf) {
-        // ---- own orphans (global sequence numbers, ascending)
-        const int b = bid - a.nbq;
-        const uint32_t flags = a.ofl[(size_t)b * kBS + threadIdx.x];
-        uint32_t tot;
-        const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(flags), (uint32_t *)misc, tot);
-        int64_t o = a.fpre[b] + ex;
-        const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
+    // ---- compaction roles as in k_emit2: one wave per tile (a phase-1 k_scan block's
+    // 2048 log entries or 256 slots), four tiles per workgroup
+    const int nbf4 = (a.nbf + 3) >> 2;
+    const bool frole = bid < a.nbq + nbf4;
+    const int t = 4 * (frole ? bid - a.nbq : bid - a.nbq - nbf4) + w;
+    if (t >= (frole ? a.nbf : a.nbw)) return;
+    if (frole) {
+        // own orphans (global sequence numbers, ascending): lane l holds flag bytes
+        // 4l .. 4l+3 of tile t, i.e. local entries t*2048 + 32l .. +32
+        const uint32_t f4 = reinterpret_cast<const uint32_t *>(a.ofl + (size_t)t * kBS)[lane];
+        const uint32_t n = (uint32_t)__popc(f4);
+        int64_t o = a.fpre[t] + (int64_t)(wave_incl_scan_u32(n) - n);
+        const int64_t base = (int64_t)t * kFTile + (int64_t)lane * 4 * kFItems;
+        for (uint32_t m = f4; m; m &= m - 1) a.orphans[o++] = (int64_t)a.lseq[base + __builtin_ctz(m)];
+    } else {
+        // own evicted slots, as global ids, ascending: lane l holds slots t*256 + 4l .. +4
+        const int s0 = t * kBS + 4 * lane;
+        const int wl = a.W > 0 ? a.W - 1 : 0;
+        uint32_t e = 0;
 #pragma unroll
-        for (int j = 0; j < kFItems; ++j)
-            if (flags & (1u << j)) a.orphans[o++] = (int64_t)a.lseq[base + j];
-        return;
+        for (int q = 0; q < 4; ++q) {
+            const uint8_t sv = a.st[min(s0 + q, wl)];
+            e |= ((s0 + q < a.W) && (sv & kStEvicted)) ? (1u << q) : 0u;
+        }
+        const uint32_t n = (uint32_t)__popc(e);
+        int64_t o = a.wpre[t] + (int64_t)(wave_incl_scan_u32(n) - n);
+        for (uint32_t m = e; m; m &= m - 1) a.evicted[o++] = a.slot_base + s0 + __builtin_ctz(m);
     }
-    // ---- own evicted slots, as global ids
-    const int b = bid - a.nbq - a.nbf;
-    const int s = b * kBS + threadIdx.x;
-    const uint32_t e = (s < a.W) & ((a.st[min(s, a.W > 0 ? a.W - 1 : 0)] & kStEvicted) != 0);
-    uint32_t tot;
-    const uint32_t ex = block_excl_scan_u32(e, (uint32_t *)misc, tot);
-    if (e) a.evicted[a.wpre[b] + ex] = a.slot_base + s;
 }
 
 // ------------------------------------------------------------ commit
@@ -2068,7 +2075,8 @@ void launch_emit2(const TickArgs &a, Stream st) {
     else launch_emit2_t<true>(a, st);
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + a.nbf + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4), dim3(kBS), 0, st.s, st.e0,
+                          st.e1, 0, a);
 }
 void launch_commit(const CommitArgs &a, int grid, Stream st) {
     hipExtLaunchKernelGGL(k_commit, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
