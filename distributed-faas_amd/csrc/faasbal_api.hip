@@ -251,7 +251,7 @@ struct XLayout {
 XLayout xlayout(int world, int64_t E, int64_t Qlog) {
     XLayout x;
     x.rec = 0;
-    x.front = (size_t)32 * world;
+    x.front = (size_t)8 * kXRecWords * world;
     x.back = x.front + 4 * (size_t)E;
     x.evs = x.back + 4 * (size_t)E;
     x.c8 = x.evs + (size_t)E;

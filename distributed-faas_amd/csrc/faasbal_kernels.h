@@ -7,6 +7,10 @@ namespace fb {
 
 constexpr int kBS = 256;           // threads per workgroup (4 wave64)
 constexpr int kWaves = kBS / 64;
+// sharded exchange record: a rank's orphan count as partials on kXRecLines separate
+// 128-byte lines (device atomics on one line serialise, ~6 ns each)
+constexpr int kXRecLines = 8;
+constexpr int kXRecWords = kXRecLines * 16;  // u64 words per rank (1 KB)
 constexpr int kFItems = 8;         // log entries per thread in log-role blocks
 constexpr int kFTile = kBS * kFItems;
 constexpr int kRsItems = 8;        // radix sort: keys per thread per tile
@@ -167,7 +171,7 @@ struct TickArgs {
     const uint32_t *lseq;
     uint32_t *lseq_out;
     uint8_t *xc8;                  // exchange: min(c, 255) per LRU position (single contributor per byte)
-    unsigned long long *xrec;      // exchange: per rank {O, sum c, max c, -}
+    unsigned long long *xrec;      // exchange: per rank kXRecLines orphan-count partials, one per 128-B line
     uint32_t *ocnt;                // [block][round] counts of this rank's positions
     uint32_t *osegcnt;             // [64-position segment][round] counts of this rank's positions
     int64_t *opre, *oA;

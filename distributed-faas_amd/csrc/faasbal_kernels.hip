@@ -832,7 +832,8 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         if (threadIdx.x == 0) {
             const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
             a.fcnt[b] = n;
-            if (a.shard && n) atomicAdd(&a.xrec[a.rank * 4 + 0], (unsigned long long)n);
+            if (a.shard && n)
+                atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)n);
         }
         STAMP(a, SO, 15);
         return;
@@ -1128,7 +1129,8 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
         cnt = wave_sum_u32(cnt);
         if (lane == 0) {
             a.fcnt[b] = cnt;
-            if (a.shard && cnt) atomicAdd(&a.xrec[a.rank * 4 + 0], (unsigned long long)cnt);
+            if (a.shard && cnt)
+                atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)cnt);
         }
     }
     STAMP(a, SO, 15);
@@ -1161,6 +1163,11 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
         // c bytes); sharded: every rank's orphan count from the exchange records
         int32_t mx = 0;
         unsigned long long sum = 0;
+        // sharded: the ranks' orphan-count partials (kXRecLines per rank), one load per
+        // thread issued up front -- a serial loop over them costs a round trip each
+        uint32_t op = 0;
+        if (a.shard)
+            for (int g = threadIdx.x; g < a.world * kXRecLines; g += kBS) op += (uint32_t)a.xrec[(size_t)g * 16];
         for (int i0 = 0; i0 < a.nbq; i0 += 8 * kBS) {
             int32_t m[8];
             unsigned long long cs[8];
@@ -1177,17 +1184,16 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
                 sum += ok ? cs[k] : 0ull;
             }
         }
+        __shared__ uint32_t ow[kWaves];
+        op = wave_sum_u32(op);
+        if (lane_id() == 0) ow[wave_id()] = op;
         mx = block_reduce_max<int32_t>(mx, m4);
         unsigned long long tot;
         block_excl_scan<unsigned long long>(sum, l4, tot);
         if (threadIdx.x == 0) {
             a.P->maxc = mx;
             a.P->cap_total = (int64_t)tot;
-            if (a.shard) {
-                unsigned long long O = 0;
-                for (int g = 0; g < a.world; ++g) O += a.xrec[g * 4 + 0];
-                a.P->O = (int64_t)O;
-            }
+            if (a.shard) a.P->O = (int64_t)ow[0] + ow[1] + ow[2] + ow[3];
         }
         return;
     }

@@ -1,8 +1,10 @@
 """Numpy model of the sharded tick protocol (faasbal_api.hip / k_*_shard) -- TEST ONLY.
 
 Reproduces, per rank, what phase 1 writes into the exchange buffer (same byte
-layout as ``xlayout`` in faasbal_api.hip: per-rank records {O, sum c, max c, 0}
-as u64, front / back lists as int32 slot+1, per-event status bytes, and
+layout as ``xlayout`` in faasbal_api.hip: per-rank records of 128 u64 words --
+the GPU spreads the orphan count over words 0, 16, .., 112 (one per 128-byte
+line); this model puts O in word 0 and also keeps sum c / max c in words 1 / 2,
+which the GPU re-derives from the c bytes instead -- front / back lists as int32 slot+1, per-event status bytes, and
 min(c, 255) per LRU position), and what phase 2 derives from the summed
 buffer.  The CPU tests all-reduce these buffers with torch.distributed (gloo,
 world_size 2) and compare the merged result with the sequential oracle.
@@ -11,11 +13,12 @@ import numpy as np
 
 KEEP, OUT, FRONT, BACK = 0, 1, 2, 3
 R_MAX = 128  # sharded ticks support fill levels below 128 rounds (c8 exchange)
+XREC_WORDS = 128  # u64 words of one rank's exchange record (kXRecWords)
 
 
 def xlayout(world, E, Qlog):
     rec = 0
-    front = 32 * world
+    front = 8 * XREC_WORDS * world
     back = front + 4 * E
     evs = back + 4 * E
     c8 = evs + E
@@ -118,8 +121,8 @@ def phase1(rs, world, rank, now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, T
         if E <= pos < E + len(rs["queue"]) and touched[gs - base] and qstat[gs - base] != KEEP:
             continue
         c[pos] = max(cur_free[gs - base], 1)
-    rec = np.zeros(4 * world, np.uint64)
-    rec[4 * rank:4 * rank + 3] = [len(orphans), c.sum(), c.max(initial=0)]
+    rec = np.zeros(XREC_WORDS * world, np.uint64)
+    rec[XREC_WORDS * rank:XREC_WORDS * rank + 3] = [len(orphans), c.sum(), c.max(initial=0)]
     x[lay["rec"]:lay["front"]] = rec.view(np.uint8)
     x[lay["front"]:lay["back"]] = front.view(np.uint8)
     x[lay["back"]:lay["evs"]] = back.view(np.uint8)
@@ -133,7 +136,7 @@ def phase1(rs, world, rank, now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, T
 def phase2(rs, ctx, x):
     """Returns (outputs of this rank, next rank state)."""
     lay, E, world, base, n, head = ctx["lay"], ctx["E"], ctx["world"], rs["base"], rs["n"], rs["head"]
-    rec = x[lay["rec"]:lay["front"]].view(np.uint64).reshape(world, 4).astype(np.int64)
+    rec = x[lay["rec"]:lay["front"]].view(np.uint64).reshape(world, XREC_WORDS).astype(np.int64)
     O, cap, maxc = int(rec[:, 0].sum()), int(rec[:, 1].sum()), int(rec[:, 2].max())
     front = x[lay["front"]:lay["back"]].view(np.int32).astype(np.int64) - 1
     back = x[lay["back"]:lay["evs"]].view(np.int32).astype(np.int64) - 1
