@@ -130,8 +130,9 @@ def bench_stream(args):
     64K results of in-flight tasks, 1K re-registrations, 10K heartbeats; the
     clock advances 10 ms per tick so silent workers expire (churn) and their
     in-flight tasks are redistributed.  Ticks are committed (state evolves);
-    the timed region holds K whole ticks: host staging of the events, the
-    launch, the wait for the results and the commit."""
+    the timed region holds K whole ticks: host staging of the events (tick
+    i+1's overlapping tick i on the device), the launch, the wait for the
+    results and the commit."""
     from faasbal import GpuBalancer, synth
     W = args.workers if args.workers != 65536 else 1 << 20
     T = 65536
@@ -144,20 +145,30 @@ def bench_stream(args):
     carried = [0]
     stats = dict(assigned=0, orphans=0, evicted=0, events=0)
 
-    def run(tk):
+    def stage(tk):
+        g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
+
+    def run(i):
+        # launch tick i on its staged messages, stage tick i+1's on the host while
+        # the device runs tick i (double-buffered pinned staging), then wait + commit
+        tk = ticks[i]
         n = carried[0] + tk["n_new"]
-        g.launch(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        g.launch_staged(10.0, n)
+        if i + 1 < len(ticks):
+            stage(ticks[i + 1])
         r = g.wait()
         g.commit()
         carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
         return r
 
-    for tk in ticks[:Wu]:
-        run(tk)
+    stage(ticks[0])
+    for i in range(Wu):
+        run(i)
     g.sync()
     t0 = time.perf_counter()
-    for tk in ticks[Wu:Wu + K]:
-        r = run(tk)
+    for i in range(Wu, Wu + K):
+        tk = ticks[i]
+        r = run(i)
         stats["assigned"] += int(r["n_assigned"])
         stats["orphans"] += int(r["n_orphans"])
         stats["evicted"] += int(r["n_evicted"])
@@ -165,8 +176,8 @@ def bench_stream(args):
     g.sync()
     dt = time.perf_counter() - t0
     g.timing_enable(True)
-    for tk in ticks[Wu + K:]:
-        run(tk)
+    for i in range(Wu + K, len(ticks)):
+        run(i)
     kt = g.timing_read()
     g.timing_enable(False)
     kern = {k: ms / max(n, 1) * 1e3 for k, (ms, n) in kt.items()}  # us per launch

@@ -61,7 +61,13 @@ struct fb_ctx {
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
     uint32_t *rs_hist = nullptr;
     int32_t *front_list = nullptr, *back_list = nullptr;
-    void *h_stage = nullptr;
+    void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};  // copies out of half h enqueued (fb_tick_launch_staged)
+    bool stage_rec[2] = {false, false};
+    int stage_half = 1;        // half of the last launch's copies
+    bool staged = false;       // fb_tick_stage done, fb_tick_launch_staged not yet
+    int32_t st_E = 0, st_vmax = 0;
+    double st_now = 0.0;
     // scan / plan / emit
     int32_t *c_arr = nullptr, *qbmax = nullptr, *qbm_raw = nullptr;
     unsigned long long *csum = nullptr;
@@ -652,7 +658,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         rc = FB_EHIP;
     if (!rc && getenv("FAASBAL_SPLIT_SLOTS")) c->split_slots = atoi(getenv("FAASBAL_SPLIT_SLOTS"));
     if (!rc && getenv("FAASBAL_DBG_STOP")) c->dbg_stop = atoi(getenv("FAASBAL_DBG_STOP"));
-    if (!rc && hipHostMalloc(&c->h_stage, E * 32, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
+    if (!rc && hipHostMalloc(&c->h_stage, (size_t)E * 32 * 2, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
+    if (!rc && (hipEventCreateWithFlags(&c->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->stage_ev[1], hipEventDisableTiming) != hipSuccess))
+        rc = FB_EHIP;
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
     if (rc) {
@@ -694,6 +703,8 @@ int fb_destroy(fb_ctx *c) {
     if (c->arena) hipFree(c->arena);
     if (c->hout) hipHostFree(c->hout);
     if (c->h_stage) hipHostFree(c->h_stage);
+    for (int h = 0; h < 2; ++h)
+        if (c->stage_ev[h]) hipEventDestroy(c->stage_ev[h]);
     for (auto &t : c->tl) {
         hipEventDestroy(t.a);
         hipEventDestroy(t.b);
@@ -923,29 +934,33 @@ int fb_tick_continue(fb_ctx *c) {
     return enqueue_tick(c);
 }
 
-int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
-                   const int32_t *val, const double *ts, const int64_t *seq, int64_t n_pending) {
+// Validate a tick's events and stage them into the pinned half the next launch
+// copies from.  Two halves: staging tick t+1 on the host overlaps tick t on the
+// device (the half's previous copies were enqueued two launches ago; its event
+// is waited for, not the stream).
+int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+                  const int32_t *val, const double *ts, const int64_t *seq) {
     if (!c) return FB_EINVAL;
     if (n_events < 0 || n_events > c->E_cap) return fail(c, FB_EINVAL, "n_events %d outside [0, %d]", n_events, c->E_cap);
-    if (n_pending < 0) return fail(c, FB_EINVAL, "n_pending < 0");
     if (n_events && (!kind || !slot || !val || !ts))
         return fail(c, FB_EINVAL, "event arrays must be non-NULL");
     const int E = n_events;
+    const int half = c->stage_half ^ 1;
     // One pass over the caller's arrays: validate (branch-free; the per-event loop
     // below runs only to name the first offending event) while staging them into
-    // pinned memory, then one async copy per array.
+    // pinned memory; fb_tick_launch_staged issues one async copy per array.
     const uint32_t Wv = (uint32_t)(c->shard ? c->W_global : c->W);
     int32_t vmax = 0;
-    HIPCHK(c, hipSetDevice(c->device));
     if (E) {
-        char *h = (char *)c->h_stage;
         const size_t ecap = (size_t)c->E_cap;
+        char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
         uint8_t *hk = (uint8_t *)h;
         int32_t *hs = (int32_t *)(h + ecap);
         int32_t *hv = (int32_t *)(h + ecap * 5);
         double *ht = (double *)(h + ecap * 9);
         int64_t *hq = (int64_t *)(h + ecap * 17);
-        HIPCHK(c, hipStreamSynchronize(c->stream));  // staging buffer reuse
+        HIPCHK(c, hipSetDevice(c->device));
+        if (c->stage_rec[half]) HIPCHK(c, hipEventSynchronize(c->stage_ev[half]));  // staging buffer reuse
         uint32_t bad = 0;
         double prev = ts[0];
         for (int i = 0; i < E; ++i) {
@@ -963,17 +978,41 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
             hq[i] = seq ? seq[i] : -1;
         }
         for (int i = 0; bad && i < E; ++i) {
+            c->staged = false;
             if ((uint32_t)slot[i] >= Wv) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %u)", i, slot[i], Wv);
             if (kind[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, kind[i]);
             if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
                 return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
         }
-        HIPCHK(c, hipMemcpyAsync(c->ev_kind, hk, E, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_slot, hs, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_val, hv, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_ts, ht, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_seq, hq, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
     }
+    c->staged = true;
+    c->st_E = E;
+    c->st_vmax = vmax;
+    c->st_now = now;
+    return FB_OK;
+}
+
+int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
+    if (!c) return FB_EINVAL;
+    if (!c->staged) return fail(c, FB_ESTATE, "fb_tick_launch_staged without fb_tick_stage");
+    if (n_pending < 0) return fail(c, FB_EINVAL, "n_pending < 0");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int E = c->st_E;
+    const int half = c->stage_half ^ 1;
+    if (E) {
+        const size_t ecap = (size_t)c->E_cap;
+        char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
+        HIPCHK(c, hipMemcpyAsync(c->ev_kind, h, E, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_slot, h + ecap, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_val, h + ecap * 5, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_ts, h + ecap * 9, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipMemcpyAsync(c->ev_seq, h + ecap * 17, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(c, hipEventRecord(c->stage_ev[half], c->stream));
+        c->stage_rec[half] = true;
+    }
+    c->stage_half = half;
+    c->staged = false;
+    const double now = c->st_now;
     c->l_now = now;
     c->l_tte = c->deque ? __builtin_inf() : tte;  // start() has no liveness: nobody ever expires
     c->l_E = E;
@@ -983,11 +1022,20 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
     c->l_Qn = c->Qn;
     c->phase = 1;
     c->tick += 1;  // per-launch stamp: a relaunch with other messages never sees this launch's marks
-    c->l_R = choose_R(std::max(c->maxc_hint, vmax));
+    c->l_R = choose_R(std::max(c->maxc_hint, c->st_vmax));
     c->reruns = 0;
     c->launched = true;
     c->waited = false;
     return enqueue_tick(c);
+}
+
+int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+                   const int32_t *val, const double *ts, const int64_t *seq, int64_t n_pending) {
+    if (!c) return FB_EINVAL;
+    if (n_pending < 0) return fail(c, FB_EINVAL, "n_pending < 0");
+    int rc = fb_tick_stage(c, now, n_events, kind, slot, val, ts, seq);
+    if (rc) return rc;
+    return fb_tick_launch_staged(c, tte, n_pending);
 }
 
 int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {

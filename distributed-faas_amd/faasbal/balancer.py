@@ -135,6 +135,24 @@ class GpuBalancer:
         self._chk(self.lib.fb_tick_launch(self.h, float(now), float(tte), E, _p(k), _p(s), _p(v), _p(t),
                                           _p(q), int(n_pending)))
 
+    def stage(self, now, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None):
+        """Validate and stage the next tick's events (host only; overlaps a running tick)."""
+        k = _arr(ev_kind, np.uint8)
+        s = _arr(ev_slot, np.int32)
+        v = _arr(ev_val, np.int32)
+        t = _arr(ev_ts, np.float64)
+        q = None if ev_seq is None else _arr(ev_seq, np.int64)
+        E = len(k)
+        if not (len(s) == E and len(v) == E and len(t) == E and (q is None or len(q) == E)):
+            raise ValueError("event arrays differ in length")
+        self._chk(self.lib.fb_tick_stage(self.h, float(now), E, _p(k), _p(s), _p(v), _p(t), _p(q)))
+        self._staged_E = E
+
+    def launch_staged(self, tte, n_pending=0):
+        """Enqueue the tick on the events of the last stage() (its `now`)."""
+        self._chk(self.lib.fb_tick_launch_staged(self.h, float(tte), int(n_pending)))
+        self._E = self._staged_E
+
     def wait(self):
         r = TickResult()
         self._chk(self.lib.fb_tick_wait(self.h, C.byref(r)))

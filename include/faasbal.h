@@ -107,6 +107,15 @@ int fb_tick_launch(fb_ctx *ctx, double now, double tte, int32_t n_events, const 
                    const int32_t *slot, const int32_t *val, const double *ts, const int64_t *seq,
                    int64_t n_pending);
 
+/* The same launch in two steps, so that a host can stage tick t+1's events
+ * while the device runs tick t (double-buffered pinned staging):
+ * fb_tick_stage validates and copies the events (same rules and errors as
+ * fb_tick_launch; no device work), fb_tick_launch_staged enqueues the tick on
+ * the staged events with the stage's `now`.  fb_tick_launch = stage + launch. */
+int fb_tick_stage(fb_ctx *ctx, double now, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+                  const int32_t *val, const double *ts, const int64_t *seq);
+int fb_tick_launch_staged(fb_ctx *ctx, double tte, int64_t n_pending);
+
 /* Wait for the last launched tick; fills *res.  Transparently reruns the tick
  * with a wider round table when free counts exceeded the launch's estimate. */
 int fb_tick_wait(fb_ctx *ctx, fb_tick_result *res);

@@ -347,3 +347,42 @@ def test_stream_ticks_vs_oracle():
         _cmp_out(a, b, t)
         _cmp_state(g, o, t)
         carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def test_stream_ticks_staged_pipeline_vs_oracle():
+    """fb_tick_stage of tick t+1 while tick t runs (double-buffered pinned staging),
+    then fb_tick_launch_staged: the same outputs and states as the oracle."""
+    st = synth.zipf_state(W=8192, seed=0, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=6, seed=3, tasks_per_tick=4096, results_per_tick=4096, dt=1.5)
+    g, o = _pair(st, len(st["log"]) + 6 * 8192 + 16, max_events=8192)
+
+    def stage(tk):
+        g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
+
+    carried = 0
+    stage(ticks[0])
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        g.launch_staged(10.0, n)
+        if t + 1 < len(ticks):
+            stage(ticks[t + 1])  # host work overlapping the device tick
+        g.wait()
+        a = dict(reconnect=g.event_status(), assign=g.assignments(), orphans=g.orphans(), evicted=g.evicted())
+        g.commit()
+        b = o.tick(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        _cmp_out(a, b, t)
+        _cmp_state(g, o, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def test_launch_staged_needs_stage():
+    st = synth.zipf_state(W=512, seed=1)
+    g = GpuBalancer(512, len(st["log"]) * 2 + 4096)
+    g.load(st)
+    with pytest.raises(FaasbalError):
+        g.launch_staged(10.0, 10)
+    g.stage(1000.0)
+    g.launch_staged(10.0, 100)
+    g.wait()
+    with pytest.raises(FaasbalError):  # a stage is consumed by its launch
+        g.launch_staged(10.0, 100)
