@@ -62,8 +62,16 @@ struct fb_ctx {
     uint32_t *rs_hist = nullptr;
     int32_t *front_list = nullptr, *back_list = nullptr;
     void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
-    hipEvent_t stage_ev[2] = {nullptr, nullptr};  // copies out of half h enqueued (fb_tick_launch_staged)
-    bool stage_rec[2] = {false, false};
+    // device event arrays, double-buffered like the pinned halves: fb_tick_stage copies
+    // half h on its own stream (overlapping a running tick), the launch waits for it
+    uint8_t *evk[2] = {nullptr, nullptr};
+    int32_t *evsl[2] = {nullptr, nullptr}, *evv[2] = {nullptr, nullptr};
+    double *evt[2] = {nullptr, nullptr};
+    int64_t *evq[2] = {nullptr, nullptr};
+    hipStream_t cp_s = nullptr;                         // H2D copies of staged events
+    hipEvent_t stage_ev[2] = {nullptr, nullptr};        // copies of half h done (on cp_s)
+    hipEvent_t use_ev[2] = {nullptr, nullptr};          // the tick reading device half h done
+    bool stage_rec[2] = {false, false}, use_rec[2] = {false, false};
     int stage_half = 1;        // half of the last launch's copies
     bool staged = false;       // fb_tick_stage done, fb_tick_launch_staged not yet
     int32_t st_E = 0, st_vmax = 0;
@@ -587,12 +595,14 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->post_free, W);
     ap.add(&c->post_hb, W);
     ap.add(&c->post_epoch, W);
-    ap.add(&c->ev_kind, E);
     ap.add(&c->ev_status, E);
-    ap.add(&c->ev_val, E);
-    ap.add(&c->ev_slot, E);
-    ap.add(&c->ev_ts, E);
-    ap.add(&c->ev_seq, E);
+    for (int i = 0; i < 2; ++i) {
+        ap.add(&c->evk[i], E);
+        ap.add(&c->evv[i], E);
+        ap.add(&c->evsl[i], E);
+        ap.add(&c->evt[i], E);
+        ap.add(&c->evq[i], E);
+    }
     for (int i = 0; i < 2; ++i) {
         ap.add(&c->keys[i], E);
         ap.add(&c->vals[i], E);
@@ -659,9 +669,18 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_SPLIT_SLOTS")) c->split_slots = atoi(getenv("FAASBAL_SPLIT_SLOTS"));
     if (!rc && getenv("FAASBAL_DBG_STOP")) c->dbg_stop = atoi(getenv("FAASBAL_DBG_STOP"));
     if (!rc && hipHostMalloc(&c->h_stage, (size_t)E * 32 * 2, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
-    if (!rc && (hipEventCreateWithFlags(&c->stage_ev[0], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->stage_ev[1], hipEventDisableTiming) != hipSuccess))
-        rc = FB_EHIP;
+    for (int h = 0; h < 2 && !rc; ++h)
+        if (hipEventCreateWithFlags(&c->stage_ev[h], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&c->use_ev[h], hipEventDisableTiming) != hipSuccess)
+            rc = FB_EHIP;
+    if (!rc && hipStreamCreateWithFlags(&c->cp_s, hipStreamNonBlocking) != hipSuccess) rc = FB_EHIP;
+    if (!rc) {
+        c->ev_kind = c->evk[0];
+        c->ev_slot = c->evsl[0];
+        c->ev_val = c->evv[0];
+        c->ev_ts = c->evt[0];
+        c->ev_seq = c->evq[0];
+    }
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
     if (rc) {
@@ -703,8 +722,12 @@ int fb_destroy(fb_ctx *c) {
     if (c->arena) hipFree(c->arena);
     if (c->hout) hipHostFree(c->hout);
     if (c->h_stage) hipHostFree(c->h_stage);
-    for (int h = 0; h < 2; ++h)
+    if (c->cp_s) hipStreamSynchronize(c->cp_s);
+    for (int h = 0; h < 2; ++h) {
         if (c->stage_ev[h]) hipEventDestroy(c->stage_ev[h]);
+        if (c->use_ev[h]) hipEventDestroy(c->use_ev[h]);
+    }
+    if (c->cp_s) hipStreamDestroy(c->cp_s);
     for (auto &t : c->tl) {
         hipEventDestroy(t.a);
         hipEventDestroy(t.b);
@@ -979,11 +1002,25 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
         }
         for (int i = 0; bad && i < E; ++i) {
             c->staged = false;
+            c->stage_rec[half] = false;  // nothing was copied out of this half
             if ((uint32_t)slot[i] >= Wv) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %u)", i, slot[i], Wv);
             if (kind[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, kind[i]);
             if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
                 return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
         }
+    }
+    if (E) {
+        // H2D on the copy stream, after the last tick that read this device half
+        const size_t ecap = (size_t)c->E_cap;
+        char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
+        if (c->use_rec[half]) HIPCHK(c, hipStreamWaitEvent(c->cp_s, c->use_ev[half], 0));
+        HIPCHK(c, hipMemcpyAsync(c->evk[half], h, E, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evsl[half], h + ecap, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evv[half], h + ecap * 5, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evt[half], h + ecap * 9, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evq[half], h + ecap * 17, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipEventRecord(c->stage_ev[half], c->cp_s));
+        c->stage_rec[half] = true;
     }
     c->staged = true;
     c->st_E = E;
@@ -999,17 +1036,12 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     HIPCHK(c, hipSetDevice(c->device));
     const int E = c->st_E;
     const int half = c->stage_half ^ 1;
-    if (E) {
-        const size_t ecap = (size_t)c->E_cap;
-        char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
-        HIPCHK(c, hipMemcpyAsync(c->ev_kind, h, E, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_slot, h + ecap, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_val, h + ecap * 5, (size_t)E * 4, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_ts, h + ecap * 9, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipMemcpyAsync(c->ev_seq, h + ecap * 17, (size_t)E * 8, hipMemcpyHostToDevice, c->stream));
-        HIPCHK(c, hipEventRecord(c->stage_ev[half], c->stream));
-        c->stage_rec[half] = true;
-    }
+    if (E) HIPCHK(c, hipStreamWaitEvent(c->stream, c->stage_ev[half], 0));  // the staged copies
+    c->ev_kind = c->evk[half];
+    c->ev_slot = c->evsl[half];
+    c->ev_val = c->evv[half];
+    c->ev_ts = c->evt[half];
+    c->ev_seq = c->evq[half];
     c->stage_half = half;
     c->staged = false;
     const double now = c->st_now;
@@ -1026,7 +1058,15 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->reruns = 0;
     c->launched = true;
     c->waited = false;
-    return enqueue_tick(c);
+    const int rc = enqueue_tick(c);
+    if (rc) return rc;
+    if (E) {
+        // the next copy into this device half waits for the tick's reads (a rerun in
+        // fb_tick_wait reads it again, but no stage can target this half before then)
+        HIPCHK(c, hipEventRecord(c->use_ev[half], c->stream));
+        c->use_rec[half] = true;
+    }
+    return FB_OK;
 }
 
 int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
