@@ -7,10 +7,14 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
+#include <functional>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "faasbal.h"
@@ -19,6 +23,61 @@
 using namespace fb;
 
 namespace {
+
+// Persistent host workers for the staging pass of large event batches: part i of
+// n runs on worker i - 1 (part 0 on the caller).  One pool per context; the ABI
+// allows one caller thread per context, so run() is never re-entered.
+struct HostPool {
+    std::vector<std::thread> th;
+    std::mutex m;
+    std::condition_variable cv, done_cv;
+    std::function<void(int)> job;
+    long gen = 0;
+    int pending = 0;
+    bool stop = false;
+
+    explicit HostPool(int n) {
+        for (int i = 1; i < n; ++i) th.emplace_back([this, i] { loop(i); });
+    }
+    ~HostPool() {
+        {
+            std::lock_guard<std::mutex> g(m);
+            stop = true;
+        }
+        cv.notify_all();
+        for (auto &t : th) t.join();
+    }
+    int size() const { return (int)th.size() + 1; }
+    void loop(int i) {
+        long seen = 0;
+        for (;;) {
+            std::function<void(int)> f;
+            {
+                std::unique_lock<std::mutex> l(m);
+                cv.wait(l, [&] { return stop || gen != seen; });
+                if (stop) return;
+                seen = gen;
+                f = job;
+            }
+            f(i);
+            std::lock_guard<std::mutex> g(m);
+            if (--pending == 0) done_cv.notify_one();
+        }
+    }
+    void run(const std::function<void(int)> &f) {
+        {
+            std::lock_guard<std::mutex> g(m);
+            job = f;
+            pending = (int)th.size();
+            ++gen;
+        }
+        cv.notify_all();
+        f(0);
+        std::unique_lock<std::mutex> l(m);
+        done_cv.wait(l, [&] { return pending == 0; });
+    }
+};
+
 
 struct TimedLaunch {
     const char *name;
@@ -76,6 +135,7 @@ struct fb_ctx {
     bool staged = false;       // fb_tick_stage done, fb_tick_launch_staged not yet
     int32_t st_E = 0, st_vmax = 0;
     double st_now = 0.0;
+    HostPool *pool = nullptr;  // staging workers (FAASBAL_STAGE_THREADS, default 4; 1 = none)
     // scan / plan / emit
     int32_t *c_arr = nullptr, *qbmax = nullptr, *qbm_raw = nullptr;
     unsigned long long *csum = nullptr;
@@ -675,6 +735,11 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
             rc = FB_EHIP;
     if (!rc && hipStreamCreateWithFlags(&c->cp_s, hipStreamNonBlocking) != hipSuccess) rc = FB_EHIP;
     if (!rc) {
+        int nt = getenv("FAASBAL_STAGE_THREADS") ? atoi(getenv("FAASBAL_STAGE_THREADS")) : 4;
+        nt = std::max(1, std::min(nt, 16));
+        if (nt > 1 && E >= kStagePar) c->pool = new HostPool(nt);
+    }
+    if (!rc) {
         c->ev_kind = c->evk[0];
         c->ev_slot = c->evsl[0];
         c->ev_val = c->evv[0];
@@ -722,6 +787,7 @@ int fb_destroy(fb_ctx *c) {
     if (c->arena) hipFree(c->arena);
     if (c->hout) hipHostFree(c->hout);
     if (c->h_stage) hipHostFree(c->h_stage);
+    delete c->pool;
     if (c->cp_s) hipStreamSynchronize(c->cp_s);
     for (int h = 0; h < 2; ++h) {
         if (c->stage_ev[h]) hipEventDestroy(c->stage_ev[h]);
@@ -984,21 +1050,39 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
         int64_t *hq = (int64_t *)(h + ecap * 17);
         HIPCHK(c, hipSetDevice(c->device));
         if (c->stage_rec[half]) HIPCHK(c, hipEventSynchronize(c->stage_ev[half]));  // staging buffer reuse
+        // parts of the batch on the pool's workers when it is large (the pass reads and
+        // writes ~25 B per event, mostly cold caller memory: memory-latency bound)
+        const int np = (c->pool && E >= kStagePar) ? c->pool->size() : 1;
+        uint32_t pbad[16] = {0};
+        int32_t pvmax[16] = {0};
+        auto part = [&](int pi) {
+            const int lo = (int)((int64_t)E * pi / np), hi = (int)((int64_t)E * (pi + 1) / np);
+            uint32_t bad = 0;
+            int32_t vm = 0;
+            double prev = ts[lo > 0 ? lo - 1 : 0];
+            for (int i = lo; i < hi; ++i) {
+                const uint8_t k = kind[i];
+                const int32_t sl = slot[i], v = val[i];
+                const double t = ts[i];
+                bad |= (uint32_t)((uint32_t)sl >= Wv) | (uint32_t)(k > FB_EV_OTHER) | (uint32_t)!(t <= now) |
+                       (uint32_t)(t < prev);
+                prev = t;
+                vm = std::max(vm, k <= FB_EV_RECONNECT ? v : 0);
+                hk[i] = k;
+                hs[i] = sl;
+                hv[i] = v;
+                ht[i] = t;
+                hq[i] = seq ? seq[i] : -1;
+            }
+            pbad[pi] = bad;
+            pvmax[pi] = vm;
+        };
+        if (np > 1) c->pool->run(part);
+        else part(0);
         uint32_t bad = 0;
-        double prev = ts[0];
-        for (int i = 0; i < E; ++i) {
-            const uint8_t k = kind[i];
-            const int32_t sl = slot[i], v = val[i];
-            const double t = ts[i];
-            bad |= (uint32_t)((uint32_t)sl >= Wv) | (uint32_t)(k > FB_EV_OTHER) | (uint32_t)!(t <= now) |
-                   (uint32_t)(t < prev);
-            prev = t;
-            vmax = std::max(vmax, k <= FB_EV_RECONNECT ? v : 0);
-            hk[i] = k;
-            hs[i] = sl;
-            hv[i] = v;
-            ht[i] = t;
-            hq[i] = seq ? seq[i] : -1;
+        for (int pi = 0; pi < np; ++pi) {
+            bad |= pbad[pi];
+            vmax = std::max(vmax, pvmax[pi]);
         }
         for (int i = 0; bad && i < E; ++i) {
             c->staged = false;

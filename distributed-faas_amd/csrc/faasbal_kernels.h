@@ -7,6 +7,7 @@ namespace fb {
 
 constexpr int kBS = 256;           // threads per workgroup (4 wave64)
 constexpr int kWaves = kBS / 64;
+constexpr int kStagePar = 16384;   // host: event batches this large are staged by the worker pool
 // sharded exchange record: a rank's orphan count as partials on kXRecLines separate
 // 128-byte lines (device atomics on one line serialise, ~6 ns each)
 constexpr int kXRecLines = 8;
