@@ -103,6 +103,7 @@ struct fb_ctx {
     uint8_t *reg = nullptr;
     HbRec *hbe = nullptr;  // {last_heartbeat (NaN: no record), epoch} per slot
     int32_t *log_slot = nullptr;
+    int32_t *trash = nullptr;  // kTrashRows x kBS words written by inactive lanes (never read)
     int64_t Qn = 0, head = 0;
     uint32_t tick = 1;
     // per-tick sparse post-message records
@@ -501,6 +502,7 @@ int enqueue_tick(fb_ctx *c) {
     a.qpre = c->qpre;
     a.A = c->A;
     a.P = c->P;
+    a.trash = c->trash;
     a.log_slot = c->log_slot;
     a.free_out = c->free_[nxt];
     a.queue_out = c->queue[nxt];
@@ -651,6 +653,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->post_reg, W);
     ap.add(&c->post_flags, W);
     ap.add(&c->st, W);
+    ap.add(&c->trash, (size_t)kTrashRows * kBS);
     ap.add(&c->dmask, (W + 63) / 64);
     ap.add(&c->post_free, W);
     ap.add(&c->post_hb, W);

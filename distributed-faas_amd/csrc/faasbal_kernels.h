@@ -7,6 +7,7 @@ namespace fb {
 
 constexpr int kBS = 256;           // threads per workgroup (4 wave64)
 constexpr int kWaves = kBS / 64;
+constexpr int kTrashRows = 1024;   // k_emit2: trash rows (one per block, modulo) for branch-free stores
 constexpr int kStagePar = 16384;   // host: event batches this large are staged by the worker pool
 // sharded exchange record: a rank's orphan count as partials on kXRecLines separate
 // 128-byte lines (device atomics on one line serialise, ~6 ns each)
@@ -14,7 +15,10 @@ constexpr int kXRecLines = 8;
 constexpr int kXRecWords = kXRecLines * 16;  // u64 words per rank (1 KB)
 constexpr int kFItems = 8;         // log entries per thread in log-role blocks
 constexpr int kFTile = kBS * kFItems;
-constexpr int kRsItems = 8;        // radix sort: keys per thread per tile
+#ifndef FAASBAL_RS_ITEMS
+#define FAASBAL_RS_ITEMS 8
+#endif
+constexpr int kRsItems = FAASBAL_RS_ITEMS;  // radix sort: keys per thread per tile
 constexpr int kRsTile = kBS * kRsItems;
 constexpr int kRFused = 128;       // fused tick: round table of at most 128 rows ...
 constexpr int kTabLd = 16;         // ... read by at most 16 int4 loads per thread
@@ -155,6 +159,7 @@ struct TickArgs {
     DevTotals *P;
     // outputs
     int32_t *log_slot;
+    int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
     int2 *free_out;     // next {free_processes (INT32_MIN: no live record), queued}
     int32_t *queue_out;
     int32_t *qfree_out;
