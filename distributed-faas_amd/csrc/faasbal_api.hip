@@ -156,6 +156,7 @@ struct fb_ctx {
     size_t dbg_n = 0;
     int force_plan = 0;
     int emit_cfirst = 0;  // FAASBAL_EMIT_CFIRST: k_emit2 grid order (A/B knob)
+    int rs_wide = 1;       // FAASBAL_RS_WIDE=0: 8-bit sort digits only (A/B knob)
     int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
     int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
@@ -372,16 +373,20 @@ int enqueue_tick(fb_ctx *c) {
         // stable radix sort of events by slot
         int bits = 1;
         while ((1ll << bits) < (int64_t)(c->shard ? c->W_global : W)) ++bits;
-        const int passes = (bits + 7) / 8;
         const int nb = (int)cdiv(E, kRsTile);
+        // digits of up to 11 bits while the batch is small enough for the scatter's
+        // table walk (1 M workers: two passes of 10 bits instead of three of 8)
+        const bool wide = c->rs_wide && nb <= kRsWideMaxBlocks;
+        const int passes = wide ? (bits + 10) / 11 : (bits + 7) / 8;
+        const int db = wide ? (bits + passes - 1) / passes : 8;
         const uint32_t *kin = (const uint32_t *)c->ev_slot, *vin = nullptr;
         for (int ps = 0; ps < passes; ++ps) {
             Timer t(c, "rs_sort");
             uint32_t *kout = c->keys[ps & 1], *vout = c->vals[ps & 1];
             // pass 0 also clears the one-GPU front / back lists (sharded: zeroed with the exchange buffer)
             const bool z = ps == 0 && !c->shard;
-            launch_rs_hist(kin, E, 8 * ps, c->rs_hist, nb, z ? front : nullptr, z ? back : nullptr, t.first());
-            launch_rs_scatter(kin, vin, kout, vout, E, 8 * ps, c->rs_hist, nb, ps == 0 ? 1 : 0, t.last());
+            launch_rs_pass(kin, vin, kout, vout, E, db * ps, db, c->rs_hist, nb, z ? front : nullptr,
+                           z ? back : nullptr, ps == 0 ? 1 : 0, t.first(), t.last());
             kin = kout;
             vin = vout;
         }
@@ -670,7 +675,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->keys[i], E);
         ap.add(&c->vals[i], E);
     }
-    ap.add(&c->rs_hist, 256 * (size_t)cdiv(E, kRsTile));
+    // 8-bit passes: 256 x blocks; wide passes (a tick of <= kRsWideMaxBlocks blocks): 2048 x blocks
+    ap.add(&c->rs_hist, std::max((size_t)256 * cdiv(E, kRsTile), (size_t)2048 * (size_t)std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks)));
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
     ap.add(&c->c_arr, Qlog);
@@ -726,6 +732,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_FORCE_PLAN")) c->force_plan = atoi(getenv("FAASBAL_FORCE_PLAN"));
     if (!rc && getenv("FAASBAL_EMIT_CFIRST")) c->emit_cfirst = atoi(getenv("FAASBAL_EMIT_CFIRST"));
     if (!rc && getenv("FAASBAL_LOGSCAN")) c->logscan = atoi(getenv("FAASBAL_LOGSCAN"));
+    if (!rc && getenv("FAASBAL_RS_WIDE")) c->rs_wide = atoi(getenv("FAASBAL_RS_WIDE"));
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;

@@ -205,10 +205,12 @@ struct Stream {
     Stream(hipStream_t s_) : s(s_) {}
     Stream(hipStream_t s_, hipEvent_t a, hipEvent_t b) : s(s_), e0(a), e1(b) {}
 };
-void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1,
-                    Stream st);
-void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,
-                       int shift, const uint32_t *hist, int nblk, int identity_vals, Stream st);
+// One LSD pass (histogram + scatter launches) over `db`-bit digits at `shift`;
+// hist holds (1 << db rounded up to 256 / 1024 / 2048) x nblk counts.
+void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
+                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
+                    Stream s);
+constexpr int kRsWideMaxBlocks = 256;  // wider digits only while the scatter prologue's table walk stays short
 void launch_ev_apply(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 void launch_slots(const TickArgs &a, Stream st);

@@ -1,7 +1,7 @@
 // faasbal_kernels.hip -- CDNA4 (gfx950) kernels of one balancer tick.
 //
 // Tick pipeline, every kernel 256 threads = 4 wave64:
-//   [E>0]  k_rs_hist / k_rs_scatter   stable LSD radix sort of events by slot (8-bit digits)
+//   [E>0]  k_rs_hist / k_rs_scatter   stable LSD radix sort of events by slot (8-11-bit digits)
 //   [E>0]  k_ev_apply     per-slot sequential message semantics (task_dispatcher.py:347-387)
 //          k_slots        heartbeat purge of every slot (is_alive :209-212, purge_workers :241-249)
 //          k_scan         log role: orphan flags per block; queue role: effective free count c
@@ -275,13 +275,20 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 }
 
 // ---------------------------------------------------------------- radix sort
-// Stable LSD radix sort of (key = slot, val = event index), 8-bit digits.
+// Stable LSD radix sort of (key = slot, val = event index), `db`-bit digits
+// (db <= log2 NB).  NB = 256 for 8-bit passes; 1024 / 2048 let a 20-bit slot
+// space (1 M workers) sort in two passes instead of three, each pass being two
+// dependent launches.  hist is [block][digit] (the scatter prologue's column
+// walk is then one contiguous row segment per wave load).
 // (pass 0 also clears the tick's front / back lists, which k_ev_apply fills)
-__global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift,
+template <int NB>
+__global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift, int db,
                                                  uint32_t *__restrict__ hist, int nblk, int32_t *__restrict__ zero0,
                                                  int32_t *__restrict__ zero1) {
-    __shared__ uint32_t cnt[256];
-    cnt[threadIdx.x] = 0;
+    constexpr int DPT = NB / kBS;
+    __shared__ uint32_t cnt[NB];
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) cnt[k * kBS + threadIdx.x] = 0;
     __syncthreads();
     const int base = blockIdx.x * kRsTile;
     if (zero0) {
@@ -294,70 +301,118 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ ke
             }
         }
     }
+    const uint32_t mask = (1u << db) - 1u;
     uint32_t kk[kRsItems];  // every key load in flight before the first use
 #pragma unroll
     for (int j = 0; j < kRsItems; ++j) kk[j] = keys[min(base + j * kBS + (int)threadIdx.x, n - 1)];
 #pragma unroll
     for (int j = 0; j < kRsItems; ++j)
-        if (base + j * kBS + (int)threadIdx.x < n) atomicAdd(&cnt[(kk[j] >> shift) & 255u], 1u);
+        if (base + j * kBS + (int)threadIdx.x < n) atomicAdd(&cnt[(kk[j] >> shift) & mask], 1u);
     __syncthreads();
-    hist[(size_t)threadIdx.x * nblk + blockIdx.x] = cnt[threadIdx.x];
+#pragma unroll
+    for (int k = 0; k < DPT; ++k) {
+        const int d = k * kBS + threadIdx.x;
+        hist[(size_t)blockIdx.x * NB + d] = cnt[d];
+    }
 }
 
+template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                     uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int n,
-                                                    int shift, const uint32_t *__restrict__ hist, int nblk,
+                                                    int shift, int db, const uint32_t *__restrict__ hist, int nblk,
                                                     int identity_vals) {
-    __shared__ uint32_t base[256];
-    __shared__ uint32_t wcnt[kWaves][256];
+    constexpr int DPT = NB / kBS;       // digits per thread
+    constexpr int CH = 32 / DPT;        // blocks per batch of 32 loads in flight
+    __shared__ uint32_t base[NB];
+    __shared__ uint32_t wcnt[kWaves][NB];
     __shared__ uint32_t l4[kWaves];
+    const int t = threadIdx.x;
     {
-        // this block's base per digit straight from the raw [digit][block] counts
-        // (no separate scan launch): thread d sums digit d over all blocks and over
-        // the blocks before this one, then one block scan over the digit totals
-        const int d = threadIdx.x;
-        uint32_t tot = 0, pre = 0;
-        for (int j0 = 0; j0 < nblk; j0 += 32) {
-            uint32_t v[32];
+        // this block's base per digit straight from the raw [block][digit] counts
+        // (no separate scan launch): thread t sums digits k*256+t over all blocks
+        // and over the blocks before this one (each wave load is one contiguous
+        // row segment), then one block scan over the digit totals in digit order
+        uint32_t tot[DPT], pre[DPT];
 #pragma unroll
-            for (int j = 0; j < 32; ++j) v[j] = hist[(size_t)d * nblk + min(j0 + j, nblk - 1)];
+        for (int k = 0; k < DPT; ++k) tot[k] = pre[k] = 0;
+        for (int j0 = 0; j0 < nblk; j0 += CH) {
+            uint32_t v[DPT][CH];
 #pragma unroll
-            for (int j = 0; j < 32; ++j) {
-                const uint32_t x = (j0 + j < nblk) ? v[j] : 0u;
-                tot += x;
-                pre += (j0 + j < (int)blockIdx.x) ? x : 0u;
-            }
+            for (int k = 0; k < DPT; ++k)
+#pragma unroll
+                for (int j = 0; j < CH; ++j) v[k][j] = hist[(size_t)min(j0 + j, nblk - 1) * NB + k * kBS + t];
+#pragma unroll
+            for (int k = 0; k < DPT; ++k)
+#pragma unroll
+                for (int j = 0; j < CH; ++j) {
+                    const uint32_t x = (j0 + j < nblk) ? v[k][j] : 0u;
+                    tot[k] += x;
+                    pre[k] += (j0 + j < (int)blockIdx.x) ? x : 0u;
+                }
         }
-        uint32_t all;
-        base[d] = block_excl_scan_u32(tot, l4, all) + pre;
+        if constexpr (DPT == 1) {
+            uint32_t all;
+            base[t] = block_excl_scan_u32(tot[0], l4, all) + pre[0];
+        } else {
+            // regroup through LDS so thread t scans the contiguous digits t*DPT ..
+#pragma unroll
+            for (int k = 0; k < DPT; ++k) {
+                base[k * kBS + t] = tot[k];
+                wcnt[0][k * kBS + t] = pre[k];
+            }
+            __syncthreads();
+            uint32_t loc[DPT], sum = 0, all;
+#pragma unroll
+            for (int k = 0; k < DPT; ++k) sum += (loc[k] = base[t * DPT + k]);
+            uint32_t ex = block_excl_scan_u32(sum, l4, all);  // its barriers order the reads above
+#pragma unroll
+            for (int k = 0; k < DPT; ++k) {
+                base[t * DPT + k] = ex + wcnt[0][t * DPT + k];
+                ex += loc[k];
+            }
+            __syncthreads();
+        }
+    }
+    if constexpr (NB > 256) {  // the leader-lane updates below keep wcnt zero between items
+#pragma unroll
+        for (int q = 0; q < kWaves; ++q)
+#pragma unroll
+            for (int k = 0; k < DPT; ++k) wcnt[q][k * kBS + t] = 0;
     }
     const int tile = blockIdx.x * kRsTile;
     const int w = wave_id();
+    const uint32_t mask = (1u << db) - 1u;
     // the tile's keys and values loaded up front (clamped, all in flight at once)
     uint32_t kk[kRsItems], vv[kRsItems];
 #pragma unroll
     for (int j = 0; j < kRsItems; ++j) {
-        const int e = tile + j * kBS + (int)threadIdx.x, ec = min(e, n - 1);
+        const int e = tile + j * kBS + t, ec = min(e, n - 1);
         kk[j] = kin[ec];
         vv[j] = identity_vals ? (uint32_t)e : vin[ec];
     }
+    __syncthreads();
 #pragma unroll
     for (int j = 0; j < kRsItems; ++j) {
+        if constexpr (NB == 256) {
 #pragma unroll
-        for (int q = 0; q < kWaves; ++q) wcnt[q][threadIdx.x] = 0;
-        __syncthreads();
-        const int e = tile + j * kBS + threadIdx.x;
+            for (int q = 0; q < kWaves; ++q) wcnt[q][t] = 0;
+            __syncthreads();
+        }
+        const int e = tile + j * kBS + t;
         const bool valid = e < n;
         const uint32_t key = kk[j], val = vv[j];
-        uint32_t d = (key >> shift) & 255u;
+        const uint32_t d = (key >> shift) & mask;
         uint64_t peers = __ballot(valid);
+        constexpr int LB = NB == 256 ? 8 : NB == 1024 ? 10 : 11;  // digit bits above db are 0 in every lane
 #pragma unroll
-        for (int b = 0; b < 8; ++b) {
-            uint64_t m = __ballot((d >> b) & 1u);
+        for (int b = 0; b < LB; ++b) {
+            const uint64_t m = __ballot((d >> b) & 1u);
             peers &= ((d >> b) & 1u) ? m : ~m;
         }
-        int wrank = popc_lt(peers);
-        if (valid && wrank == 0) wcnt[w][d] = (uint32_t)__popcll(peers);
+        const int wrank = popc_lt(peers);
+        const bool lead = valid && wrank == 0;
+        const uint32_t wn = (uint32_t)__popcll(peers);
+        if (lead) wcnt[w][d] = wn;
         __syncthreads();
         if (valid) {
             uint32_t off = base[d] + (uint32_t)wrank;
@@ -366,10 +421,19 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
             vout[off] = val;
         }
         __syncthreads();
-        uint32_t add = 0;
+        if constexpr (NB == 256) {
+            uint32_t add = 0;
 #pragma unroll
-        for (int q = 0; q < kWaves; ++q) add += wcnt[q][threadIdx.x];
-        base[threadIdx.x] += add;
+            for (int q = 0; q < kWaves; ++q) add += wcnt[q][t];
+            base[t] += add;
+        } else {
+            // only the digits this item touched move: each wave's leader lanes advance
+            // their digit's base and clear their own count (no NB-wide sweep)
+            if (lead) {
+                atomicAdd(&base[d], wn);
+                wcnt[w][d] = 0;
+            }
+        }
         __syncthreads();
     }
 }
@@ -2036,15 +2100,24 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
 // ------------------------------------------------------------ launchers
 namespace fb {
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
-void launch_rs_hist(const uint32_t *keys, int n, int shift, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1,
-                    Stream st) {
-    hipExtLaunchKernelGGL(k_rs_hist, dim3(nblk), dim3(kBS), 0, st.s, st.e0, st.e1, 0, keys, n, shift, hist, nblk,
+template <int NB>
+static void rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
+                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
+                    Stream s) {
+    hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, kin, n, shift, db, hist, nblk,
                           zero0, zero1);
+    hipExtLaunchKernelGGL(k_rs_scatter<NB>, dim3(nblk), dim3(kBS), 0, s.s, s.e0, s.e1, 0, kin, vin, kout, vout, n,
+                          shift, db, hist, nblk, identity_vals);
 }
-void launch_rs_scatter(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n,
-                       int shift, const uint32_t *hist, int nblk, int identity_vals, Stream st) {
-    hipExtLaunchKernelGGL(k_rs_scatter, dim3(nblk), dim3(kBS), 0, st.s, st.e0, st.e1, 0, kin, vin, kout, vout, n, shift, hist, nblk,
-                       identity_vals);
+void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
+                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
+                    Stream s) {
+    if (db <= 8)
+        rs_pass<256>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, identity_vals, h, s);
+    else if (db <= 10)
+        rs_pass<1024>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, identity_vals, h, s);
+    else
+        rs_pass<2048>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, identity_vals, h, s);
 }
 void launch_ev_apply(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -386,3 +386,39 @@ def test_launch_staged_needs_stage():
     g.wait()
     with pytest.raises(FaasbalError):  # a stage is consumed by its launch
         g.launch_staged(10.0, 100)
+
+
+def _sort_tick(W, E, hot_frac, seed):
+    """One tick of E messages (kinds mixed, clocks ascending) on a W-slot table,
+    hot_frac of them on five hot slots; GPU vs oracle.  The oracle purges after
+    every message (O(W) each), so E * W stays around 1e9."""
+    rng = np.random.default_rng(seed)
+    st = synth.zipf_state(W=W, seed=seed % 7, dead_frac=0.02)
+    hot = rng.choice(W, size=5, replace=False)
+    slot = np.where(rng.random(E) < hot_frac, hot[rng.integers(0, 5, E)], rng.integers(0, W, E)).astype(np.int32)
+    kind = rng.choice([synth.EV_REGISTER, synth.EV_HEARTBEAT, synth.EV_RESULT, synth.EV_RECONNECT], size=E,
+                      p=[0.1, 0.4, 0.4, 0.1]).astype(np.int32)
+    val = rng.integers(0, 4, E).astype(np.int32)
+    now = 1000.0  # zipf_state's clock
+    ts = np.sort(now - rng.random(E)).astype(np.float64)
+    g, o = _pair(st, 2 * len(st["log"]) + 100_000, max_events=E)
+    args = (now, 10.0, kind, slot, val, ts, np.full(E, -1, np.int64), 20_000)
+    a, b = g.tick(*args), o.tick(*args)
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+
+
+@pytest.mark.parametrize("W,E,wide", [((1 << 17) + 5, 12000, "1"), (1 << 20, 2000, "1"), (1 << 21, 1000, "1"),
+                                      ((1 << 17) + 5, 12000, "0"), (1 << 20, 2000, "0")])
+def test_event_sort_wide_digits(monkeypatch, W, E, wide):
+    """Slot spaces of 17-22 bits: the event sort runs two passes of 9-11-bit
+    digits (FAASBAL_RS_WIDE=0: three of 8 bits); identical to the oracle."""
+    monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
+    _sort_tick(W, E, 0.0, W + E)
+
+
+@pytest.mark.parametrize("W,E", [(300, 30000), (5000, 30000), ((1 << 19) + 3, 2000)])
+def test_event_sort_stable_on_repeated_slots(W, E):
+    """90 % of the messages on five slots (equal-key runs across sort tiles): the
+    per-slot arrival order the sort must keep decides every register / result."""
+    _sort_tick(W, E, 0.9, W)
