@@ -513,14 +513,23 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
 __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     const int j = blockIdx.x * kBS + threadIdx.x;
     if (j >= a.E) return;
-    const uint32_t gs = a.skeys[j];
-    if (j > 0 && a.skeys[j - 1] == gs) return;
+    // this position's key, its neighbours and its event index in one load round
+    const uint32_t gs = a.skeys[j], gprev = a.skeys[max(j - 1, 0)], gnext = a.skeys[min(j + 1, a.E - 1)];
+    const int i0 = (int)a.svals[j];
+    if (j > 0 && gprev == gs) return;
     if (a.deque) {
         ev_apply_deque(a, j, gs);
         return;
     }
     if (a.shard && ((int)gs < a.slot_base || (int)gs >= a.slot_base + a.W)) return;  // another rank's worker
     const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
+    // the first message's payload, loaded alongside the slot record (most slots
+    // get one message: the chain is key -> {record, payload} -> log entry)
+    int kind = a.ev_kind[i0];
+    int32_t val = a.ev_val[i0];
+    double ts = a.ev_ts[i0];
+    int64_t seq = a.ev_seq[i0];
+    int i = i0;
     int reg = a.reg[s];
     const int2 fq = a.free_in[s];
     int32_t fr = fq.x;
@@ -530,11 +539,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     int qstat = inq ? kQsKeep : kQsOut;
     int qidx = -1;
     int cur_is_start = reg, died_start = 0;
-    for (int k = j; k < a.E && a.skeys[k] == gs; ++k) {
-        const int i = (int)a.svals[k];
-        const int kind = a.ev_kind[i];
-        const int32_t val = a.ev_val[i];
-        const double ts = a.ev_ts[i];
+    for (int k = j;;) {
         // purge at ts before the message is polled (:390 of the previous iteration)
         if (reg && (ts - hb) > a.tte) {
             reg = 0;
@@ -560,7 +565,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
         } else if (kind == kEvResult) {                  // :374-387
             fr += 1;
             hb = ts;
-            const int64_t q = a.ev_seq[i];
+            const int64_t q = seq;
             if (q >= 0 && q < a.head_in) {
                 const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
                 if (li >= 0 && a.log_slot[li] == (int32_t)gs) a.log_slot[li] = -1;
@@ -568,6 +573,12 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
             if (fr == 1 && !inq) { inq = 1; qstat = kQsBack; qidx = i; }
         }
         a.ev_status[i] = status;
+        if (++k >= a.E || (k == j + 1 ? gnext : a.skeys[k]) != gs) break;
+        i = (int)a.svals[k];
+        kind = a.ev_kind[i];
+        val = a.ev_val[i];
+        ts = a.ev_ts[i];
+        seq = a.ev_seq[i];
     }
     a.post_reg[s] = (uint8_t)reg;
     a.post_free[s] = fr;

@@ -64,6 +64,14 @@ def load(path=None):
     if not os.path.exists(path):
         raise ImportError("libfaasbal.so not found at %s: run `python -c 'import __graft_entry__ as g; "
                           "g.build()'` (hipcc --offload-arch=gfx950)" % path)
+    # torch bundles its own HIP runtime under the same soname as /opt/rocm's.
+    # Whichever loads first serves the whole process; when this library came
+    # first, a later `import torch` (faasbal.sharded's exchange buffers) found no
+    # GPU on the box.  So torch, when installed, is imported before the library.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(path)
     i32, i64, dbl = C.c_int32, C.c_int64, C.c_double
     proto = {
