@@ -322,7 +322,7 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
                                                     int shift, int db, const uint32_t *__restrict__ hist, int nblk,
                                                     int identity_vals) {
     constexpr int DPT = NB / kBS;       // digits per thread
-    constexpr int CH = 32 / DPT;        // blocks per batch of 32 loads in flight
+    constexpr int CH = 64 / DPT;        // blocks per batch of 64 loads in flight
     __shared__ uint32_t base[NB];
     __shared__ uint32_t wcnt[kWaves][NB];
     __shared__ uint32_t l4[kWaves];
@@ -429,12 +429,14 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
         } else {
             // only the digits this item touched move: each wave's leader lanes advance
             // their digit's base and clear their own count (no NB-wide sweep)
+            // (no barrier after: a wave clears only its own wcnt row, and the next
+            // item reads base / wcnt only after its first barrier)
             if (lead) {
                 atomicAdd(&base[d], wn);
                 wcnt[w][d] = 0;
             }
         }
-        __syncthreads();
+        if constexpr (NB == 256) __syncthreads();
     }
 }
 
