@@ -160,3 +160,23 @@ def test_sharded_random_multitick_logscan(logscan, seed):
 
 def test_sharded_churn_logscan(logscan):
     test_sharded_churn()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_wide_sort_digits(world):
+    """A 18-bit global slot space: every rank sorts the whole message batch by
+    global slot with two passes of 9-bit digits, then applies its own range."""
+    W, E = (1 << 17) + 5, 6000
+    rng = np.random.default_rng(world)
+    st = synth.zipf_state(W=W, seed=world, dead_frac=0.02)
+    bals, o = _group(st, world, 2 * len(st["log"]) + 100_000, max_events=E)
+    slot = rng.integers(0, W, E).astype(np.int32)
+    kind = rng.choice([synth.EV_REGISTER, synth.EV_HEARTBEAT, synth.EV_RESULT, synth.EV_RECONNECT], size=E,
+                      p=[0.1, 0.4, 0.4, 0.1]).astype(np.int32)
+    val = rng.integers(0, 4, E).astype(np.int32)
+    now = 1000.0
+    ts = np.sort(now - rng.random(E)).astype(np.float64)
+    args = (now, 10.0, kind, slot, val, ts, np.full(E, -1, np.int64), 20_000)
+    a, _ = _group_tick(bals, *args)
+    b = o.tick(*args)
+    _cmp(bals, o, a, b, 0)
