@@ -101,7 +101,8 @@ struct fb_ctx {
     double *c_hb = nullptr;                  // per tick: heartbeat of a live LRU position
     bool qaos = false;                       // qfree/qhb[cur] describe the committed queue
     uint8_t *reg = nullptr;
-    HbRec *hbe = nullptr;  // {last_heartbeat (NaN: no record), epoch} per slot
+    double *hb = nullptr;        // last_heartbeat per slot (NaN: no record)
+    uint32_t *epoch = nullptr;   // first log sequence of the slot's current registration
     int32_t *log_slot = nullptr;
     int32_t *trash = nullptr;  // kTrashRows x kBS words written by inactive lanes (never read)
     int64_t Qn = 0, head = 0;
@@ -415,7 +416,8 @@ int enqueue_tick(fb_ctx *c) {
         a.ev_status = evs;
         a.reg = c->reg;
         a.free_in = c->free_[cur];
-        a.hbe = c->hbe;
+        a.hb = c->hb;
+        a.epoch = c->epoch;
         a.log_slot = c->log_slot;
         a.post_reg = c->post_reg;
         a.post_free = c->post_free;
@@ -478,7 +480,7 @@ int enqueue_tick(fb_ctx *c) {
     a.T = c->l_T;
     a.log_cap = c->log_cap;
     a.reg = c->reg;
-    a.hbe = c->hbe;
+    a.hb = c->hb;
     a.free_in = c->free_[cur];
     a.queue_in = c->queue[cur];
     a.qaos = (!c->shard && c->qaos) ? 1 : 0;
@@ -653,7 +655,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         }
     }
     ap.add(&c->reg, W);
-    ap.add(&c->hbe, W);
+    ap.add(&c->hb, W);
+    ap.add(&c->epoch, W);
     ap.add(&c->touched, W);
     ap.add(&c->post_reg, W);
     ap.add(&c->post_flags, W);
@@ -840,12 +843,12 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         if (log_slot[i] < -1 || log_slot[i] >= n_workers)
             return fail(c, FB_EINVAL, "log_slot[%lld] = %d out of range", (long long)i, log_slot[i]);
     std::vector<uint8_t> reg(W ? W : 1, 0);
-    std::vector<HbRec> hbv(W ? W : 1);
+    std::vector<double> hbv(W ? W : 1);
+    std::vector<uint32_t> epv(W ? W : 1);
     for (size_t s = 0; s < W; ++s) {
         reg[s] = registered[s] ? 1 : 0;
-        hbv[s].hb = reg[s] ? last_heartbeat[s] : __builtin_nan("");  // no record: NaN (never "dead")
-        hbv[s].epoch = epoch ? epoch[s] : 0u;
-        hbv[s].pad = 0;
+        hbv[s] = reg[s] ? last_heartbeat[s] : __builtin_nan("");  // no record: NaN (never "dead")
+        epv[s] = epoch ? epoch[s] : 0u;
     }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -855,7 +858,8 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         std::vector<int2> fq(W);
         for (size_t s = 0; s < W; ++s) fq[s] = make_int2(free_processes[s], inq[s]);
         HIPCHK(c, hipMemcpy(c->free_[0], fq.data(), W * sizeof(int2), hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->hb, hbv.data(), W * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->epoch, epv.data(), W * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     if (queue_len) {
         HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
@@ -877,7 +881,16 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         }
         if (queue_len) HIPCHK(c, hipMemcpy(c->qrank[0], qrank.data(), (size_t)queue_len * 4, hipMemcpyHostToDevice));
     }
-    if (log_len) HIPCHK(c, hipMemcpy(c->log_slot, log_slot, (size_t)log_len * 4, hipMemcpyHostToDevice));
+    if (log_len) {
+        // heartbeat contexts keep only live entries of current registrations in the log:
+        // an entry of a slot without a record, or older than its registration's epoch,
+        // can never be redistributed (build-defined)
+        std::vector<int32_t> lg(log_slot, log_slot + log_len);
+        if (!c->deque)
+            for (int64_t i = 0; i < log_len; ++i)
+                if (lg[i] >= 0 && (!reg[lg[i]] || (uint64_t)i < (uint64_t)epv[lg[i]])) lg[i] = -1;
+        HIPCHK(c, hipMemcpy(c->log_slot, lg.data(), (size_t)log_len * 4, hipMemcpyHostToDevice));
+    }
     c->W = n_workers;
     c->Qn = queue_len;
     c->head = log_len;
@@ -900,14 +913,8 @@ int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, doubl
             HIPCHK(c, hipMemcpy(fq.data(), c->free_[c->cur], W * sizeof(int2), hipMemcpyDeviceToHost));
             for (size_t s = 0; s < W; ++s) free_processes[s] = fq[s].x;
         }
-        if (last_heartbeat || epoch) {
-            std::vector<HbRec> hbv(W);
-            HIPCHK(c, hipMemcpy(hbv.data(), c->hbe, W * sizeof(HbRec), hipMemcpyDeviceToHost));
-            for (size_t s = 0; s < W; ++s) {
-                if (last_heartbeat) last_heartbeat[s] = hbv[s].hb;
-                if (epoch) epoch[s] = hbv[s].epoch;
-            }
-        }
+        if (last_heartbeat) HIPCHK(c, hipMemcpy(last_heartbeat, c->hb, W * sizeof(double), hipMemcpyDeviceToHost));
+        if (epoch) HIPCHK(c, hipMemcpy(epoch, c->epoch, W * sizeof(uint32_t), hipMemcpyDeviceToHost));
     }
     if (queue && c->Qn) HIPCHK(c, hipMemcpy(queue, c->queue[c->cur], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
     if (queue_len) *queue_len = c->Qn;
@@ -952,12 +959,12 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
             return fail(c, FB_EINVAL, "log_seq must ascend below log_head (entry %lld)", (long long)i);
     }
     std::vector<uint8_t> reg(W ? W : 1, 0);
-    std::vector<HbRec> hbv(W ? W : 1);
+    std::vector<double> hbv(W ? W : 1);
+    std::vector<uint32_t> epv(W ? W : 1);
     for (size_t s = 0; s < W; ++s) {
         reg[s] = registered[s] ? 1 : 0;
-        hbv[s].hb = reg[s] ? last_heartbeat[s] : __builtin_nan("");  // no record: NaN (never "dead")
-        hbv[s].epoch = epoch ? epoch[s] : 0u;
-        hbv[s].pad = 0;
+        hbv[s] = reg[s] ? last_heartbeat[s] : __builtin_nan("");  // no record: NaN (never "dead")
+        epv[s] = epoch ? epoch[s] : 0u;
     }
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -967,11 +974,17 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
         std::vector<int2> fq(W);
         for (size_t s = 0; s < W; ++s) fq[s] = make_int2(free_processes[s], inq[s]);
         HIPCHK(c, hipMemcpy(c->free_[0], fq.data(), W * sizeof(int2), hipMemcpyHostToDevice));
-        HIPCHK(c, hipMemcpy(c->hbe, hbv.data(), W * sizeof(HbRec), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->hb, hbv.data(), W * sizeof(double), hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->epoch, epv.data(), W * sizeof(uint32_t), hipMemcpyHostToDevice));
     }
     if (queue_len) HIPCHK(c, hipMemcpy(c->queue[0], queue, (size_t)queue_len * 4, hipMemcpyHostToDevice));
     if (log_len) {
-        HIPCHK(c, hipMemcpy(c->log_slot, log_slot, (size_t)log_len * 4, hipMemcpyHostToDevice));
+        // live entries of current registrations only (see fb_load_state)
+        std::vector<int32_t> lg(log_slot, log_slot + log_len);
+        for (int64_t i = 0; i < log_len; ++i)
+            if (lg[i] >= 0 && (!reg[lg[i] - slot_base] || (uint64_t)log_seq[i] < (uint64_t)epv[lg[i] - slot_base]))
+                lg[i] = -1;
+        HIPCHK(c, hipMemcpy(c->log_slot, lg.data(), (size_t)log_len * 4, hipMemcpyHostToDevice));
         HIPCHK(c, hipMemcpy(c->lseq, log_seq, (size_t)log_len * 4, hipMemcpyHostToDevice));
     }
     c->slot_base = slot_base;
@@ -1217,18 +1230,27 @@ int fb_tick_commit(fb_ctx *c) {
     if (!c) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "fb_tick_commit without a waited tick");
     HIPCHK(c, hipSetDevice(c->device));
-    if (c->W > 0) {
+    const int64_t n_orph = c->last.n_orphans_local;
+    if (c->W > 0 || n_orph > 0) {
         CommitArgs a{};
         a.W = c->W;
+        a.nbw = (int)cdiv(c->W, kBS);
         a.tick = c->tick;
         a.st = c->st;
         a.touched = c->touched;
         a.post_hb = c->post_hb;
         a.post_epoch = c->post_epoch;
         a.reg = c->reg;
-        a.hbe = c->hbe;
+        a.hb = c->hb;
+        a.epoch = c->epoch;
+        a.n_orph = n_orph;
+        a.orphans = c->orphans;
+        a.log_slot = c->log_slot;
+        a.lseq = c->lseq;
+        a.head_local = c->l_head_local;
+        a.shard = c->shard;
         Timer t(c, "commit");
-        launch_commit(a, (int)cdiv(c->W, kBS), t.st());
+        launch_commit(a, a.nbw + (int)cdiv(n_orph, kBS), t.st());
         HIPCHK(c, hipGetLastError());
     }
     c->cur = 1 - c->cur;
@@ -1313,8 +1335,8 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     if (!c || !v) return FB_EINVAL;
     v->free_processes = &c->free_[c->cur]->x;
     v->free_processes_stride = (int32_t)sizeof(int2);
-    v->last_heartbeat = &c->hbe->hb;
-    v->last_heartbeat_stride = (int32_t)sizeof(HbRec);
+    v->last_heartbeat = c->hb;
+    v->last_heartbeat_stride = (int32_t)sizeof(double);
     v->registered = c->reg;
     v->queue = c->queue[c->cur];
     v->log_slot = c->log_slot;

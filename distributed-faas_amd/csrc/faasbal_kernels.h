@@ -43,14 +43,12 @@ constexpr uint8_t kStEvicted = 4;    // record deleted during the tick and not r
 constexpr int kPfDiedStart = 1;
 constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 
-// Committed per-slot heartbeat record: last_heartbeat (NaN when the slot holds no
-// record) and the first log sequence of the current registration, in one 16-byte
-// line so the log scan gets both with a single gather.
-struct alignas(16) HbRec {
-    double hb;
-    uint32_t epoch;
-    uint32_t pad;
-};
+// Committed per-slot heartbeat: last_heartbeat, NaN when the slot holds no record
+// (so the log scan's one 8-byte gather per in-flight entry decides liveness
+// without a registered flag); the first log sequence of the current registration
+// lives in its own array (epoch) that no scan reads.  Log entries of a dead
+// registration are cleared (-1) when the tick that redistributed them commits,
+// so every live entry belongs to its slot's current registration.
 
 // results of a tick, written by k_emit into host-mapped pinned memory
 struct HostOut {
@@ -98,7 +96,8 @@ struct EvArgs {
     uint8_t *ev_status;
     const uint8_t *reg;
     const int2 *free_in;  // {free_processes, queued} per slot
-    const HbRec *hbe;
+    const double *hb;
+    const uint32_t *epoch;
     int32_t *log_slot;
     uint8_t *post_reg;
     int32_t *post_free;
@@ -132,7 +131,7 @@ struct TickArgs {
     int64_t Qn, Qlog, head_in, T, log_cap;
     // committed state
     const uint8_t *reg;
-    const HbRec *hbe;
+    const double *hb;
     const int2 *free_in;  // {free_processes, queued} per slot: one 8-byte record per worker
     const int32_t *queue_in;
     // free_processes / last_heartbeat of the committed queue, by LRU position
@@ -186,13 +185,21 @@ struct TickArgs {
 struct CommitArgs {
     int W;
     int slot_base;
+    int nbw;            // slot blocks; blocks [nbw, nbw + ceil(n_orph / 256)) clear orphaned log entries
     uint32_t tick;
     const uint8_t *st;
     const uint32_t *touched;
     const double *post_hb;
     const uint32_t *post_epoch;
     uint8_t *reg;
-    HbRec *hbe;
+    double *hb;
+    uint32_t *epoch;
+    int64_t n_orph;            // orphans of the committed tick (this rank's, sharded)
+    const int64_t *orphans;    // their sequence numbers (global, sharded)
+    int32_t *log_slot;
+    const uint32_t *lseq;      // sharded: global sequence of each local entry (ascending)
+    int64_t head_local;        // sharded: local entries
+    int shard;
 };
 
 // Host-side launchers (defined in faasbal_kernels.hip; grid sizes are the caller's).

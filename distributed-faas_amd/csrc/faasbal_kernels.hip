@@ -470,8 +470,8 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
     const int k_old = a.tokcnt_in[s];
     int reg = a.reg[s];
     int32_t fr = a.free_in[s].x;
-    double hb = a.hbe[s].hb;
-    uint32_t epoch = a.hbe[s].epoch;
+    double hb = a.hb[s];
+    uint32_t epoch = a.epoch[s];
     int mf = 0, nb = 0;
     for (int k = j; k < a.E && a.skeys[k] == s; ++k) {
         const int i = (int)a.svals[k];
@@ -535,8 +535,8 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     int reg = a.reg[s];
     const int2 fq = a.free_in[s];
     int32_t fr = fq.x;
-    double hb = a.hbe[s].hb;
-    uint32_t epoch = a.hbe[s].epoch;
+    double hb = a.hb[s];
+    uint32_t epoch = a.epoch[s];
     int inq = fq.y;
     int qstat = inq ? kQsKeep : kQsOut;
     int qidx = -1;
@@ -605,7 +605,7 @@ struct Cur {
 __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
     Cur c;
     c.reg0 = a.reg[s];
-    const double hb0 = a.hbe[s].hb;
+    const double hb0 = a.hb[s];
     const int32_t fr0 = a.free_in[s].x;
     if (a.E > 0) {
         // message tick: committed and post-message records loaded together and
@@ -830,36 +830,25 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) v[j] = v[j] < 0 ? -1 : v[j] - a.slot_base;
         }
+        // an entry is an orphan iff its slot's registration alive at tick start died this
+        // tick (entries of earlier registrations were cleared when their tick committed)
         uint32_t died = 0;
         if (a.slots_in_scan) {
-            // died-at-start straight from the records: 8 independent 16-byte {hb, epoch}
-            // gathers per thread; the epoch rides along, so the orphan test needs no
-            // further load
-            double2 h[kFItems];
-            uint32_t tc[kFItems], sq[kFItems];
+            // died-at-start straight from the heartbeats: 8 independent 8-byte gathers per
+            // thread (the committed hb is NaN for a slot without a record: never dead)
+            double h[kFItems];
+            uint32_t tc[kFItems];
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) {
                 const int sj = v[j] < 0 ? 0 : v[j];
-                h[j] = *reinterpret_cast<const double2 *>(a.hbe + sj);
+                h[j] = a.hb[sj];
                 tc[j] = a.E > 0 ? a.touched[sj] : 0u;
-            }
-            if (a.shard) {
-                // the entries' global sequence numbers, in flight with the gathers
-                // (loaded per entry inside the test below they cost one more round trip)
-                const int64_t lb = base + kFItems <= nlog ? base : (nlog > kFItems ? nlog - kFItems : 0);
-                const uint4 s0 = *reinterpret_cast<const uint4 *>(a.lseq + (lb & ~(int64_t)3));
-                const uint4 s1 = *reinterpret_cast<const uint4 *>(a.lseq + (lb & ~(int64_t)3) + 4);
-                sq[0] = s0.x; sq[1] = s0.y; sq[2] = s0.z; sq[3] = s0.w;
-                sq[4] = s1.x; sq[5] = s1.y; sq[6] = s1.z; sq[7] = s1.w;
             }
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) {
                 bool d = false;
-                if (v[j] >= 0) d = (a.E > 0 && tc[j] == a.tick) ? died_touched(a, v[j]) : ((a.now - h[j].x) > a.tte);
-                const uint64_t seq = a.shard ? (uint64_t)(base + kFItems <= nlog ? sq[j] : a.lseq[base + j])
-                                             : (uint64_t)(base + j);
-                const uint32_t ep = (uint32_t)__double_as_longlong(h[j].y);
-                died |= (d && seq >= (uint64_t)ep) ? (1u << j) : 0u;
+                if (v[j] >= 0) d = (a.E > 0 && tc[j] == a.tick) ? died_touched(a, v[j]) : ((a.now - h[j]) > a.tte);
+                died |= d ? (1u << j) : 0u;
             }
         } else {
         const int nwords = (a.W + 63) >> 6;
@@ -889,19 +878,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             died |= (v[j] >= 0 && ((wd >> (sj & 63)) & 1ull)) ? (1u << j) : 0u;
         }
         }
-        uint32_t flags = 0;
-        if (a.slots_in_scan) {
-            flags = died;
-        } else if (died) {
-            uint32_t ep[kFItems];  // all gathers in flight (no per-entry branch + wait)
-#pragma unroll
-            for (int j = 0; j < kFItems; ++j) ep[j] = a.hbe[((died >> j) & 1u) ? v[j] : 0].epoch;
-#pragma unroll
-            for (int j = 0; j < kFItems; ++j) {
-                const uint64_t seq = a.shard ? (uint64_t)a.lseq[base + j] : (uint64_t)(base + j);
-                flags |= (((died >> j) & 1u) & (uint32_t)(seq >= (uint64_t)ep[j])) << j;
-            }
-        }
+        const uint32_t flags = died;
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
         const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
         if (lane_id() == 0) l4[wave_id()] = wv;
@@ -997,7 +974,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 } else {
                     raw = a.free_out[ls].x;
                     // the heartbeat after this tick's messages rides along into the next queue
-                    const double h0 = a.hbe[ls].hb, h1 = a.post_hb[ls];
+                    const double h0 = a.hb[ls], h1 = a.post_hb[ls];
                     hbq = (a.E > 0 && a.touched[ls] == a.tick) ? h1 : h0;
                 }
             }
@@ -1155,51 +1132,19 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
                 for (int j = 0; j < kFItems; ++j) v[k][j] = (base + j < nlog) ? a.log_slot[base + j] : -1;
             }
         }
-        // died bits from LDS, then every epoch gather of a died entry in flight at
-        // once (a died slot's entry is an orphan unless it predates the
-        // registration: sequence below its epoch)
-        uint32_t died[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            died[k] = 0;
-#pragma unroll
-            for (int j = 0; j < kFItems; ++j) {
-                int sj = v[k][j];
-                if (a.shard && sj >= 0) sj -= a.slot_base;  // log slots are global ids
-                v[k][j] = sj;
-                const int sc = sj < 0 ? 0 : sj;
-                died[k] |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
-            }
-        }
-        uint32_t ep[4][kFItems];
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int j = 0; j < kFItems; ++j) ep[k][j] = a.hbe[((died[k] >> j) & 1u) ? v[k][j] : 0].epoch;
-        // sequence numbers: the entry index, or (sharded) the global sequence of
-        // the local entry, loaded as a whole before any use
-        uint32_t sq[4][kFItems];
-        if (a.shard) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const int64_t base = (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems;
-#pragma unroll
-                for (int j = 0; j < kFItems; ++j) sq[k][j] = a.lseq[min(base + j, nlog > 0 ? nlog - 1 : 0)];
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-#pragma unroll
-                for (int j = 0; j < kFItems; ++j)
-                    sq[k][j] = (uint32_t)((int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems + j);
-        }
+        // died bits from LDS: an entry is an orphan iff its slot's registration alive at
+        // tick start died (entries of earlier registrations are cleared at commit)
         uint32_t cnt = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             uint32_t flags = 0;
 #pragma unroll
-            for (int j = 0; j < kFItems; ++j)
-                flags |= (((died[k] >> j) & 1u) & (uint32_t)(sq[k][j] >= ep[k][j])) << j;
+            for (int j = 0; j < kFItems; ++j) {
+                int sj = v[k][j];
+                if (a.shard && sj >= 0) sj -= a.slot_base;  // log slots are global ids
+                const int sc = sj < 0 ? 0 : sj;
+                flags |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
+            }
             a.ofl[(size_t)b * kBS + k * 64 + lane] = (uint8_t)flags;
             cnt += (uint32_t)__popc(flags);
         }
@@ -2090,6 +2035,16 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
 
 // ------------------------------------------------------------ commit
 __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
+    if ((int)blockIdx.x >= a.nbw) {
+        // the committed tick redistributed these entries: their tasks now run under new
+        // sequence numbers, so the old entries leave the in-flight log
+        const int64_t i = (int64_t)(blockIdx.x - a.nbw) * kBS + threadIdx.x;
+        if (i >= a.n_orph) return;
+        const int64_t q = a.orphans[i];
+        const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
+        if (li >= 0) a.log_slot[li] = -1;
+        return;
+    }
     const int s = blockIdx.x * kBS + threadIdx.x;
     if (s >= a.W) return;
     const uint8_t stt = a.st[s];
@@ -2097,14 +2052,11 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
     if (a.touched[s] == a.tick) {
         const bool alive = (stt & kStAlive) != 0;
         a.reg[s] = alive ? 1 : 0;
-        HbRec r;
-        r.hb = alive ? a.post_hb[s] : __builtin_nan("");
-        r.epoch = a.post_epoch[s];
-        r.pad = 0;
-        a.hbe[s] = r;
+        a.hb[s] = alive ? a.post_hb[s] : __builtin_nan("");
+        a.epoch[s] = a.post_epoch[s];
     } else if (stt & kStEvicted) {
         a.reg[s] = 0;
-        a.hbe[s].hb = __builtin_nan("");
+        a.hb[s] = __builtin_nan("");
     }
 }
 

@@ -22,7 +22,8 @@
  * at clock `now` pops one task per iteration while the queue is non-empty.
  * Redistribution (build-defined): at the first dispatch
  * iteration, log entries of registrations that died during the tick are
- * prepended, in ascending sequence, to the pending tasks.
+ * prepended, in ascending sequence, to the pending tasks; at the end of the tick
+ * those entries leave the log (-1), like completed ones.
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -126,7 +127,13 @@ int oracle_load(oracle_t *o, const uint8_t *reg, const int32_t *free_, const dou
         if (s < 0 || s >= o->W || !o->reg[s] || o->inq[s]) return -1;
         q_push_back(o, s);
     }
-    memcpy(o->log, log, (size_t)log_len * 4);
+    /* The in-flight log (build-defined) holds live entries of current
+     * registrations only: an entry of a slot without a record, or older than its
+     * registration's epoch, can never be redistributed, so it is dropped here. */
+    for (int64_t i = 0; i < log_len; i++) {
+        int32_t s = log[i];
+        o->log[i] = (s >= 0 && (!o->reg[s] || (uint64_t)i < o->epoch[s])) ? -1 : s;
+    }
     o->head = log_len;
     o->events_since_purge = 1;
     return 0;
@@ -251,6 +258,8 @@ int oracle_tick(oracle_t *o, double now, double tte, int32_t E, const uint8_t *k
         }
     }
     o->head = head_in + k;
+    /* redistributed entries leave the log: their tasks run under new sequence numbers */
+    for (int64_t i = 0; i < O; i++) o->log[orphan_out[i]] = -1;
     int32_t ne = 0;
     for (int32_t s = 0; s < o->W; s++)
         if (o->seen[s] && !o->reg[s]) evicted_out[ne++] = s;

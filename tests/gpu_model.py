@@ -18,6 +18,10 @@ def tick(st, now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, T):
     log = st["log"].copy()
     head = len(log)
     W = len(reg0)
+    # the log holds live entries of current registrations only (entries of slots
+    # without a record, or older than their registration's epoch, are dropped at load)
+    stale = (log >= 0) & ((~reg0[np.clip(log, 0, None)]) | (np.arange(head) < epoch[np.clip(log, 0, None)]))
+    log[stale] = -1
     E = len(ev_kind)
     inq = np.zeros(W, bool)
     inq[queue] = True
@@ -127,6 +131,7 @@ def tick(st, now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, T):
                 newq[AL - p + rankL1[pos]] = s
     nq = [newq[i] for i in range(len(newq))]
     new_log = np.concatenate([log, assign.astype(np.int32)])
+    new_log[np.asarray(orph, np.int64)] = -1  # redistributed entries leave the log at commit
     reg_out = reg0.copy()
     hb_out = hb.copy()
     ep_out = epoch.copy()

@@ -35,7 +35,11 @@ def shard_range(W, world, rank):
 def split(st, world, rank):
     W = len(st["reg"])
     base, n = shard_range(W, world, rank)
-    log = np.asarray(st["log"], np.int64)
+    log = np.asarray(st["log"], np.int64).copy()
+    # live entries of current registrations only (fb_load_shard drops the others)
+    reg, ep = np.asarray(st["reg"]).astype(bool), np.asarray(st["epoch"], np.int64)
+    li = np.clip(log, 0, None)
+    log[(log >= 0) & (~reg[li] | (np.arange(len(log)) < ep[li]))] = -1
     seq = np.nonzero((log >= base) & (log < base + n))[0]
     return dict(base=base, n=n, reg=st["reg"][base:base + n].astype(bool).copy(),
                 free=st["free"][base:base + n].astype(np.int64).copy(), hb=st["hb"][base:base + n].copy(),
@@ -183,8 +187,10 @@ def phase2(rs, ctx, x):
     hb[touched], ep[touched] = ctx["cur_hb"][touched], ctx["cur_ep"][touched]
     reg[evicted & ~touched] = False
     assert np.all(np.diff(tasks) > 0)
+    log_slot = ctx["log_slot"].copy()
+    log_slot[np.isin(rs["log_seq"], ctx["orphans"])] = -1  # redistributed entries leave the log at commit
     nxt = dict(rs, reg=reg, free=free_out, hb=hb, epoch=ep, queue=queue,
-               log_slot=np.concatenate([ctx["log_slot"], slots]),
+               log_slot=np.concatenate([log_slot, slots]),
                log_seq=np.concatenate([rs["log_seq"], head + tasks]), head=head + N_eff)
     out = dict(task=tasks, slot=slots.astype(np.int32), orphans=ctx["orphans"].astype(np.int64),
                evicted=(np.nonzero(evicted)[0] + base).astype(np.int32),
