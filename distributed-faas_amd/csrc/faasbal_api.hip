@@ -146,6 +146,9 @@ struct fb_ctx {
     int64_t *fpre = nullptr, *wpre = nullptr;
     uint32_t *qcnt = nullptr;
     uint32_t *segcnt = nullptr;  // fused path: per-segment round counts (4 x table)
+    uint32_t *grp[2] = {nullptr, nullptr};  // fused path: group rows of round totals, by launch parity
+    int gpar = 0;                           // parity of the last fused launch
+    int gdirty[2] = {0, 0};                 // words of grp[p] written since it was last zeroed
     int64_t *qpre = nullptr, *A = nullptr;
     size_t table_cap = 0;  // entries of qcnt / qpre
     int R_cap = 0;         // entries of A
@@ -458,6 +461,22 @@ int enqueue_tick(fb_ctx *c) {
     // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
     a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
     a.cfirst = c->emit_cfirst;
+    if (a.fused) {
+        // group rows: about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads both)
+        int gs = 0;
+        while ((1 << (2 * gs)) < nbq) ++gs;
+        a.grp_on = 1;
+        a.gshift = gs;
+        a.gstride = R + 4;
+        a.ngrp = (int)cdiv(nbq, 1 << gs);
+        if ((int64_t)a.ngrp * a.gstride > kGrpWords) return fail(c, FB_ERANGE, "group rows exceed %d words", kGrpWords);
+        c->gpar ^= 1;
+        a.grp = c->grp[c->gpar];  // zero: its last user's k_emit2 cleared it
+        a.grp_zero = c->grp[c->gpar ^ 1];
+        a.zero_words = c->gdirty[c->gpar ^ 1];
+        c->gdirty[c->gpar ^ 1] = 0;
+        c->gdirty[c->gpar] = a.ngrp * a.gstride;
+    }
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
     // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
     // (2 MB of records) those gathers miss L2, so k_slots first writes the
@@ -699,6 +718,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     const size_t tab = (size_t)128 * (size_t)cdiv(Qlog, kBS);
     ap.add(&c->qcnt, tab);
     ap.add(&c->segcnt, 4 * tab);
+    ap.add(&c->grp[0], kGrpWords);
+    ap.add(&c->grp[1], kGrpWords);
     ap.add(&c->qpre, tab);
     ap.add(&c->A, 128);
     ap.add(&c->log_slot, F);
@@ -760,6 +781,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         c->ev_seq = c->evq[0];
     }
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
+    for (int p = 0; p < 2 && !rc; ++p)
+        if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
     if (rc) {
         fb_destroy(c);

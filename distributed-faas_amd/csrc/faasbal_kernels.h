@@ -25,6 +25,7 @@ constexpr int kTabLd = 16;         // ... read by at most 16 int4 loads per thre
 constexpr int kPeel = 4;           // fused tick: block-count arrays of at most 4*256 entries
 constexpr int kLdsBitmapSlots = 1 << 17;  // died bitmap staged in LDS up to 128K slots (16 KB)
 constexpr int kLsBS = 1024;        // k_logscan: one 16-wave workgroup per CU
+constexpr int kGrpWords = 64 * 132;  // fused path: group rows of round totals (<= 64 groups x (128 + 4) words)
 
 // event kinds / status (include/faasbal.h)
 constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3;
@@ -124,6 +125,13 @@ struct TickArgs {
     int4 *c_tok;                               // deque: {rank j, m, q, k} per position (k_scan -> emit)
     int32_t *tokcnt_out, *xw_out, *kl_out;
     uint32_t *qrank_out;
+    // fused path: every k_scan queue block adds its round counts into its group's
+    // row (2^gshift blocks per group; row = R counts, then max c), k_emit2 reads the
+    // ngrp group rows plus its group's earlier block rows instead of the whole table
+    int grp_on, gshift, gstride, ngrp;
+    uint32_t *grp;       // this launch's rows (zero before k_scan)
+    uint32_t *grp_zero;  // the other parity's rows: k_emit2 zeroes zero_words of them for the next launch
+    int zero_words;
     int f_sep;        // 1: log role in its own launch (k_logscan, died bitmap in LDS); k_scan W-role writes the bitmap
     int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;

@@ -811,9 +811,11 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     const int SO = a.nbw;
     const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
     STAMP(a, SO, 0);
-    if (bid < nbf) {
+    // grid: queue blocks first (the critical path: their loads go out before the log
+    // role's gathers fill the memory queues), then log blocks, then slot blocks
+    if (bid >= a.nbq && bid - a.nbq < nbf) {
         // ---- F-role: orphan flags of log entries [b*2048 + t*8, +8)
-        const int b = bid;
+        const int b = bid - a.nbq;
         const int64_t nlog = a.shard ? a.head_local : a.head_in;
         const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
         int32_t v[kFItems];
@@ -892,15 +894,14 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         STAMP(a, SO, 15);
         return;
     }
-    const int nbw = (a.shard == 2 || !a.slots_in_scan) ? 0 : a.nbw;
-    if (bid < nbf + nbw) {
+    if (bid >= a.nbq) {
         // ---- W-role: heartbeat purge of slots [b*256, +256)
-        slots_body(a, bid - nbf, l4);
+        slots_body(a, bid - a.nbq - nbf, l4);
         STAMP(a, SO, 15);
         return;
     }
     // ---- Q-role: LRU positions [b*256, +256) of fronts ++ queue ++ backs
-    const int b = bid - nbf - nbw;
+    const int b = bid;
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
     int c = 0, oc = 0;
     if (a.shard == 2) {
@@ -1062,6 +1063,8 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 t = wc[0][threadIdx.x] + wc[1][threadIdx.x] + wc[2][threadIdx.x] + wc[3][threadIdx.x];
                 uint32_t *tabp = tab ? a.ocnt : a.qcnt;
                 tabp[(size_t)b * a.R + rc + threadIdx.x] = t;
+                // fused: the group's row of round totals (memory-side atomics, no return)
+                if (a.grp_on && t) atomicAdd(&a.grp[(b >> a.gshift) * a.gstride + rc + threadIdx.x], t);
             }
             if (tab == 0) {
                 // sum_r count(c > r) over r < R = sum of min(c, R): the block's capacity when c <= R
@@ -1078,6 +1081,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         for (int w = 1; w < kWaves; ++w) bm = m4[w] > bm ? m4[w] : bm;
         a.qbm_raw[b] = bm;
         a.csum[b] = csum;
+        if (a.grp_on && bm > 0) atomicMax(&a.grp[(b >> a.gshift) * a.gstride + a.R], (uint32_t)bm);
     }
     STAMP(a, SO, 15);
 }
@@ -1490,31 +1494,43 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
 }
 
 // ------------------------------------------------------------ k_emit2
-// k_emit for the fused path (round table of at most 8192 entries read as int4
-// [block][round]; no k_plan launch).  Two block barriers in all: per-thread
-// table partials -> barrier -> round rows (this block's prefix, totals) ->
+// k_emit for the fused path (no k_plan launch).  Every k_scan queue block added
+// its round counts into its group's row (atomics, groups of 2^gshift blocks), so
+// a queue block reads the group rows (totals A(r), the prefix of earlier groups)
+// and the rows of the earlier blocks of its own group: about 2 sqrt(nbq) rows
+// instead of the whole nbq x R table.  One block barrier: per-thread partials ->
 // barrier; then every wave works alone: S(r) and the fill level L by a wave
-// scan, the task index base of each round in one register (lane i: round
-// 64k + i) from the round prefix plus the earlier segments' counts that k_scan
-// stored per 64-position segment, and the emission.  F / W roles as k_emit's.
-constexpr int kTabLd2 = 8;  // int4 table loads per thread (tail loop beyond 8192 entries)
-constexpr int kRCh = 3;     // 64-round chunks: rounds 0 .. L+1 <= 129
+// scan, the task index base of each round in one register (lane i: round 64k +
+// i) from the round prefix plus the earlier segments' counts that k_scan stored
+// per 64-position segment, and the emission.  F / W roles as k_emit's.
+// NCH: 64-round chunks kept per lane (rounds 0 .. L+1): 1 for R = 32, 3 up to R = 128.
+constexpr int kGrpLd = 4;   // group / block row loads per thread per batch
+
+template <int NCH, typename T>
+__device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
+    T x = v[0];
+#pragma unroll
+    for (int i = 1; i < NCH; ++i) x = k == i ? v[i] : x;
+    return x;
+}
 
 // PLAN: large tables (round table beyond the fused limit, R <= 128) -- the same
-// emission with this block's prefixes and the totals from k_plan instead of an
-// in-block reduction of the whole table.
-template <int MODE, bool PLAN>
+// emission with this block's prefixes and the totals from k_plan.
+template <int MODE, bool PLAN, int NCH>
 __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const TickArgs a = specialise<MODE>(a_);
-    __shared__ uint32_t part[kWaves * 32][9];  // per-wave class partials
+    __shared__ uint32_t gpre[kBS], gtot[kBS];  // per-thread partials of (round, part)
     __shared__ uint32_t red[kWaves][4];
-    __shared__ uint32_t pre_c[kRFused];        // this block's prefix of round r
-    __shared__ uint32_t tot_f[kRFused];        // A(r)
-    __shared__ int32_t misc[8];
+    __shared__ uint32_t pre_c[kRFused];        // PLAN: this block's prefix of round r
+    __shared__ uint32_t tot_f[kRFused];        // PLAN: A(r)
     const int bid = blockIdx.x;
     const int SO = a.nbw + a.nbf + a.nbq + (a.slots_in_scan ? a.nbw : 0);
     STAMP(a, SO, 0);
     const int lane = lane_id(), w = wave_id();
+    if constexpr (!PLAN) {
+        // the other parity's group rows, for the next launch's k_scan atomics
+        for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
+    }
     // grid: queue blocks then compaction blocks, or (a.cfirst) compaction first
     const int nbf4 = (a.nbf + 3) >> 2, nbw4 = (a.nbw + 3) >> 2;
     const int qb0 = a.cfirst ? nbf4 + nbw4 : 0;  // first queue block
@@ -1523,9 +1539,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int b = bid - qb0;
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
         const int R = a.R;       // 32, 64 or 128
-        const int cls = R >> 2;  // int4 columns per table row
-        const int lcls = 31 - __builtin_clz(cls);
-        const int nq4 = (a.nbq * R) >> 2;
         // ---- every load in flight at once (clamped indices, no branches)
         const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
         const int32_t raw0 = a.c_arr[pq];
@@ -1534,17 +1547,21 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         // counts of c > r in the earlier segments of this block: lane i, round 64 k + i
         // (all three earlier segments loaded unconditionally, clamped, then masked:
         // a loop bounded by the wave id would issue one load and wait per segment)
-        uint32_t segc[kRCh] = {0, 0, 0};
-        uint32_t sv[kRCh][kWaves - 1];
+        uint32_t segc[NCH];
+        uint32_t sv[NCH][kWaves - 1];
 #pragma unroll
-        for (int k = 0; k < kRCh; ++k)
+        for (int k = 0; k < NCH; ++k) {
+            segc[k] = 0;
 #pragma unroll
             for (int q = 0; q < kWaves - 1; ++q) {
                 const int r = min(64 * k + lane, R - 1);
                 sv[k][q] = a.segcnt[(size_t)(4 * b + q) * R + r];
             }
-        int64_t O, nev, cap;
+        }
+        int64_t O, nev, cap = 0;
         int maxc;
+        uint32_t fo = 0, wo = 0, mo = 0;
+        uint32_t prev[NCH], totv[NCH];  // lane i of chunk k, round 64 k + i: this block's prefix, A(r)
         if constexpr (PLAN) {
             // this block's prefix and the total of every round, scanned by k_plan
             if ((int)threadIdx.x < R) {
@@ -1556,129 +1573,130 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             cap = a.P->cap_total;
             maxc = a.P->maxc;
 #pragma unroll
-        for (int k = 0; k < kRCh; ++k)
+            for (int k = 0; k < NCH; ++k)
 #pragma unroll
-            for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
+                for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
             lds_barrier();
-        } else {
-        const uint4 *tab = reinterpret_cast<const uint4 *>(a.qcnt);
-        uint4 tv[kTabLd2];
 #pragma unroll
-        for (int k = 0; k < kTabLd2; ++k) {
-            const int q = threadIdx.x + k * kBS;
-            tv[k] = tab[q < nq4 ? q : nq4 - 1];
-        }
-        uint32_t fv[kPeel], wv[kPeel], mv[kPeel], cv[kPeel];
-        const int nbf1 = a.nbf > 0 ? a.nbf - 1 : 0, nbw1 = a.nbw - 1, nbq1 = a.nbq - 1;
-#pragma unroll
-        for (int k = 0; k < kPeel; ++k) {
-            const int i = threadIdx.x + k * kBS;
-            fv[k] = a.fcnt[i < nbf1 ? i : nbf1];
-            wv[k] = a.wcnt[i < nbw1 ? i : nbw1];
-            mv[k] = (uint32_t)a.qbm_raw[i < nbq1 ? i : nbq1];
-            cv[k] = (uint32_t)a.csum[i < nbq1 ? i : nbq1];
-        }
-#pragma unroll
-        for (int k = 0; k < kRCh; ++k)
-#pragma unroll
-            for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
-        STAMP(a, SO, 9);
-        uint32_t fo = 0, wo = 0, mo = 0, co = 0;
-#pragma unroll
-        for (int k = 0; k < kPeel; ++k) {
-            const int i = threadIdx.x + k * kBS;
-            fo += i < a.nbf ? fv[k] : 0u;
-            wo += i < a.nbw ? wv[k] : 0u;
-            mo = (i < a.nbq && mv[k] > mo) ? mv[k] : mo;
-            co += i < a.nbq ? cv[k] : 0u;
-        }
-        for (int i = threadIdx.x + kPeel * kBS; i < a.nbf; i += kBS) fo += a.fcnt[i];
-        for (int i = threadIdx.x + kPeel * kBS; i < a.nbw; i += kBS) wo += a.wcnt[i];
-        for (int i = threadIdx.x + kPeel * kBS; i < a.nbq; i += kBS) {
-            mo = (uint32_t)a.qbm_raw[i] > mo ? (uint32_t)a.qbm_raw[i] : mo;
-            co += (uint32_t)a.csum[i];
-        }
-        // table: thread t covers rows r0..r0+3, r0 = 4 (t mod cls), of blocks q / cls
-        uint32_t pp[4] = {0, 0, 0, 0}, tt[4] = {0, 0, 0, 0};
-#pragma unroll
-        for (int k = 0; k < kTabLd2; ++k) {
-            const int q = threadIdx.x + k * kBS;
-            const uint32_t in = q < nq4 ? ~0u : 0u;
-            const uint32_t before = (q < nq4 && (q >> lcls) < b) ? ~0u : 0u;
-            tt[0] += tv[k].x & in; tt[1] += tv[k].y & in; tt[2] += tv[k].z & in; tt[3] += tv[k].w & in;
-            pp[0] += tv[k].x & before; pp[1] += tv[k].y & before;
-            pp[2] += tv[k].z & before; pp[3] += tv[k].w & before;
-        }
-        for (int q = threadIdx.x + kTabLd2 * kBS; q < nq4; q += kBS) {
-            const uint4 v = tab[q];
-            const uint32_t before = (q >> lcls) < b ? ~0u : 0u;
-            tt[0] += v.x; tt[1] += v.y; tt[2] += v.z; tt[3] += v.w;
-            pp[0] += v.x & before; pp[1] += v.y & before; pp[2] += v.z & before; pp[3] += v.w & before;
-        }
-        // lanes of one class (lane mod cls) hold partials of the same 4 rows
-#pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            pp[u] = class_sum_u32(pp[u], cls);
-            tt[u] = class_sum_u32(tt[u], cls);
-        }
-        if (lane < cls) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) {
-                part[w * 32 + lane][u] = pp[u];
-                part[w * 32 + lane][4 + u] = tt[u];
+            for (int k = 0; k < NCH; ++k) {
+                const int rr = min(64 * k + lane, kRFused - 1);
+                prev[k] = pre_c[rr];
+                totv[k] = tot_f[rr];
             }
-        }
-        fo = wave_sum_u32(fo);
-        wo = wave_sum_u32(wo);
-        co = wave_sum_u32(co);
-        mo = wave_max_u32(mo);
-        if (lane == 0) {
-            red[w][0] = fo;
-            red[w][1] = wo;
-            red[w][2] = co;
-            red[w][3] = mo;
-        }
-        lds_barrier();
-        // round rows: this block's prefix and the total, summed over the threads of row r's class
-        if ((int)threadIdx.x < R) {
-            const int r = threadIdx.x, c0 = r >> 2, u = r & 3;
-            pre_c[r] = part[c0][u] + part[32 + c0][u] + part[64 + c0][u] + part[96 + c0][u];
-            tot_f[r] = part[c0][4 + u] + part[32 + c0][4 + u] + part[64 + c0][4 + u] + part[96 + c0][4 + u];
-        }
-        O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
-        cap = (int64_t)red[0][2] + red[1][2] + red[2][2] + red[3][2];
-        maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
-        lds_barrier();
+        } else {
+            // thread t: round r = t mod R, part p = t / R of the rows
+            const int P = kBS / R, r = (int)threadIdx.x & (R - 1), p = (int)threadIdx.x / R;
+            const int g = b >> a.gshift, gsz = 1 << a.gshift, ng = a.ngrp;
+            const int gs = a.gstride;
+            uint32_t pre = 0, tot = 0;
+            // group rows g' = p + P j: totals, and the prefix of the groups before g
+            for (int j0 = 0; j0 * P < ng; j0 += kGrpLd) {
+                uint32_t v[kGrpLd];
+#pragma unroll
+                for (int j = 0; j < kGrpLd; ++j) v[j] = a.grp[min(p + P * (j0 + j), ng - 1) * gs + r];
+#pragma unroll
+                for (int j = 0; j < kGrpLd; ++j) {
+                    const int gg = p + P * (j0 + j);
+                    tot += gg < ng ? v[j] : 0u;
+                    pre += gg < g ? v[j] : 0u;
+                }
+            }
+            // rows of the blocks of group g before b
+            const int nb_in = b - g * gsz;
+            for (int j0 = 0; j0 * P < nb_in; j0 += kGrpLd) {
+                uint32_t v[kGrpLd];
+#pragma unroll
+                for (int j = 0; j < kGrpLd; ++j) {
+                    const int jj = min(p + P * (j0 + j), nb_in - 1);
+                    v[j] = a.qcnt[(size_t)(g * gsz + jj) * R + r];
+                }
+#pragma unroll
+                for (int j = 0; j < kGrpLd; ++j) pre += p + P * (j0 + j) < nb_in ? v[j] : 0u;
+            }
+            // O and evictions from the per-block counts; max c from the group rows
+            uint32_t fv[kPeel], wv[kPeel];
+            const int nbf1 = a.nbf > 0 ? a.nbf - 1 : 0, nbw1 = a.nbw > 0 ? a.nbw - 1 : 0;
+#pragma unroll
+            for (int k = 0; k < kPeel; ++k) {
+                const int i = threadIdx.x + k * kBS;
+                fv[k] = a.fcnt[i < nbf1 ? i : nbf1];
+                wv[k] = a.wcnt[i < nbw1 ? i : nbw1];
+            }
+            const uint32_t mg = a.grp[min((int)threadIdx.x, ng - 1) * gs + R];
+            gpre[threadIdx.x] = pre;
+            gtot[threadIdx.x] = tot;
+#pragma unroll
+            for (int k = 0; k < NCH; ++k)
+#pragma unroll
+                for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
+            STAMP(a, SO, 9);
+#pragma unroll
+            for (int k = 0; k < kPeel; ++k) {
+                const int i = threadIdx.x + k * kBS;
+                fo += i < a.nbf ? fv[k] : 0u;
+                wo += i < a.nbw ? wv[k] : 0u;
+            }
+            for (int i = threadIdx.x + kPeel * kBS; i < a.nbf; i += kBS) fo += a.fcnt[i];
+            for (int i = threadIdx.x + kPeel * kBS; i < a.nbw; i += kBS) wo += a.wcnt[i];
+            mo = (int)threadIdx.x < ng ? mg : 0u;
+            fo = wave_sum_u32(fo);
+            wo = wave_sum_u32(wo);
+            mo = wave_max_u32(mo);
+            if (lane == 0) {
+                red[w][0] = fo;
+                red[w][1] = wo;
+                red[w][3] = mo;
+            }
+            lds_barrier();
+            O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+            nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
+            maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
+            // this lane's rounds: the sum of the P parts
+#pragma unroll
+            for (int k = 0; k < NCH; ++k) {
+                const int rr = 64 * k + lane;
+                uint32_t sp = 0, st_ = 0;
+                if (rr < R)
+                    for (int q = 0; q < P; ++q) {
+                        sp += gpre[q * R + rr];
+                        st_ += gtot[q * R + rr];
+                    }
+                prev[k] = sp;
+                totv[k] = st_;
+            }
         }
         STAMP(a, SO, 1);
         const int rlim = maxc < R ? maxc : R;
-        if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
-        const int64_t N = O + a.T;
-        const int64_t N_eff = N < cap ? N : cap;
-        // ---- per wave: S(r) (lane i of chunk k: round 64 k + i), fill level L
-        int64_t Sv[kRCh];
-        int L = 0;
+        // ---- per wave: S(r) (lane i of chunk k: round 64 k + i), capacity, fill level L
+        int64_t Sv[NCH], S1v[NCH];
         {
             int64_t carry = 0;
 #pragma unroll
-            for (int k = 0; k < kRCh; ++k) {
+            for (int k = 0; k < NCH; ++k) {
                 const int r = 64 * k + lane;
-                const uint32_t v = r < rlim ? tot_f[r] : 0u;
+                const uint32_t v = r < rlim ? totv[k] : 0u;
                 const uint32_t incl = wave_incl_scan_u32(v);
-                const int64_t S1 = carry + (int64_t)incl;  // S(r + 1)
-                Sv[k] = S1 - (int64_t)v;                   // S(r)
-                L += __popcll(__ballot(r < rlim && S1 <= N_eff));
+                S1v[k] = carry + (int64_t)incl;  // S(r + 1)
+                Sv[k] = S1v[k] - (int64_t)v;     // S(r)
                 carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
             }
+            // fused: sum_r A(r) over r < max c = sum of c (PLAN: k_plan's capacity)
+            if constexpr (!PLAN) cap = carry;
         }
+        if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
+        const int64_t N = O + a.T;
+        const int64_t N_eff = N < cap ? N : cap;
+        int L = 0;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) L += __popcll(__ballot(64 * k + lane < rlim && S1v[k] <= N_eff));
         const int Lc = L >> 6, Ll = L & 63;
-        const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Sv[0] : (Lc == 1 ? Sv[1] : Sv[2])), Ll);
+        const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(Sv, Lc), Ll);
         int status = 0;
         if (maxc > R && L >= R - 1) status = 1;   // rows beyond the table needed: rerun wider
         if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log
         const int64_t pL = N_eff - S_L;
-        const int64_t AL = (L < maxc && L < rlim) ? (int64_t)tot_f[L] : 0;
+        const int64_t AL =
+            (L < maxc && L < rlim) ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(totv, Lc), Ll) : 0;
         if (b == 0 && threadIdx.x == 0) {
             a.hout->O = O;
             a.hout->n_evicted = nev;
@@ -1697,11 +1715,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int s = s0;
         // free <= 0 still takes one task; deque mode: c_arr holds the token's c itself
         const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
-        int32_t rbv[kRCh], basev[kRCh];
+        int32_t rbv[NCH], basev[NCH];
 #pragma unroll
-        for (int k = 0; k < kRCh; ++k) {
+        for (int k = 0; k < NCH; ++k) {
             const int r = 64 * k + lane;
-            rbv[k] = (int32_t)((r < rlim ? pre_c[r] : 0u) + segc[k]);
+            rbv[k] = (int32_t)((r < rlim ? prev[k] : 0u) + segc[k]);
             basev[k] = (int32_t)Sv[k] + rbv[k];  // valid for r <= rlim
         }
         STAMP(a, SO, 2);
@@ -1710,7 +1728,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int wmx = (int)wave_max_u32((uint32_t)c);
         const int rfull = L < wmx ? L : wmx;
 #pragma unroll
-        for (int k = 0; k < kRCh; ++k) {
+        for (int k = 0; k < NCH; ++k) {
             const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
             int i = 0;
             // fused (small) ticks branch-free: every lane stores, inactive ones into the
@@ -1747,8 +1765,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         STAMP(a, SO, 3);
         // ---- round L (partial: ranks < pL) and round L + 1 (ranks for the next queue)
         const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
-        const int rbL = __builtin_amdgcn_readlane(Lc == 0 ? rbv[0] : (Lc == 1 ? rbv[1] : rbv[2]), Ll);
-        const int rbL1 = __builtin_amdgcn_readlane(L1c == 0 ? rbv[0] : (L1c == 1 ? rbv[1] : rbv[2]), L1l);
+        const int rbL = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, Lc), Ll);
+        const int rbL1 = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, L1c), L1l);
         const uint64_t mL = __ballot(c > L);
         const int64_t rankL = (int64_t)rbL + popc_lt(mL);
         if (c > L && rankL < pL) out[S_L + rankL] = s;
@@ -1827,6 +1845,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 }
 
 // ------------------------------------------------------------ k_emit_shard
+constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // Phase 2 of a sharded tick.  Every rank computes the global water-filling from
 // the exchanged counts (identical on all ranks), writes the whole next LRU queue,
 // and appends only its own workers' tasks to its log shard -- in ascending global
@@ -2118,18 +2137,24 @@ void launch_plan(const TickArgs &a, Stream st) {
 void launch_emit(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
 }
-template <bool PLAN>
+template <bool PLAN, int NCH>
 static void launch_emit2_t(const TickArgs &a, Stream st) {
     const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
     switch (tick_mode(a)) {
-    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
-    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
-    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PLAN>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN, NCH>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN, NCH>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PLAN, NCH>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
     }
 }
 void launch_emit2(const TickArgs &a, Stream st) {
-    if (a.fused) launch_emit2_t<false>(a, st);
-    else launch_emit2_t<true>(a, st);
+    // one 64-round chunk while rounds 0 .. L+1 <= R+1 fit in a wave's lanes (R = 32)
+    if (a.fused) {
+        if (a.R <= 32) launch_emit2_t<false, 1>(a, st);
+        else launch_emit2_t<false, 3>(a, st);
+    } else {
+        if (a.R <= 32) launch_emit2_t<true, 1>(a, st);
+        else launch_emit2_t<true, 3>(a, st);
+    }
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4), dim3(kBS), 0, st.s, st.e0,

@@ -55,14 +55,14 @@ def main():
         nplan = 3 + 128
         kernels = {"scan": (S, S + nbw + nbq), "logscan": (L0, L0 + ls), "plan": (P0, P0 + nplan),
                    "emit": (E0, E0 + G1)}
-        roles = {"scan.W": (S, S + nbw), "scan.Q": (S + nbw, S + nbw + nbq), "logscan": (L0, L0 + ls),
+        roles = {"scan.Q": (S, S + nbq), "scan.W": (S + nbq, S + nbq + nbw), "logscan": (L0, L0 + ls),
                  "plan": (P0, P0 + nplan)}
     elif split:
         kernels = {"slots": (0, nbw), "scan": (S, S + nbf + nbq), "emit": (E0, E0 + G1)}
-        roles = {"slots": (0, nbw), "scan.F": (S, S + nbf), "scan.Q": (S + nbf, S + nbf + nbq)}
+        roles = {"slots": (0, nbw), "scan.Q": (S, S + nbq), "scan.F": (S + nbq, S + nbq + nbf)}
     else:
         kernels = {"scan": (S, S + nbf + nbw + nbq), "emit": (E0, E0 + G1)}
-        roles = {"scan.F": (S, S + nbf), "scan.W": (S + nbf, S + nbf + nbw), "scan.Q": (S + nbf + nbw, S + G1)}
+        roles = {"scan.Q": (S, S + nbq), "scan.F": (S + nbq, S + nbq + nbf), "scan.W": (S + nbq + nbf, S + G1)}
     nbf4, nbw4 = -(-nbf // 4), -(-nbw // 4)  # k_emit2: one wave per compaction tile
     roles.update({"emit.Q": (E0, E0 + nbq), "emit.F": (E0 + nbq, E0 + nbq + nbf4),
                   "emit.W": (E0 + nbq + nbf4, E0 + nbq + nbf4 + nbw4)})
