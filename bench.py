@@ -206,6 +206,64 @@ def bench_stream(args):
     print(json.dumps(line), flush=True)
 
 
+# The reference loop itself (task_dispatcher.py:324-419, CPython, one core), measured
+# in the survey container with stub zmq/redis and a frozen clock: not
+# re-run on the GPU box (the reference does not travel), carried for comparison.
+REFERENCE_PYTHON = {"value": 82.7, "unit": "assignments/s", "cores": 1,
+                    "sample": "SURVEY.md §6: reference start_heartbeat loop as written, W=64K, T=2K, Zipf free, "
+                              "5% dead, measured in the survey container (CPython 3.10, stub I/O)",
+                    "purge_once_value": 141816.0}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def self_launch(args):
+    """`--gpus N` without a torch.distributed launcher around us: start the N rank
+    processes (one per GPU) as children before anything touches the GPU, and exit
+    with their status."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=%d" % args.gpus,
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def host_observed(g, T, steps, n_assigned):
+    """Decisions the Python host can act on: per tick launch, wait, read the
+    assignments (4 B/task), orphans and evicted slots back into pinned host memory.
+    The tick is relaunched uncommitted (same workload every step); the commit (one
+    kernel, then the host's bookkeeping) is timed once at the end and added per tick."""
+    buf = g.pinned(max(n_assigned, 1), np.int32)
+    for _ in range(3):
+        g.launch(1000.0, 10.0, n_pending=T)
+        g.wait()
+        g.assignments(out=buf)
+    g.sync()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        g.launch(1000.0, 10.0, n_pending=T)
+        g.wait()
+        g.assignments(out=buf)
+        g.orphans()
+        g.evicted()
+    dt = (time.perf_counter() - t0) / steps
+    t1 = time.perf_counter()
+    g.commit()
+    g.sync()
+    tc = time.perf_counter() - t1
+    return {"value": n_assigned / (dt + tc), "unit": "assignments/s", "ms_per_tick": (dt + tc) * 1e3,
+            "readback_ms_per_tick": dt * 1e3, "commit_ms": tc * 1e3, "readback_bytes": 4 * n_assigned,
+            "note": "launch + wait + pinned D2H of assignments/orphans/evicted per tick (uncommitted relaunch), "
+                    "plus one measured commit"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -214,6 +272,7 @@ def main():
     ap.add_argument("--workers", type=int, default=65536)
     ap.add_argument("--tasks", type=int, default=1_000_000)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-host-observed", action="store_true", help="skip the launch+wait+readback+commit timing")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--mode", default="heartbeat", choices=("heartbeat", "deque"),
@@ -221,12 +280,20 @@ def main():
     ap.add_argument("--workload", default="tick", choices=("tick", "stream"),
                     help="stream: configs[4] per GPU -- committed ticks with churn and 64K results each (one GPU)")
     args = ap.parse_args()
+    if args.gpus < 1:
+        raise SystemExit("--gpus must be >= 1")
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(self_launch(args))
     if args.workload == "stream":
+        if args.gpus > 1:
+            raise SystemExit("--workload stream runs on one GPU")
         return bench_stream(args)
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit("--gpus %d but the launcher started %d ranks" % (args.gpus, world))
     dist = None
     dev = 0
     if world > 1:
@@ -235,6 +302,8 @@ def main():
         dev = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev)
         dist.init_process_group(args.backend, device_id=torch.device("cuda", dev) if args.backend == "nccl" else None)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit("torch.distributed reports %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
 
     from faasbal import GpuBalancer, synth
 
@@ -264,7 +333,7 @@ def main():
         def step():
             g.launch(1000.0, 10.0, n_pending=T)
             with torch.cuda.stream(g.stream):
-                dist.all_reduce(g.exchange())
+                dist.all_reduce(g.exchange(), async_op=True).wait()  # phase 2 ordered after it on g.stream
             g.cont()
     step()
     res = g.wait()
@@ -386,9 +455,16 @@ def main():
     if deque:
         line["metric"] = "task assignments/sec, start() loop (no heartbeats), 1M tasks x 64K workers"
         line["data"] = "synthetic (faasbal.synth.zipf_deque_state, seed=0, dup_frac=0.02)"
+    if world > 1:
+        line["config"]["world_size_reported"] = dist.get_world_size()
+        line["config"]["backend"] = dist.get_backend()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_deque(st, T, args.cpu_budget) if deque else \
             cpu_baseline(st, T, args.cpu_budget)
+        if not deque:
+            line["reference_python_value"] = REFERENCE_PYTHON
+    if world == 1 and not args.no_host_observed:
+        line["host_observed"] = host_observed(g, T, min(args.steps, 50), n_assigned)
     if rank == 0:
         print(json.dumps(line), flush=True)
     if dist is not None:

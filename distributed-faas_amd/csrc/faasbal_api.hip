@@ -469,7 +469,8 @@ int enqueue_tick(fb_ctx *c) {
         a.gshift = gs;
         a.gstride = R + 4;
         a.ngrp = (int)cdiv(nbq, 1 << gs);
-        if ((int64_t)a.ngrp * a.gstride > kGrpWords) return fail(c, FB_ERANGE, "group rows exceed %d words", kGrpWords);
+        if (a.ngrp > 64 || (int64_t)a.ngrp * a.gstride > kGrpWords)
+            return fail(c, FB_ERANGE, "group rows (%d x %d words) exceed the reservation", a.ngrp, a.gstride);
         c->gpar ^= 1;
         a.grp = c->grp[c->gpar];  // zero: its last user's k_emit2 cleared it
         a.grp_zero = c->grp[c->gpar ^ 1];
@@ -1305,28 +1306,50 @@ int fb_get_local_assignments(fb_ctx *c, int64_t first, int64_t n, int64_t *task,
     return FB_OK;
 }
 
+// Device -> host copy of a waited tick's output on the context stream.  Into pinned
+// memory (fb_host_alloc) it is one DMA at PCIe rate; into pageable memory the
+// runtime stages it.
+static int copy_out(fb_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!bytes) return FB_OK;
+    HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
+}
+
 int fb_get_assignments(fb_ctx *c, int64_t first, int64_t n, int32_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_get_local_assignments");
     if (first < 0 || n < 0 || first + n > c->last.n_assigned) return fail(c, FB_EINVAL, "assignment range");
-    if (n) HIPCHK(c, hipMemcpy(dst, c->log_slot + c->l_head + first, (size_t)n * 4, hipMemcpyDeviceToHost));
-    return FB_OK;
+    return copy_out(c, dst, c->log_slot + c->l_head + first, (size_t)n * 4);
 }
 
 int fb_get_orphans(fb_ctx *c, int64_t n, int64_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (n < 0 || n > c->last.n_orphans_local) return fail(c, FB_EINVAL, "orphan count");
-    if (n) HIPCHK(c, hipMemcpy(dst, c->orphans, (size_t)n * 8, hipMemcpyDeviceToHost));
-    return FB_OK;
+    return copy_out(c, dst, c->orphans, (size_t)n * 8);
 }
 
 int fb_get_evicted(fb_ctx *c, int32_t n, int32_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (n < 0 || n > c->last.n_evicted) return fail(c, FB_EINVAL, "evicted count");
-    if (n) HIPCHK(c, hipMemcpy(dst, c->evicted, (size_t)n * 4, hipMemcpyDeviceToHost));
+    return copy_out(c, dst, c->evicted, (size_t)n * 4);
+}
+
+int fb_host_alloc(fb_ctx *c, int64_t bytes, void **ptr) {
+    if (!c || !ptr || bytes < 0) return FB_EINVAL;
+    *ptr = nullptr;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (hipHostMalloc(ptr, (size_t)std::max<int64_t>(bytes, 1), hipHostMallocDefault) != hipSuccess)
+        return fail(c, FB_ENOMEM, "hipHostMalloc(%lld B) failed", (long long)bytes);
+    return FB_OK;
+}
+
+int fb_host_free(fb_ctx *c, void *ptr) {
+    if (!c) return FB_EINVAL;
+    if (ptr) HIPCHK(c, hipHostFree(ptr));
     return FB_OK;
 }
 

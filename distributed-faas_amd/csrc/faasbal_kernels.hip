@@ -41,7 +41,16 @@ namespace fb {
 #define STAMPR(a, kernel_off, slot) \
     do {                            \
     } while (0)
+// realtime at the very top of a kernel, before the argument block is copied (slot 12)
+#define STAMP_TOP(a_, kernel_off)                                                                   \
+    do {                                                                                            \
+        const unsigned long long rt_ = __builtin_amdgcn_s_memrealtime();                            \
+        if (threadIdx.x == 0) (a_).dbg[((kernel_off) + blockIdx.x) * 16 + 12] = rt_;              \
+    } while (0)
 #else
+#define STAMP_TOP(a_, kernel_off) \
+    do {                          \
+    } while (0)
 #define STAMPR(a, kernel_off, slot) \
     do {                            \
     } while (0)
@@ -49,6 +58,30 @@ namespace fb {
     do {                           \
     } while (0)
 #endif
+
+// Output stores of the emission kernel: write-through (agent-scope relaxed atomic
+// store = global_store ... sc1) so the lines do not stay dirty in the writing XCD's
+// L2 -- a predecessor's dirty lines stagger the next kernel's start across XCDs by
+// ~1 us while they are written back -- but sc1 stores cost more than they save
+// on configs[2] (11.2 vs 11.0 us per tick), so plain stores are the default
+// (FAASBAL_WT=1: write-through, A/B knob).
+#ifndef FAASBAL_WT
+#define FAASBAL_WT 0
+#endif
+template <typename T>
+__device__ __forceinline__ void wt_store(T *p, T v) {
+#if FAASBAL_WT
+    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte stores");
+    if constexpr (sizeof(T) == 4)
+        __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    else
+        __hip_atomic_store(reinterpret_cast<uint64_t *>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+#else
+    *p = v;
+#endif
+}
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
@@ -774,7 +807,12 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
     const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
     if (lane_id() == 0) l4[wave_id()] = ev;
     lds_barrier();
-    if (threadIdx.x == 0) a.wcnt[blk] = l4[0] + l4[1] + l4[2] + l4[3];
+    if (threadIdx.x == 0) {
+        const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
+        a.wcnt[blk] = n;
+        // fused: evictions into column R + 2 of a group row (k_emit2 sums every row)
+        if (a.grp_on && n) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 2], n);
+    }
 }
 
 template <int MODE>
@@ -801,6 +839,7 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
 // for every round r (table laid out [block][round]).
 template <int MODE>
 __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
+    STAMP_TOP(a_, a_.nbw);
     const TickArgs a = specialise<MODE>(a_);
     extern __shared__ __attribute__((aligned(16))) unsigned long long dyn[];
     __shared__ uint32_t l4[kWaves];
@@ -888,6 +927,8 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         if (threadIdx.x == 0) {
             const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
             a.fcnt[b] = n;
+            // fused: orphans into column R + 1 of a group row (k_emit2 sums every row)
+            if (a.grp_on && n) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], n);
             if (a.shard && n)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)n);
         }
@@ -1037,7 +1078,31 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         if (lane_id() == 0) l4[wave_id()] = ts;
         lds_barrier();
         csum = (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
-    } else
+    } else {
+    // R <= 128: the wave's counts of c > r for every round from a histogram of
+    // min(c, R) in LDS -- one LDS atomic per lane and a wave scan instead of one
+    // ballot per round: count(c > r) = 64 - #(lanes with min(c, R) <= r)
+    uint32_t hcnt[2] = {0u, 0u};
+    if (a.R <= kRFused) {
+        __shared__ uint32_t hist[kWaves][kRFused + 1];
+        uint32_t *h = hist[wave_id()];
+        const int lane = lane_id();
+        for (int i = lane; i <= a.R; i += 64) h[i] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        atomicAdd(&h[c < a.R ? c : a.R], 1u);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t carry = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = 64 * k + lane;
+            const uint32_t hv = h[r < a.R ? r : a.R];
+            const uint32_t P = carry + wave_incl_scan_u32(r < a.R ? hv : 0u);
+            hcnt[k] = r < a.R ? 64u - P : 0u;
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+        }
+    }
     for (int rc = 0; rc < a.R; rc += kBS) {
         const int rn = (a.R - rc) < kBS ? (a.R - rc) : kBS;
         for (int tab = 0; tab < 1; ++tab) {
@@ -1046,7 +1111,9 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             for (int g = 0; g < kBS / 64; ++g) {
                 const int r0 = rc + g * 64;
                 uint32_t cnt = 0;
-                if (r0 < rc + rn && r0 < (int)wmx) {
+                if (a.R <= kRFused) {
+                    cnt = g < 2 ? hcnt[g] : 0u;
+                } else if (r0 < rc + rn && r0 < (int)wmx) {
                     int k = rc + rn - r0;
                     k = k < 64 ? k : 64;
                     k = k < (int)wmx - r0 ? k : (int)wmx - r0;
@@ -1075,6 +1142,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             }
             lds_barrier();
         }
+    }
     }
     if (threadIdx.x == 0) {
         int bm = m4[0];
@@ -1155,6 +1223,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
         cnt = wave_sum_u32(cnt);
         if (lane == 0) {
             a.fcnt[b] = cnt;
+            if (a.grp_on && cnt) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], cnt);
             if (a.shard && cnt)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)cnt);
         }
@@ -1518,6 +1587,7 @@ __device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
 // emission with this block's prefixes and the totals from k_plan.
 template <int MODE, bool PLAN, int NCH>
 __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
+    STAMP_TOP(a_, a_.nbw + a_.nbf + a_.nbq + (a_.slots_in_scan ? a_.nbw : 0));
     const TickArgs a = specialise<MODE>(a_);
     __shared__ uint32_t gpre[kBS], gtot[kBS];  // per-thread partials of (round, part)
     __shared__ uint32_t red[kWaves][4];
@@ -1613,16 +1683,10 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 #pragma unroll
                 for (int j = 0; j < kGrpLd; ++j) pre += p + P * (j0 + j) < nb_in ? v[j] : 0u;
             }
-            // O and evictions from the per-block counts; max c from the group rows
-            uint32_t fv[kPeel], wv[kPeel];
-            const int nbf1 = a.nbf > 0 ? a.nbf - 1 : 0, nbw1 = a.nbw > 0 ? a.nbw - 1 : 0;
-#pragma unroll
-            for (int k = 0; k < kPeel; ++k) {
-                const int i = threadIdx.x + k * kBS;
-                fv[k] = a.fcnt[i < nbf1 ? i : nbf1];
-                wv[k] = a.wcnt[i < nbw1 ? i : nbw1];
-            }
-            const uint32_t mg = a.grp[min((int)threadIdx.x, ng - 1) * gs + R];
+            // max c, orphans and evictions: columns R, R + 1, R + 2 of the group rows
+            // (ngrp <= 64: wave 0 holds them)
+            const int gi = min((int)threadIdx.x, ng - 1) * gs + R;
+            const uint32_t mg = a.grp[gi], og = a.grp[gi + 1], eg = a.grp[gi + 2];
             gpre[threadIdx.x] = pre;
             gtot[threadIdx.x] = tot;
 #pragma unroll
@@ -1630,15 +1694,10 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 #pragma unroll
                 for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
             STAMP(a, SO, 9);
-#pragma unroll
-            for (int k = 0; k < kPeel; ++k) {
-                const int i = threadIdx.x + k * kBS;
-                fo += i < a.nbf ? fv[k] : 0u;
-                wo += i < a.nbw ? wv[k] : 0u;
-            }
-            for (int i = threadIdx.x + kPeel * kBS; i < a.nbf; i += kBS) fo += a.fcnt[i];
-            for (int i = threadIdx.x + kPeel * kBS; i < a.nbw; i += kBS) wo += a.wcnt[i];
-            mo = (int)threadIdx.x < ng ? mg : 0u;
+            const bool gin = (int)threadIdx.x < ng;
+            mo = gin ? mg : 0u;
+            fo = gin ? og : 0u;
+            wo = gin ? eg : 0u;
             fo = wave_sum_u32(fo);
             wo = wave_sum_u32(wo);
             mo = wave_max_u32(mo);
@@ -1733,7 +1792,9 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             int i = 0;
             // fused (small) ticks branch-free: every lane stores, inactive ones into the
             // trash words (an `if (act)` store costs an exec save / branch / restore per
-            // round; configs[2]: tick 13.4 -> 13.0 us)
+            // round; configs[2]: tick 13.4 -> 13.0 us).  (A buffer store predicated by its
+            // range check instead -- inactive lanes given an out-of-range offset -- took
+            // the 19 rounds from 2.0 K to 3.6 K cycles: rejected.)
             // (one 1 KB trash row per block, 1024 rows: no line shared between blocks)
             int32_t *const tr = a.trash + (size_t)(blockIdx.x & (kTrashRows - 1)) * kBS + threadIdx.x;
             for (; i + 3 < r1; i += 4) {
@@ -1746,11 +1807,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                     if constexpr (!PLAN) {
                         // select by mask arithmetic: a ?: on the pointers becomes an exec-masked block
                         const uint64_t pa = (uint64_t)(out + (base + (int)popc_lt(m))), pt = (uint64_t)tr;
-                        *(int32_t *)(pt ^ ((pa ^ pt) & (0ull - (uint64_t)act))) = s;
+                        wt_store((int32_t *)(pt ^ ((pa ^ pt) & (0ull - (uint64_t)act))), s);
                     } else {
                         // large tables (after k_plan): thousands of blocks, where the trash
                         // stores cost more than the branches they save (16M x 1M: +1.2 us)
-                        if (act) out[base + popc_lt(m)] = s;
+                        if (act) wt_store(out + base + popc_lt(m), s);
                     }
                 }
             }
@@ -1759,7 +1820,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 const bool act = c > r;
                 const uint64_t m = __ballot(act);
                 const int base = __builtin_amdgcn_readlane(basev[k], i);
-                if (act) out[base + popc_lt(m)] = s;
+                if (act) wt_store(out + base + popc_lt(m), s);
             }
         }
         STAMP(a, SO, 3);
@@ -1769,7 +1830,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int rbL1 = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, L1c), L1l);
         const uint64_t mL = __ballot(c > L);
         const int64_t rankL = (int64_t)rbL + popc_lt(mL);
-        if (c > L && rankL < pL) out[S_L + rankL] = s;
+        if (c > L && rankL < pL) wt_store(out + S_L + rankL, s);
         const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
@@ -1787,11 +1848,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 return;
             }
             // the worker's next {free, queued}: one 8-byte store
-            a.free_out[s] = make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0);
+            wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
             if (np >= 0) {
-                a.queue_out[np] = s;
-                a.qfree_out[np] = raw - (int32_t)n_q;
-                a.qhb_out[np] = hb0;
+                wt_store(a.queue_out + np, s);
+                wt_store(a.qfree_out + np, raw - (int32_t)n_q);
+                wt_store(a.qhb_out + np, hb0);
             }
         }
         STAMP(a, SO, 15);
@@ -1826,7 +1887,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const uint32_t n = (uint32_t)__popc(f4);
         int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
         const int64_t base = (int64_t)t * kFTile + (int64_t)lane * 4 * kFItems;
-        for (uint32_t m = f4; m; m &= m - 1) a.orphans[o++] = base + __builtin_ctz(m);
+        for (uint32_t m = f4; m; m &= m - 1) wt_store(a.orphans + o++, (int64_t)(base + __builtin_ctz(m)));
     } else {
         // evicted slots, ascending: lane l holds slots t*256 + 4l .. +4
         const int s0 = t * kBS + 4 * lane;
@@ -1839,7 +1900,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         }
         const uint32_t n = (uint32_t)__popc(e);
         int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
-        for (uint32_t m = e; m; m &= m - 1) a.evicted[o++] = s0 + __builtin_ctz(m);
+        for (uint32_t m = e; m; m &= m - 1) wt_store(a.evicted + o++, (int32_t)(s0 + __builtin_ctz(m)));
     }
     STAMP(a, SO, 15);
 }

@@ -22,7 +22,8 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_get_event_status", "fb_tick", "fb_device_view_get", "fb_timing_enable", "fb_timing_read",
            "fb_selftest", "fb_debug_read", "fb_sync", "fb_set_stream", "fb_get_local_assignments",
            "fb_create_sharded", "fb_load_shard", "fb_read_shard_log", "fb_exchange_bytes", "fb_bind_exchange",
-           "fb_tick_continue", "fb_create_deque", "fb_tick_stage", "fb_tick_launch_staged")
+           "fb_tick_continue", "fb_create_deque", "fb_tick_stage", "fb_tick_launch_staged", "fb_host_alloc",
+           "fb_host_free")
 
 
 class TickResult(C.Structure):
@@ -107,6 +108,8 @@ def load(path=None):
         "fb_create_deque": (C.c_int, [C.POINTER(_P), i32, i64, i64, i32, C.c_int]),
         "fb_tick_stage": (C.c_int, [_P, dbl, i32, _P, _P, _P, _P, _P]),
         "fb_tick_launch_staged": (C.c_int, [_P, dbl, i64]),
+        "fb_host_alloc": (C.c_int, [_P, i64, C.POINTER(_P)]),
+        "fb_host_free": (C.c_int, [_P, _P]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name, None)

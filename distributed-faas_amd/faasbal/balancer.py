@@ -73,8 +73,23 @@ class GpuBalancer:
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
+            for p in getattr(self, "_pinned", ()):
+                self.lib.fb_host_free(self.h, p)
+            self._pinned = []
             self.lib.fb_destroy(self.h)
             self.h = C.c_void_p()
+
+    def pinned(self, n, dtype=np.int32):
+        """A numpy array in pinned host memory (freed with the context): output copies
+        into it (``assignments(out=...)``) are single DMA transfers."""
+        dtype = np.dtype(dtype)
+        p = C.c_void_p()
+        self._chk(self.lib.fb_host_alloc(self.h, int(n) * dtype.itemsize, C.byref(p)))
+        if not hasattr(self, "_pinned"):
+            self._pinned = []
+        self._pinned.append(p)
+        buf = (C.c_char * max(int(n) * dtype.itemsize, 1)).from_address(p.value)
+        return np.frombuffer(buf, dtype=dtype, count=int(n))
 
     def __del__(self):
         try:
@@ -162,10 +177,15 @@ class GpuBalancer:
     def commit(self):
         self._chk(self.lib.fb_tick_commit(self.h))
 
-    def assignments(self, first=0, n=None):
+    def assignments(self, first=0, n=None, out=None):
+        """Slot per dispatched task of the waited tick (into ``out`` when given, e.g. a
+        ``pinned()`` array)."""
         n = self.last["n_assigned"] - first if n is None else n
-        out = np.zeros(max(n, 1), np.int32)
-        self._chk(self.lib.fb_get_assignments(self.h, int(first), int(n), _p(out)))
+        if out is None:
+            out = np.zeros(max(n, 1), np.int32)
+        elif len(out) < n or out.dtype != np.int32:
+            raise ValueError("out must be an int32 array of at least %d entries" % n)
+        self._chk(self.lib.fb_get_assignments(self.h, int(first), int(n), out.ctypes.data_as(C.c_void_p)))
         return out[:n]
 
     def local_assignments(self, first=0, n=None):

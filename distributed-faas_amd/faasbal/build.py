@@ -18,10 +18,12 @@ def build_lib(verbose=False, out=None, defines=()):
     OUT_ = out or OUT
     srcs = [os.path.join(CSRC, s) for s in SOURCES]
     hdrs = [os.path.join(CSRC, "faasbal_kernels.h"), os.path.join(REPO, "include", "faasbal.h")]
-    if os.path.exists(OUT_):
+    stamp = OUT_ + ".defines"
+    want = " ".join(sorted(defines))
+    if os.path.exists(OUT_) and os.path.exists(stamp) and open(stamp).read() == want:
         t = os.path.getmtime(OUT_)
         if all(os.path.getmtime(p) < t for p in srcs + hdrs):
-            return OUT
+            return OUT_
     cmd = ["hipcc", "--offload-arch=" + ARCH, "-O3", "-std=c++17", "-fPIC", "-shared",
            "-Wno-unused-result", "-Wno-unused-value",
            *["-D" + d for d in defines],
@@ -30,6 +32,8 @@ def build_lib(verbose=False, out=None, defines=()):
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(OUT_ + ".tmp", OUT_)
+    with open(stamp, "w") as f:  # the -D set this library was built with (up-to-date check)
+        f.write(want)
     return OUT_
 
 

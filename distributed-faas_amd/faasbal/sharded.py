@@ -121,7 +121,9 @@ class ShardedBalancer(GpuBalancer):
         self.launch(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
         with self.torch.cuda.stream(self.stream):
             if allreduce is None:
-                self.torch.distributed.all_reduce(self.exchange())
+                # issued on self.stream; the explicit wait orders phase 2 after it on that
+                # stream (RCCL) or after its completion (gloo)
+                self.torch.distributed.all_reduce(self.exchange(), async_op=True).wait()
             else:
                 allreduce(self.exchange())
         self.cont()

@@ -129,6 +129,11 @@ int fb_get_orphans(fb_ctx *ctx, int64_t n, int64_t *dst);   /* old sequence numb
 int fb_get_evicted(fb_ctx *ctx, int32_t n, int32_t *dst);   /* slots, ascending                */
 int fb_get_event_status(fb_ctx *ctx, int32_t n, uint8_t *dst); /* FB_EVS_* per event          */
 
+/* Pinned host memory: fb_get_* copies into it are single DMA transfers on the
+ * context stream (the drop-in's readback of a tick's assignments). */
+int fb_host_alloc(fb_ctx *ctx, int64_t bytes, void **ptr);
+int fb_host_free(fb_ctx *ctx, void *ptr);
+
 /* launch + wait + copies + commit.  Output arrays may be NULL. */
 int fb_tick(fb_ctx *ctx, double now, double tte, int32_t n_events, const uint8_t *kind,
             const int32_t *slot, const int32_t *val, const double *ts, const int64_t *seq,

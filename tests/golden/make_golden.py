@@ -20,7 +20,7 @@ registrations that died during the tick are put, in ascending original dispatch
 sequence, ahead of the pending tasks.
 
 Only data leaves this script: ``tests/golden/*.npz`` (inputs + expected outputs).
-No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque]
+No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque|cfg2full]
 
 The same harness drives the loop without heartbeats, ``PushDispatcher.start``
 (``task_dispatcher.py:251-322``, a deque of ids instead of the OrderedDict) for
@@ -141,6 +141,20 @@ class RefHarness:
                 self._purge_key = key
             d.purge_workers = purge_once_wrapper
         self._event_epoch = 0
+        # purge-once runs: the worker set changes only when a purge actually ran or an
+        # event was delivered, so the O(W) key sync is skipped otherwise (a 1M-task
+        # dispatch phase over 64K workers stays O(T), not O(T * W))
+        self._dirty = True
+        self._purge_once = purge_once
+        if purge_once:
+            orig2 = d.purge_workers
+
+            def mark_dirty(fw):
+                n = len(d.workers)
+                orig2(fw)
+                if len(d.workers) != n:
+                    self._dirty = True
+            d.purge_workers = mark_dirty
         # registration ids: bumped whenever a key (re)appears in d.workers
         self.regid = collections.defaultdict(int)
         self.keys = set(d.workers)
@@ -222,7 +236,9 @@ class RefHarness:
                 self.records[seq][2] = "completed"
             self.delivering = None
         self.sent_this_iter = []
-        self._sync_keys()
+        if self._dirty or not self._purge_once:
+            self._sync_keys()
+            self._dirty = False
 
     def _end_tick(self):
         self._compute_orphans()
@@ -301,6 +317,7 @@ class RefHarness:
         self.resolved_seq[i] = seq
         self.delivering = (i, w, kind, seq)
         self._event_epoch += 1
+        self._dirty = True
         return w, _Wire(msg)
 
     def send_multipart(self, parts):
@@ -381,6 +398,45 @@ def capture(td, scen, purge_once=False, loop="start_heartbeat"):
     return RefHarness(td, scen, purge_once=purge_once, loop=loop).run()
 
 
+def digests(assign, orphans, evicted, post_reg, post_free, post_hb, post_queue):
+    """sha256 of each output as little-endian bytes (post_free / post_hb of the
+    registered slots only: the reference keeps no record for the others)."""
+    import hashlib
+    reg = np.asarray(post_reg, np.uint8)
+    arrs = dict(assign=np.asarray(assign, "<i4"), orphans=np.asarray(orphans, "<i8"),
+                evicted=np.asarray(evicted, "<i4"), post_reg=reg,
+                post_free=np.asarray(post_free, np.int64)[reg == 1].astype("<i4"),
+                post_hb=np.asarray(post_hb, "<f8")[reg == 1], post_queue=np.asarray(post_queue, "<i4"))
+    return {k: {"sha256": hashlib.sha256(v.tobytes()).hexdigest(), "len": int(len(v))} for k, v in arrs.items()}
+
+
+# BASELINE.json configs[2] at its stated size: the headline tick pinned against the
+# reference itself (digests only: the outputs are MBs; tests recompute them)
+CFG2_FULL = dict(W=65536, seed=0, T=1_000_000, now=1000.0, tte=10.0)
+
+
+def cfg2_full_fixture(td):
+    import json
+    import time
+    p = CFG2_FULL
+    st = synth.zipf_state(W=p["W"], seed=p["seed"])
+    scen = synth.state_to_scenario(st, [synth.empty_tick(p["now"], p["T"])], tte=p["tte"])
+    t0 = time.perf_counter()
+    o = capture(td, scen, purge_once=True)[0]
+    dt = time.perf_counter() - t0
+    out = dict(params=p, generator="faasbal.synth.zipf_state(W, seed) + one tick of T pending tasks at now",
+               reference="task_dispatcher.py:324-419 via tests/golden/make_golden.py (purge once per unchanged "
+                         "clock, SURVEY.md App. B), %.1f s in the capture container" % dt,
+               n_assigned=int(len(o["assign"])), n_orphans=int(len(o["orphans"])),
+               n_evicted=int(len(o["evicted"])), n_pending=int(o["n_pending"]),
+               digests=digests(o["assign"], o["orphans"], o["evicted"], o["post_reg"], o["post_free"], o["post_hb"],
+                               o["post_queue"]))
+    path = os.path.join(HERE, "cfg2_full_digests.json")
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    return [path]
+
+
 def main(which="all"):
     td = load_reference()
     made = []
@@ -388,6 +444,8 @@ def main(which="all"):
         made += heartbeat_fixtures(td)
     if which in ("all", "deque"):
         made += deque_fixtures(td)
+    if which in ("all", "cfg2full"):
+        made += cfg2_full_fixture(td)
     for p in made:
         print(p, os.path.getsize(p))
 

@@ -1,0 +1,122 @@
+"""BASELINE.json configs at their stated sizes.
+
+* configs[2] (1M tasks x 64K workers, Zipf loads, 5 % dead): the oracle and the
+  HIP tick against digests captured from the REFERENCE loop itself
+  (``tests/golden/cfg2_full_digests.json``, ``make_golden.py cfg2full``: the
+  unmodified ``task_dispatcher.py:324-419`` with a purge once per unchanged clock).
+* configs[4] (64K new tasks per tick against 1M workers with churn): committed
+  ticks, the HIP path against the oracle, bit-exact on every output.
+* configs[3] (16M tasks x 1M workers) sharded over world 2 and 4: one tick of the
+  rank contexts (single process, exchange summed on the device) against the oracle.
+"""
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, os.path.join(REPO, "distributed-faas_amd"))
+sys.path.insert(0, os.path.join(REPO, "oracle"))
+sys.path.insert(0, os.path.join(HERE, "golden"))
+
+from faasbal import synth  # noqa: E402
+from make_golden import digests  # noqa: E402  (pure numpy: no reference code is loaded)
+
+CFG2 = json.load(open(os.path.join(HERE, "golden", "cfg2_full_digests.json")))
+
+
+def _cfg2_state():
+    p = CFG2["params"]
+    return p, synth.zipf_state(W=p["W"], seed=p["seed"])
+
+
+def _check(d, where):
+    for k, v in CFG2["digests"].items():
+        assert d[k] == v, "%s: %s differs from the reference capture (%s)" % (where, k, d[k])
+
+
+def test_oracle_cfg2_full_matches_reference():
+    from oracle import Oracle
+    p, st = _cfg2_state()
+    o = Oracle(p["W"], len(st["log"]) + p["T"] + len(st["log"]) + 16, purge_mode=1)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    out = o.tick(p["now"], p["tte"], [], [], [], [], [], p["T"])
+    so = o.export()
+    _check(digests(out["assign"], out["orphans"], out["evicted"], so["reg"], so["free"], so["hb"], so["queue"]),
+           "oracle")
+
+
+@pytest.mark.gpu
+def test_gpu_cfg2_full_matches_reference():
+    from faasbal import GpuBalancer
+    p, st = _cfg2_state()
+    g = GpuBalancer(p["W"], 2 * len(st["log"]) + p["T"] + 16, max_events=1, device=0)
+    g.load(st)
+    out = g.tick(p["now"], p["tte"], n_pending=p["T"])
+    sg = g.read_state(with_log=False)
+    assert out["result"]["n_assigned"] == CFG2["n_assigned"]
+    _check(digests(out["assign"], out["orphans"], out["evicted"], sg["reg"], sg["free"], sg["hb"], sg["queue"]),
+           "HIP tick")
+    g.close()
+
+
+def _cmp(a, b, t):
+    for k in ("reconnect", "assign", "orphans", "evicted"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg="tick %d %s" % (t, k))
+
+
+@pytest.mark.gpu
+def test_gpu_stream_1m_workers_matches_oracle():
+    """configs[4] per GPU: 1M workers, 64K new tasks + 64K results + joins +
+    heartbeats per tick, the clock advancing so silent workers expire; committed
+    ticks, every output and the post-state compared with the oracle (purge once)."""
+    from faasbal import GpuBalancer
+    from oracle import Oracle
+    W, T = 1 << 20, 65536
+    st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=4, seed=2, tasks_per_tick=T, results_per_tick=T)
+    cap = len(st["log"]) + 8 * T
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g = GpuBalancer(W, cap, max_events=E, device=0)
+    g.load(st)
+    o = Oracle(W, cap, purge_mode=1)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    carried, n_orph = 0, 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a = g.tick(*args)
+        b = o.tick(*args)
+        _cmp(a, b, t)
+        assert len(b["assign"]) > 0, "the stream must dispatch"
+        n_orph += len(b["orphans"])
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert n_orph > 0, "silent workers must expire and their tasks be redistributed"
+    sg, so = g.read_state(), o.export()
+    for k in ("reg", "queue", "log"):
+        np.testing.assert_array_equal(sg[k], so[k], err_msg=k)
+    m = so["reg"].astype(bool)
+    np.testing.assert_array_equal(sg["free"][m], so["free"][m])
+    np.testing.assert_array_equal(sg["hb"][m], so["hb"][m])
+    g.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("world", [2, 4])
+def test_gpu_sharded_16m_x_1m_matches_oracle(world):
+    """configs[3]: 16M pending tasks x 1M workers, the worker table sharded by
+    slot range over `world` rank contexts on one GPU; the exchange buffers are
+    summed on the device (what the RCCL all-reduce computes)."""
+    from test_gpu_sharded import _cmp as _cmp_sharded, _group, _group_tick
+    W, T = 1 << 20, 16_000_000
+    st = synth.zipf_state(W=W, seed=0)
+    bals, o = _group(st, world, len(st["log"]) + T + len(st["log"]) + 16, max_events=1)
+    merged, res = _group_tick(bals, 1000.0, 10.0, (), (), (), (), None, T)
+    b = o.tick(1000.0, 10.0, [], [], [], [], [], T)
+    assert len(b["assign"]) == res["n_assigned"] > 0 and len(b["orphans"]) > 0
+    _cmp_sharded(bals, o, merged, b, 0)
+    for x in bals:
+        x.close()

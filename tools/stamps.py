@@ -79,6 +79,13 @@ def main():
         span = (ext.max(axis=1) - ent.min(axis=1)) / 100.0
         spread = (ent.max(axis=1) - ent.min(axis=1)) / 100.0
         print("%-6s span %.2f us (median), entry spread %.2f us" % (kern, np.median(span), np.median(spread)))
+        top = d[:, lo:hi, 12]
+        if (top > 0).all():
+            # realtime at the top of the kernel, before the argument copy
+            tsp = (top.max(axis=1) - top.min(axis=1)) / 100.0
+            lag = np.median((ent - top) / 100.0, axis=1)
+            print("       top-of-kernel spread %.2f us, top -> entry stamp median %.2f us" % (np.median(tsp),
+                                                                                          np.median(lag)))
     ks = list(kernels)
     for a, b in zip(ks[:-1], ks[1:]):
         gap = (starts[b] - d[:, kernels[a][0]:kernels[a][1], 14].max(axis=1)) / 100.0
@@ -94,7 +101,7 @@ def main():
         dur = (x[..., 14] - x[..., 13]) / 100.0
         print("%-7s %4d blocks: entry +%.2f us (p90 %.2f), duration %.2f us (p90 %.2f)" % (
             name, hi - lo, np.median(off), np.percentile(off, 90), np.median(dur), np.percentile(dur, 90)))
-        used = [k for k in range(13) if (x[..., k] > 0).all()] + [15]
+        used = [k for k in range(12) if (x[..., k] > 0).all()] + [15]
         med = {k: np.median(x[..., k] - x[..., 0]) for k in used}
         order = sorted(used, key=lambda k: med[k])
         for a, b in zip(order[:-1], order[1:]):
@@ -102,5 +109,65 @@ def main():
             print("      %2d->%2d  median %7d cyc  p90 %7d" % (a, b, np.median(dt), np.percentile(dt, 90)))
 
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--hist" not in sys.argv and "--xcd" not in sys.argv:
     main()
+
+
+def entry_histogram(workers=65536, tasks=1_000_000, reps=20):
+    """Diagnostic: sorted top-of-kernel offsets of k_scan's blocks (first rep) in 10 bins."""
+    st = synth.zipf_state(W=workers, seed=0)
+    g = GpuBalancer(workers, 2 * len(st["log"]) + tasks + 16, max_events=1, lib_path=STAMPS_SO)
+    g.load(st)
+    nbw, nbf, nbq = -(-workers // 256), -(-len(st["log"]) // 2048), max(1, -(-len(st["queue"]) // 256))
+    for _ in range(reps):
+        g.launch(1000.0, 10.0, n_pending=tasks)
+        g.wait()
+    d = g.debug_read()[: 4 * (nbw + nbf + nbq) * 16].reshape(-1, 16).astype(np.int64)
+    top = d[nbw:nbw + nbq + nbf + nbw, 12]
+    rel = (top - top.min()) / 100.0
+    roles = np.array(["Q"] * nbq + ["F"] * nbf + ["W"] * nbw)
+    order = np.argsort(rel)
+    print("k_scan top-of-kernel offsets (us) by block-id decile:")
+    for dec in range(10):
+        lo, hi = dec * len(rel) // 10, (dec + 1) * len(rel) // 10
+        print("  blocks %4d-%4d: median +%.2f  max +%.2f" % (lo, hi - 1, np.median(rel[lo:hi]), rel[lo:hi].max()))
+    print("  latest 20 blocks:", [(int(i), roles[i], round(float(rel[i]), 2)) for i in order[-20:]])
+
+
+if __name__ == "__main__" and "--hist" in sys.argv:
+    entry_histogram()
+
+
+def xcd_table(workers=65536, tasks=1_000_000, reps=30):
+    """Diagnostic: per XCD (block id mod 8) the median top-of-kernel offset and the
+    median exit offset of k_scan and k_emit2 blocks, relative to the kernel's first top stamp."""
+    st = synth.zipf_state(W=workers, seed=0)
+    g = GpuBalancer(workers, 2 * len(st["log"]) + tasks + 16, max_events=1, lib_path=STAMPS_SO)
+    g.load(st)
+    nbw, nbf, nbq = -(-workers // 256), -(-len(st["log"]) // 2048), max(1, -(-len(st["queue"]) // 256))
+    G1 = nbw + nbf + nbq
+    acc = []
+    for _ in range(reps):
+        g.launch(1000.0, 10.0, n_pending=tasks)
+        g.wait()
+        acc.append(g.debug_read()[: 4 * G1 * 16].reshape(-1, 16).astype(np.int64).copy())
+    d = np.stack(acc)
+    E0 = G1 + nbw
+    ne = nbq + -(-nbf // 4) + -(-nbw // 4)
+    for name, lo, n in (("scan", nbw, G1), ("emit", E0, ne)):
+        x = d[:, lo:lo + n]
+        t0 = x[..., 12].min(axis=1)[:, None]
+        top = (x[..., 12] - t0) / 100.0
+        ext = (x[..., 14] - t0) / 100.0
+        xcd = np.arange(n) % 8
+        print("%s: per block-id mod 8: median top offset / median exit offset (us)" % name)
+        print("   " + "  ".join("%d: %.2f/%.2f" % (k, np.median(top[:, xcd == k]), np.median(ext[:, xcd == k]))
+                               for k in range(8)))
+        if name == "scan":
+            prev_end = None
+        # gap from the previous kernel's last exit
+    print("emit end -> next scan top: measured per rep is not available (one tick per rep)")
+
+
+if __name__ == "__main__" and "--xcd" in sys.argv:
+    xcd_table()
