@@ -179,6 +179,8 @@ struct fb_ctx {
     bool launched = false, waited = false;
     double l_now = 0, l_tte = 0;
     int32_t l_E = 0;
+    bool l_purge_only = false;  // fb_purge_launch: orphans reported, not dispatched
+    bool next_purge_only = false;
     int64_t l_T = 0, l_head = 0, l_Qn = 0;
     int l_R = 64;
     int32_t maxc_hint = 1;
@@ -441,6 +443,7 @@ int enqueue_tick(fb_ctx *c) {
     a.nbf = c->deque ? 0 : nbf;  // start(): nobody dies, no log scan
     a.nbq = nbq;
     a.deque = c->deque;
+    a.redist = c->l_purge_only ? 0 : 1;
     a.q_cap = c->Wq_cap;
     a.tokcnt_in = c->tokcnt[cur];
     a.xw_in = c->xw[cur];
@@ -1189,6 +1192,8 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->reruns = 0;
     c->launched = true;
     c->waited = false;
+    c->l_purge_only = c->next_purge_only;
+    c->next_purge_only = false;
     const int rc = enqueue_tick(c);
     if (rc) return rc;
     if (E) {
@@ -1207,6 +1212,16 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
     int rc = fb_tick_stage(c, now, n_events, kind, slot, val, ts, seq);
     if (rc) return rc;
     return fb_tick_launch_staged(c, tte, n_pending);
+}
+
+int fb_purge_launch(fb_ctx *c, double now, double tte) {
+    if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "sharded context: purge through a tick with n_pending = 0");
+    // a tick without messages or pending tasks whose orphans are reported, not dispatched
+    int rc = fb_tick_stage(c, now, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    c->next_purge_only = true;
+    return fb_tick_launch_staged(c, tte, 0);
 }
 
 int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {

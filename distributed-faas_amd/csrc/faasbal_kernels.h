@@ -118,6 +118,7 @@ struct TickArgs {
     int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
     int slots_in_scan;
     int deque;        // 1: PushDispatcher.start semantics (see EvArgs)
+    int redist;       // 1: orphans are dispatched first (a tick); 0: reported only (fb_purge_launch)
     int64_t q_cap;    // deque: token capacity of queue_out
     const int32_t *tokcnt_in, *xw_in, *kl_in;  // deque: committed per-slot token count, x_w, K_L
     const uint32_t *qrank_in;                  // deque: committed token rank (+ kPart2) per position

@@ -1376,7 +1376,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
             maxc = a.P->maxc;
             rlim = maxc < a.R ? maxc : a.R;
             if (maxc > a.R) cap = INT64_MAX;
-            const int64_t N = O + a.T;
+            const int64_t N = (a.redist ? O : 0) + a.T;  // purge-only ticks report orphans, dispatch none
             N_eff = N < cap ? N : cap;
             int64_t carry = 0;  // S(rc)
             for (int rc = 0; rc < rlim; rc += kBS) {
@@ -1743,7 +1743,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             if constexpr (!PLAN) cap = carry;
         }
         if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
-        const int64_t N = O + a.T;
+        const int64_t N = (a.redist ? O : 0) + a.T;  // purge-only ticks report orphans, dispatch none
         const int64_t N_eff = N < cap ? N : cap;
         int L = 0;
 #pragma unroll
@@ -1962,7 +1962,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         const int maxc = a.P->maxc;
         const int rlim = maxc < R ? maxc : R;
         if (maxc > R) cap = INT64_MAX;
-        const int64_t N = O + a.T;
+        const int64_t N = (a.redist ? O : 0) + a.T;  // purge-only ticks report orphans, dispatch none
         const int64_t N_eff = N < cap ? N : cap;
         // ---- per wave: S(r) and So(r) (lane i of chunk k: round 64 k + i), fill level L
         int64_t Sv[kRCh], Sov[kRCh];

@@ -213,6 +213,18 @@ class GpuBalancer:
         self._chk(self.lib.fb_get_event_status(self.h, int(self._E), _p(out)))
         return out[: self._E]
 
+    def purge(self, now, tte, commit=True):
+        """``purge_workers`` (``task_dispatcher.py:241-249``) alone: expired records
+        deleted, the dead registrations' in-flight tasks reported as orphans but not
+        dispatched.  Returns dict(result, evicted, orphans)."""
+        self._E = 0
+        self._chk(self.lib.fb_purge_launch(self.h, float(now), float(tte)))
+        res = self.wait()
+        out = dict(result=res, evicted=self.evicted(), orphans=self.orphans())
+        if commit:
+            self.commit()
+        return out
+
     def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
              commit=True, outputs=True):
         """One full tick.  Returns dict(result, reconnect, assign, orphans, evicted)."""

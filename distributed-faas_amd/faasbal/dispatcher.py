@@ -366,10 +366,24 @@ class GpuPushDispatcher:
             self.tick()
 
     def purge_workers(self, free_workers=None):
-        """``:241-249`` on its own: a tick at the current clock with no new messages
-        or tasks.  The dead workers' in-flight tasks are redistributed (and already
-        pending tasks dispatched) exactly as in a full tick."""
-        return self._run([])
+        """``purge_workers`` (``:241-249``) on its own: records whose heartbeat expired
+        at the current clock are deleted (their identities become unknown), nothing
+        is dispatched and no message is sent.  The in-flight tasks of the dead
+        workers -- which the reference loses (README.md:263-264) -- go to the front
+        of the pending tasks, for the next tick's dispatch.  Returns the evicted
+        identities."""
+        out = self.balancer.purge(self._stamp(), float(self.time_to_expire))
+        orphan_tids = []
+        for q in out["orphans"]:
+            tid, _ = self.inflight.pop(int(q))
+            self.task_seq.pop(tid, None)
+            orphan_tids.append(tid)
+        if orphan_tids:
+            self.pending.extendleft(reversed(orphan_tids))
+        gone = [self.identity[int(s)] for s in out["evicted"]]
+        for s in out["evicted"]:
+            self._release(int(s))
+        return gone
 
     # ------------------------------------------------------- state / inspection
     @property

@@ -116,6 +116,14 @@ int fb_tick_stage(fb_ctx *ctx, double now, int32_t n_events, const uint8_t *kind
                   const int32_t *val, const double *ts, const int64_t *seq);
 int fb_tick_launch_staged(fb_ctx *ctx, double tte, int64_t n_pending);
 
+/* purge_workers (task_dispatcher.py:241-249, called at :390) on its own: a tick at
+ * `now` with no messages and no pending tasks.  Records whose heartbeat expired
+ * are deleted (fb_get_evicted) and the in-flight tasks of the dead registrations
+ * are reported (fb_get_orphans) but NOT dispatched: the caller keeps them pending
+ * (the reference drops them, README.md:263-264).  Then fb_tick_wait / outputs /
+ * fb_tick_commit as for any tick.  One-GPU and deque contexts. */
+int fb_purge_launch(fb_ctx *ctx, double now, double tte);
+
 /* Wait for the last launched tick; fills *res.  Transparently reruns the tick
  * with a wider round table when free counts exceeded the launch's estimate. */
 int fb_tick_wait(fb_ctx *ctx, fb_tick_result *res);

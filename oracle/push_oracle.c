@@ -48,10 +48,63 @@ typedef struct oracle {
     /* per-tick scratch */
     uint8_t *cur_is_start, *died_start, *seen;
     uint32_t *start_epoch;
-    int purge_mode;    /* 0: purge every iteration (as written), 1: skip when unchanged */
+    int purge_mode;    /* 0: purge every iteration (as written), 1: skip when unchanged,
+                          2: 1 + a min-heap of heartbeats (large tables, per-event clocks) */
     double last_purge_t;
     int64_t events_since_purge;
+    /* purge_mode 2: binary min-heap of (last_heartbeat, slot) entries of registered
+     * slots; an entry is stale once the slot's hb changed or its record was deleted */
+    double *hkey;
+    int32_t *hslot;
+    int64_t hn, hcap;
 } oracle_t;
+
+/* ------------------------------------------------------------ heartbeat heap */
+static int heap_push(oracle_t *o, double key, int32_t s) {
+    if (o->hn == o->hcap) {
+        int64_t cap = o->hcap ? 2 * o->hcap : 1024;
+        double *k2 = (double *)realloc(o->hkey, (size_t)cap * sizeof(double));
+        if (!k2) return -1;
+        o->hkey = k2;
+        int32_t *s2 = (int32_t *)realloc(o->hslot, (size_t)cap * sizeof(int32_t));
+        if (!s2) return -1;
+        o->hslot = s2;
+        o->hcap = cap;
+    }
+    int64_t i = o->hn++;
+    while (i > 0) {
+        int64_t p = (i - 1) / 2;
+        if (!(key < o->hkey[p])) break;
+        o->hkey[i] = o->hkey[p];
+        o->hslot[i] = o->hslot[p];
+        i = p;
+    }
+    o->hkey[i] = key;
+    o->hslot[i] = s;
+    return 0;
+}
+static void heap_pop(oracle_t *o) {
+    double key = o->hkey[--o->hn];
+    int32_t s = o->hslot[o->hn];
+    int64_t i = 0;
+    for (;;) {
+        int64_t c = 2 * i + 1;
+        if (c >= o->hn) break;
+        if (c + 1 < o->hn && o->hkey[c + 1] < o->hkey[c]) c++;
+        if (!(o->hkey[c] < key)) break;
+        o->hkey[i] = o->hkey[c];
+        o->hslot[i] = o->hslot[c];
+        i = c;
+    }
+    if (o->hn) {
+        o->hkey[i] = key;
+        o->hslot[i] = s;
+    }
+}
+/* a registered slot's heartbeat changed (or it was just created) */
+static void hb_touch(oracle_t *o, int32_t s) {
+    if (o->purge_mode == 2 && o->reg[s]) heap_push(o, o->hb[s], s);
+}
 
 /* ---------------------------------------------------------------- queue ops */
 static void q_unlink(oracle_t *o, int32_t s) {
@@ -105,6 +158,7 @@ oracle_t *oracle_create(int32_t W, int64_t log_cap) {
 
 void oracle_destroy(oracle_t *o) {
     if (!o) return;
+    free(o->hkey); free(o->hslot);
     free(o->reg); free(o->free_); free(o->hb); free(o->epoch); free(o->qprev); free(o->qnext);
     free(o->inq); free(o->cur_is_start); free(o->died_start); free(o->seen); free(o->start_epoch);
     free(o->log); free(o);
@@ -127,6 +181,8 @@ int oracle_load(oracle_t *o, const uint8_t *reg, const int32_t *free_, const dou
         if (s < 0 || s >= o->W || !o->reg[s] || o->inq[s]) return -1;
         q_push_back(o, s);
     }
+    o->hn = 0;
+    for (int32_t s = 0; s < o->W; s++) hb_touch(o, s);
     /* The in-flight log (build-defined) holds live entries of current
      * registrations only: an entry of a slot without a record, or older than its
      * registration's epoch, can never be redistributed, so it is dropped here. */
@@ -156,14 +212,32 @@ int64_t oracle_export(const oracle_t *o, uint8_t *reg, int32_t *free_, double *h
 
 /* ------------------------------------------------------------ loop pieces */
 /* purge_workers (:241-249) with PushWorker.is_alive (:209-212) at clock t */
+static void evict(oracle_t *o, int32_t s) {
+    o->reg[s] = 0;
+    if (o->inq[s]) q_unlink(o, s);                    /* del free_workers[remove_id] (:248-249) */
+    if (o->cur_is_start[s]) { o->died_start[s] = 1; o->cur_is_start[s] = 0; }
+}
+
 static void purge(oracle_t *o, double t, double tte) {
-    if (o->purge_mode == 1 && t == o->last_purge_t && o->events_since_purge == 0) return;
-    for (int32_t s = 0; s < o->W; s++) {
-        if (o->reg[s] && (t - o->hb[s]) > tte) {      /* time.time() - last_heartbeat > tte */
-            o->reg[s] = 0;
-            if (o->inq[s]) q_unlink(o, s);            /* del free_workers[remove_id] (:248-249) */
-            if (o->cur_is_start[s]) { o->died_start[s] = 1; o->cur_is_start[s] = 0; }
+    if (o->purge_mode >= 1 && t == o->last_purge_t && o->events_since_purge == 0) return;
+    if (o->purge_mode == 2) {
+        /* the same deletions as the O(W) scan: (t - hb) > tte is monotone in hb (the
+         * fp64 subtraction rounds monotonically), so the dead records are exactly the
+         * smallest heartbeats -- pop them until the smallest live one survives */
+        while (o->hn) {
+            int32_t s = o->hslot[0];
+            double key = o->hkey[0];
+            if (!o->reg[s] || !(o->hb[s] == key)) { heap_pop(o); continue; }  /* stale entry */
+            if (!((t - key) > tte)) break;
+            heap_pop(o);
+            evict(o, s);
         }
+        o->last_purge_t = t;
+        o->events_since_purge = 0;
+        return;
+    }
+    for (int32_t s = 0; s < o->W; s++) {
+        if (o->reg[s] && (t - o->hb[s]) > tte) evict(o, s);  /* time.time() - last_heartbeat > tte */
     }
     o->last_purge_t = t;
     o->events_since_purge = 0;
@@ -176,6 +250,7 @@ static uint8_t handle(oracle_t *o, uint8_t kind, int32_t s, int32_t val, double 
     if (kind == EV_REGISTER) {                                   /* :347-353 */
         if (!o->reg[s]) { o->reg[s] = 1; o->epoch[s] = (uint32_t)head_in; o->seen[s] = 1; }
         o->hb[s] = t;
+        hb_touch(o, s);
         o->free_[s] = val;
         if (val > 0) q_move_front(o, s);
         return 0;
@@ -183,6 +258,7 @@ static uint8_t handle(oracle_t *o, uint8_t kind, int32_t s, int32_t val, double 
     if (!o->reg[s]) {                                            /* :356-358 unknown id */
         o->reg[s] = 1; o->epoch[s] = (uint32_t)head_in; o->seen[s] = 1;
         o->free_[s] = 0; o->hb[s] = t;
+        hb_touch(o, s);
         return 1;                                                /* 'reconnect' sent, payload dropped */
     }
     if (kind == EV_RECONNECT) {                                  /* :360-367 */
@@ -197,6 +273,7 @@ static uint8_t handle(oracle_t *o, uint8_t kind, int32_t s, int32_t val, double 
         if (seq >= 0 && seq < o->head && o->log[seq] == s) o->log[seq] = -1;   /* HSET result */
         if (o->free_[s] == 1 && !o->inq[s]) q_push_back(o, s);
     }
+    if (kind != EV_OTHER) hb_touch(o, s);
     return 0;
 }
 

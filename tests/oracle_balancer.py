@@ -32,3 +32,9 @@ class OracleBalancer:
         out["result"] = dict(n_assigned=len(out["assign"]), n_orphans=len(out["orphans"]),
                              log_head=self.o.export()["head"])
         return out
+
+    def purge(self, now, tte):
+        # purge_workers alone: orphans reported, none dispatched (dispatch_limit = 0)
+        out = self.o.tick(now, tte, [], [], [], [], np.zeros(0, np.int64), 0, dispatch_limit=0)
+        out["result"] = dict(n_assigned=0, n_orphans=len(out["orphans"]), log_head=self.o.export()["head"])
+        return out

@@ -245,6 +245,42 @@ def test_dispatcher_log_compaction_keeps_results(dispatcher_cls):
     assert sum(len(x) for x in runs[0]) > 50
 
 
+def test_purge_workers_evicts_without_dispatching(dispatcher_cls):
+    """purge_workers() (task_dispatcher.py:241-249) deletes the expired records and
+    sends nothing; the dead worker's in-flight tasks go to the front of the pending
+    tasks and the next tick dispatches them first (the reference loses them)."""
+    GpuPushDispatcher = dispatcher_cls
+    env = FakeEnv()
+    d = GpuPushDispatcher("127.0.0.1", 0, 10, max_workers=16, max_events=64, max_inflight=1 << 12,
+                          redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+    env.now = 1000.0
+    for w in range(4):
+        env.inbound.append((wid(w), codec.serialize({"type": "register", "data": {"num_processes": 2}}).encode(),
+                            1000.0))
+    env.tasks.extend("t%d" % j for j in range(6))
+    d.tick()
+    first = [(dst, m["data"]["task_id"]) for dst, m in env.sent if m["type"] == "task"]
+    assert len(first) == 6
+    # workers 1..3 keep sending heartbeats; worker 0 goes silent and expires
+    env.now = 1005.0
+    for w in (1, 2, 3):
+        env.inbound.append((wid(w), codec.serialize({"type": "heartbeat"}).encode(), 1005.0))
+    d.tick()
+    env.sent.clear()
+    env.hsets.clear()
+    env.t = 1010.5  # worker 0's last heartbeat is 10.5 s old, the others' 5.5 s
+    gone = d.purge_workers()
+    assert gone == [wid(0)]
+    assert env.sent == [] and env.hsets == []  # purge sends and writes nothing
+    lost = [tid for dst, tid in first if dst == wid(0)]
+    assert lost and list(d.pending)[:len(lost)] == lost
+    assert wid(0) not in d.workers and wid(0) not in d.free_workers
+    env.now = 1011.0
+    d.tick()
+    redone = [m["data"]["task_id"] for dst, m in env.sent if m["type"] == "task"]
+    assert redone[:len(lost)] == lost and all(dst != wid(0) for dst, _ in env.sent)
+
+
 DEQUE = sorted(glob.glob(os.path.join(os.path.dirname(__file__), "golden", "deque_*.npz")))
 
 

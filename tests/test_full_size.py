@@ -72,7 +72,7 @@ def _cmp(a, b, t):
 def test_gpu_stream_1m_workers_matches_oracle():
     """configs[4] per GPU: 1M workers, 64K new tasks + 64K results + joins +
     heartbeats per tick, the clock advancing so silent workers expire; committed
-    ticks, every output and the post-state compared with the oracle (purge once)."""
+    ticks, every output and the post-state compared with the oracle (heap purge)."""
     from faasbal import GpuBalancer
     from oracle import Oracle
     W, T = 1 << 20, 65536
@@ -82,7 +82,7 @@ def test_gpu_stream_1m_workers_matches_oracle():
     E = max(len(t["ev_kind"]) for t in ticks)
     g = GpuBalancer(W, cap, max_events=E, device=0)
     g.load(st)
-    o = Oracle(W, cap, purge_mode=1)
+    o = Oracle(W, cap, purge_mode=2)  # heap purge: per-event clocks over 1M slots
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
     carried, n_orph = 0, 0
     for t, tk in enumerate(ticks):

@@ -29,7 +29,7 @@ def replay(z, purge_mode):
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
-@pytest.mark.parametrize("purge_mode", [0, 1])
+@pytest.mark.parametrize("purge_mode", [0, 1, 2])
 def test_oracle_matches_reference(path, purge_mode):
     z = np.load(path)
     if purge_mode == 0 and int(z["W"]) > 1024:
@@ -89,3 +89,31 @@ def test_deque_fixtures_hold_duplicates():
             seg = q[off[t]:off[t + 1]]
             n += len(seg) - len(np.unique(seg))
     assert n > 20
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_heap_purge_equals_scan(seed):
+    """purge_mode 2 (min-heap of heartbeats) deletes exactly the records the O(W)
+    scan of purge_workers (task_dispatcher.py:241-249) deletes: random streams with
+    per-event clocks, every output and the exported state compared."""
+    from faasbal import synth
+    scen = synth.random_scenario(100 + seed, W=64, n_ticks=6, max_events=120, max_new=150)
+    outs = []
+    for mode in (1, 2):
+        o = Oracle(scen["W"], len(scen["init_log"]) + 4096, purge_mode=mode)
+        o.load(scen["init_reg"], scen["init_free"], scen["init_hb"], scen["init_epoch"], scen["init_queue"],
+               scen["init_log"])
+        res, carried = [], 0
+        for tk in scen["ticks"]:
+            n = carried + tk["n_new"]
+            r = o.tick(tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"],
+                       tk["ev_seq"], n)
+            res.append(r)
+            carried = n + len(r["orphans"]) - len(r["assign"])
+        outs.append((res, o.export()))
+    (ra, sa), (rb, sb) = outs
+    for a, b in zip(ra, rb):
+        for k in ("reconnect", "assign", "orphans", "evicted"):
+            np.testing.assert_array_equal(a[k], b[k])
+    for k in ("reg", "free", "queue", "log"):
+        np.testing.assert_array_equal(sa[k], sb[k])
