@@ -591,7 +591,7 @@ int enqueue_tick(fb_ctx *c) {
         return FB_OK;
     }
     if (a.shard == 2) {
-        if (R > kRFused) return fail(c, FB_ERANGE, "sharded tick: free counts need %d rounds (limit %d)", R, kRFused);
+        if (R > kRFused) return fail(c, FB_ERANGE, "sharded tick: round table of %d rows (limit %d)", R, kRFused);
         {
             Timer t(c, "scan2");
             launch_scan(a, t.st());
@@ -1189,6 +1189,10 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->phase = 1;
     c->tick += 1;  // per-launch stamp: a relaunch with other messages never sees this launch's marks
     c->l_R = choose_R(std::max(c->maxc_hint, c->st_vmax));
+    // sharded: a round table of at most 128 rows whatever the free counts (k_emit_shard);
+    // counts beyond it are exact for every round below the table (the exchange clamps c
+    // to a byte, 255 > 128), so only a fill level reaching the table fails the tick
+    if (c->shard) c->l_R = std::min(c->l_R, kRFused);
     c->reruns = 0;
     c->launched = true;
     c->waited = false;
@@ -1216,7 +1220,6 @@ int fb_tick_launch(fb_ctx *c, double now, double tte, int32_t n_events, const ui
 
 int fb_purge_launch(fb_ctx *c, double now, double tte) {
     if (!c) return FB_EINVAL;
-    if (c->shard) return fail(c, FB_ESTATE, "sharded context: purge through a tick with n_pending = 0");
     // a tick without messages or pending tasks whose orphans are reported, not dispatched
     int rc = fb_tick_stage(c, now, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
     if (rc) return rc;
@@ -1236,6 +1239,9 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
                         (long long)c->l_head, (long long)c->log_cap);
         // the queue holds free counts beyond the round table: widen and rerun
+        if (c->shard)
+            return fail(c, FB_ERANGE, "sharded tick: the fill level reaches the %d-round table (max free %d)",
+                        c->l_R, c->hout->maxc);
         const int R = choose_R(c->hout->maxc);
         if (R <= c->l_R || c->reruns > 4)
             return fail(c, FB_ERANGE, "fill level beyond the round table (maxc %d, R %d)", c->hout->maxc, c->l_R);

@@ -1033,7 +1033,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     STAMP(a, SO, 1);
     if (a.shard == 1) {
         // phase 1 ends with the c bytes: phase 2 re-derives capacity and max c from
-        // them (exact: sharded ticks keep every c <= 128 < 255, the byte's clamp).
+        // them (exact below the 128-row round table: the byte clamp is 255).
         // Per-wave atomics on one exchange word cost ~10 ns each, serialised --
         // 14 K of them per tick at 8 ranks.
         STAMP(a, SO, 15);

@@ -80,7 +80,7 @@ class GpuPushDispatcher:
 
     def __init__(self, ip_address, port, time_to_expire=10, *, max_workers=65536, max_inflight=1 << 24,
                  max_events=65536, device=0, redis_client=None, subscriber=None, socket=None, poller=None,
-                 clock=time.time, tasks_channel="tasks", batch_io=True):
+                 clock=time.time, tasks_channel="tasks", batch_io=True, balancer=None):
         self.port = port
         self.batch_io = bool(batch_io)
         self.ip_address = ip_address
@@ -111,7 +111,10 @@ class GpuPushDispatcher:
         self.max_inflight = int(max_inflight)
         self.device = device
         self.mode = "heartbeat"
-        self.balancer = GpuBalancer(self.max_workers, self.max_inflight, max_events=self.max_events, device=device)
+        # balancer: the worker table -- one GPU by default; a faasbal.sharded group for a
+        # table sharded over several GPUs (same API, see ShardedPushDispatcher)
+        self.balancer = balancer if balancer is not None else \
+            GpuBalancer(self.max_workers, self.max_inflight, max_events=self.max_events, device=device)
         self._reset_host()
         W = self.max_workers
         self.balancer.load_state(np.zeros(W, np.uint8), np.zeros(W, np.int32), np.zeros(W, np.float64))
@@ -126,6 +129,8 @@ class GpuPushDispatcher:
             return
         if self.ticks:
             raise FaasbalError(-6, "cannot switch the dispatcher loop after %d ticks" % self.ticks)
+        if not isinstance(self.balancer, GpuBalancer):
+            raise FaasbalError(-6, "the loop without heartbeats runs on a one-GPU balancer")
         self.balancer.close()
         self.balancer = GpuBalancer(self.max_workers, self.max_inflight, max_events=self.max_events,
                                     device=self.device, mode=mode)
@@ -450,3 +455,28 @@ class GpuPushDispatcher:
         self.task_seq = {tid: q for q, (tid, _) in self.inflight.items()}
         self.pending = collections.deque(st.get("pending", ()))
         self.head = len(st["log"])
+
+
+def ShardedPushDispatcher(ip_address, port, time_to_expire=10, *, max_workers=65536, max_inflight=1 << 24,
+                          max_events=65536, backend_balancer=None, **kw):
+    """The heartbeat push dispatcher over a worker table sharded across the ranks of
+    the current torch.distributed group (one process per GPU, RCCL over xGMI).
+
+    Rank 0 gets a GpuPushDispatcher whose balancer is a DistShardGroup: it runs the
+    ZMQ / Redis loop, broadcasts each tick's messages and pending count, every rank
+    ticks its own slot range (exchange all-reduce in between) and rank 0 gathers the
+    (task, slot) pairs and sends the task messages in ascending task order
+    (task_dispatcher.py:409-413).  Ranks > 0 serve their shard and return None
+    when rank 0 closes the group (``dispatcher.balancer.close()``)."""
+    import torch.distributed as dist
+
+    from .sharded import DistShardGroup, ShardedBalancer, serve_shard
+    rank, world = dist.get_rank(), dist.get_world_size()
+    bal = backend_balancer if backend_balancer is not None else \
+        ShardedBalancer(rank, world, max_workers, max_inflight, max_events=max_events, device=kw.pop("device", 0))
+    if rank != 0:
+        serve_shard(bal)
+        return None
+    group = DistShardGroup(bal, max_workers)
+    return GpuPushDispatcher(ip_address, port, time_to_expire, max_workers=max_workers, max_inflight=max_inflight,
+                             max_events=max_events, balancer=group, **kw)

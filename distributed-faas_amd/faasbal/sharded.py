@@ -115,6 +115,30 @@ class ShardedBalancer(GpuBalancer):
     def assignments(self, first=0, n=None):
         raise FaasbalError(_lib.FB_ESTATE, "sharded context: use local_assignments()")
 
+    def _allreduce(self, allreduce):
+        n = C.c_int64()
+        self._chk(self.lib.fb_exchange_bytes(self.h, self._E, C.byref(n)))
+        self._xbytes = n.value
+        with self.torch.cuda.stream(self.stream):
+            if allreduce is None:
+                self.torch.distributed.all_reduce(self.exchange(), async_op=True).wait()
+            else:
+                allreduce(self.exchange())
+
+    def purge(self, now, tte, commit=True, allreduce=None):
+        """This rank's share of ``purge_workers`` (``task_dispatcher.py:241-249``):
+        the exchange and phase 2 run as for a tick, nothing is dispatched; returns
+        dict(result, evicted, orphans) of this rank's slots and log shard."""
+        self._E = 0
+        self._chk(self.lib.fb_purge_launch(self.h, float(now), float(tte)))
+        self._allreduce(allreduce)
+        self.cont()
+        res = self.wait()
+        out = dict(result=res, evicted=self.evicted(), orphans=self.orphans())
+        if commit:
+            self.commit()
+        return out
+
     def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
              commit=True, outputs=True, allreduce=None):
         """One sharded tick; ``allreduce(tensor)`` defaults to torch.distributed.all_reduce (SUM)."""
@@ -136,6 +160,186 @@ class ShardedBalancer(GpuBalancer):
         if commit:
             self.commit()
         return out
+
+
+def merge_states(states, n_workers):
+    """The global state (GpuBalancer.read_state layout) from every rank's read_state()."""
+    reg = np.zeros(n_workers, np.uint8)
+    free = np.zeros(n_workers, np.int32)
+    hb = np.zeros(n_workers, np.float64)
+    epoch = np.zeros(n_workers, np.uint32)
+    for st in states:
+        lo, n = st["base"], len(st["reg"])
+        reg[lo:lo + n], free[lo:lo + n], hb[lo:lo + n], epoch[lo:lo + n] = st["reg"], st["free"], st["hb"], st["epoch"]
+    head = states[0]["head"]
+    out = dict(reg=reg, free=free, hb=hb, epoch=epoch, queue=np.asarray(states[0]["queue"], np.int32), head=head)
+    if all("log" in st for st in states):
+        log = np.full(head, -1, np.int32)
+        for st in states:
+            log[np.asarray(st["log_seq"], np.int64)] = st["log"]
+        out["log"] = log
+    return out
+
+
+class ShardGroup:
+    """A worker table sharded over ranks, behind GpuBalancer's tick API -- what
+    GpuPushDispatcher drives (``balancer=``), so the drop-in's host loop, message
+    flow and Redis I/O are the same for one GPU and for N.  Subclasses say how a
+    call reaches the ranks: in this process (LocalShardGroup) or over
+    torch.distributed from rank 0 (DistShardGroup)."""
+
+    mode = "heartbeat"
+
+    def __init__(self, n_workers):
+        self.n_workers_global = int(n_workers)
+
+    def _each(self, op, **kw):  # -> list of per-rank results, rank order
+        raise NotImplementedError
+
+    def load_state(self, reg, free, hb, epoch=None, queue=(), log=()):
+        W = len(reg)
+        st = dict(reg=np.asarray(reg, np.uint8), free=np.asarray(free, np.int32), hb=np.asarray(hb, np.float64),
+                  epoch=np.zeros(W, np.uint32) if epoch is None else np.asarray(epoch, np.uint32),
+                  queue=np.asarray(queue, np.int32), log=np.asarray(log, np.int32))
+        self._each("load", st=st)
+
+    def load(self, st):
+        self.load_state(st["reg"], st["free"], st["hb"], st.get("epoch"), st["queue"], st["log"])
+
+    def read_state(self, with_log=True):
+        return merge_states(self._each("read", with_log=with_log), self.n_workers_global)
+
+    def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0):
+        k = np.asarray(ev_kind, np.uint8)
+        ev = dict(ev_kind=k, ev_slot=np.asarray(ev_slot, np.int32), ev_val=np.asarray(ev_val, np.int32),
+                  ev_ts=np.asarray(ev_ts, np.float64),
+                  ev_seq=np.full(len(k), -1, np.int64) if ev_seq is None else np.asarray(ev_seq, np.int64))
+        outs = self._each("tick", now=float(now), tte=float(tte), n_pending=int(n_pending), **ev)
+        res = dict(outs[0]["result"])
+        for key in ("n_local", "n_orphans_local"):
+            res[key] = sum(int(o["result"][key]) for o in outs)
+        res["n_evicted"] = sum(int(o["result"]["n_evicted"]) for o in outs)
+        merged = merge_outputs(outs, int(res["n_assigned"]))
+        merged["result"] = res
+        return merged
+
+    def purge(self, now, tte):
+        outs = self._each("purge", now=float(now), tte=float(tte))
+        res = dict(outs[0]["result"])
+        res["n_evicted"] = sum(int(o["result"]["n_evicted"]) for o in outs)
+        return dict(result=res, evicted=np.sort(np.concatenate([o["evicted"] for o in outs])).astype(np.int32),
+                    orphans=np.sort(np.concatenate([o["orphans"] for o in outs])).astype(np.int64))
+
+    def close(self):
+        pass
+
+
+def serve_op(bal, op, kw, allreduce=None):
+    """One group operation on this rank's balancer (every rank runs the same op)."""
+    if op == "load":
+        bal.load(kw["st"])
+        return None
+    if op == "read":
+        return bal.read_state(with_log=kw["with_log"])
+    if op == "tick":
+        out = bal.tick(kw["now"], kw["tte"], kw["ev_kind"], kw["ev_slot"], kw["ev_val"], kw["ev_ts"], kw["ev_seq"],
+                       kw["n_pending"], allreduce=allreduce)
+        return out
+    if op == "purge":
+        return bal.purge(kw["now"], kw["tte"], allreduce=allreduce)
+    raise ValueError("unknown group operation %r" % op)
+
+
+class DistShardGroup(ShardGroup):
+    """Rank 0's view of a table sharded over a torch.distributed group (one process
+    per GPU): every call is broadcast to the ranks (serve_shard() runs on the
+    others), each rank runs it on its own shard -- ticks with the exchange
+    all-reduce over the group's backend (RCCL over xGMI for ``nccl``) -- and the
+    per-rank results come back through one all_gather_object."""
+
+    def __init__(self, balancer, n_workers):
+        super().__init__(n_workers)
+        import torch.distributed as dist
+        self.dist, self.bal = dist, balancer
+        if dist.get_rank() != 0:
+            raise FaasbalError(_lib.FB_ESTATE, "DistShardGroup lives on rank 0; run serve_shard() on the others")
+
+    def _each(self, op, **kw):
+        self.dist.broadcast_object_list([(op, kw)], src=0)
+        mine = serve_op(self.bal, op, kw)
+        outs = [None] * self.dist.get_world_size()
+        self.dist.all_gather_object(outs, mine)
+        return outs
+
+    def close(self):
+        self.dist.broadcast_object_list([("stop", {})], src=0)
+
+
+def serve_shard(balancer):
+    """Rank r > 0 of a DistShardGroup: run rank 0's calls on this shard until it stops."""
+    import torch.distributed as dist
+    while True:
+        box = [None]
+        dist.broadcast_object_list(box, src=0)
+        op, kw = box[0]
+        if op == "stop":
+            return
+        mine = serve_op(balancer, op, kw)
+        dist.all_gather_object([None] * dist.get_world_size(), mine)
+
+
+class LocalShardGroup(ShardGroup):
+    """Every rank's shard in this process (one GPU, or rank contexts on several
+    devices); the exchange is summed on the device -- the reduction RCCL performs
+    across GPUs, byte for byte (one contributor per byte)."""
+
+    def __init__(self, world, n_workers, max_log, max_events=65536, device=0, rank_factory=None):
+        super().__init__(n_workers)
+        make = rank_factory or (lambda r: ShardedBalancer(r, world, n_workers, max_log, max_events, device))
+        self.bals = [make(r) for r in range(world)]
+
+    def _each(self, op, **kw):
+        if op in ("tick", "purge"):
+            return self._collective(op, kw)
+        return [serve_op(b, op, kw) for b in self.bals]
+
+    def _collective(self, op, kw):
+        # phase 1 on every rank, then the summed exchange, then phase 2 / outputs / commit
+        torch = self.bals[0].torch
+        for b in self.bals:
+            if op == "tick":
+                b.launch(kw["now"], kw["tte"], kw["ev_kind"], kw["ev_slot"], kw["ev_val"], kw["ev_ts"], kw["ev_seq"],
+                         kw["n_pending"])
+            else:
+                b._E = 0
+                b._chk(b.lib.fb_purge_launch(b.h, kw["now"], kw["tte"]))
+                n = C.c_int64()
+                b._chk(b.lib.fb_exchange_bytes(b.h, 0, C.byref(n)))
+                b._xbytes = n.value
+        torch.cuda.synchronize()
+        total = self.bals[0].exchange().clone()
+        for b in self.bals[1:]:
+            total += b.exchange()
+        for b in self.bals:
+            b.exchange().copy_(total)
+        torch.cuda.synchronize()
+        outs = []
+        for b in self.bals:
+            b.cont()
+            res = b.wait()
+            if op == "tick":
+                task, slot = b.local_assignments()
+                outs.append(dict(result=res, task=task, slot=slot, orphans=b.orphans(), evicted=b.evicted(),
+                                 reconnect=b.event_status()))
+            else:
+                outs.append(dict(result=res, evicted=b.evicted(), orphans=b.orphans()))
+        for b in self.bals:
+            b.commit()
+        return outs
+
+    def close(self):
+        for b in self.bals:
+            b.close()
 
 
 def merge_outputs(outs, n_assigned):

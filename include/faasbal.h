@@ -121,7 +121,8 @@ int fb_tick_launch_staged(fb_ctx *ctx, double tte, int64_t n_pending);
  * are deleted (fb_get_evicted) and the in-flight tasks of the dead registrations
  * are reported (fb_get_orphans) but NOT dispatched: the caller keeps them pending
  * (the reference drops them, README.md:263-264).  Then fb_tick_wait / outputs /
- * fb_tick_commit as for any tick.  One-GPU and deque contexts. */
+ * fb_tick_commit as for any tick (sharded contexts: the exchange all-reduce and
+ * fb_tick_continue in between, as for a tick). */
 int fb_purge_launch(fb_ctx *ctx, double now, double tte);
 
 /* Wait for the last launched tick; fills *res.  Transparently reruns the tick

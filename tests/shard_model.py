@@ -137,8 +137,9 @@ def phase1(rs, world, rank, now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, T
     return x, ctx
 
 
-def phase2(rs, ctx, x):
-    """Returns (outputs of this rank, next rank state)."""
+def phase2(rs, ctx, x, redist=True):
+    """Returns (outputs of this rank, next rank state).  redist=False: a purge-only
+    tick (fb_purge_launch) -- orphans reported, none dispatched."""
     lay, E, world, base, n, head = ctx["lay"], ctx["E"], ctx["world"], rs["base"], rs["n"], rs["head"]
     rec = x[lay["rec"]:lay["front"]].view(np.uint64).reshape(world, XREC_WORDS).astype(np.int64)
     O, cap, maxc = int(rec[:, 0].sum()), int(rec[:, 1].sum()), int(rec[:, 2].max())
@@ -147,7 +148,7 @@ def phase2(rs, ctx, x):
     lq = np.concatenate([front, rs["queue"], back])
     c = x[lay["c8"]:lay["c8"] + len(lq)].astype(np.int64)
     own = (lq >= base) & (lq < base + n) & (c > 0)
-    N_eff = min(O + ctx["T"], cap)
+    N_eff = min((O if redist else 0) + ctx["T"], cap)
     rlim = min(maxc, R_MAX)
     S = [0]
     for r in range(rlim):

@@ -128,13 +128,27 @@ def pipelines(request):
 def test_dispatcher_replays_reference(path, dispatcher_cls, pipelines):
     GpuPushDispatcher = dispatcher_cls
     z = np.load(path)
+    replay_golden(z, lambda sizes, env: GpuPushDispatcher(
+        "127.0.0.1", 0, float(z["tte"]), **sizes, redis_client=env, subscriber=env, socket=env, poller=env,
+        clock=env.clock), pipelines)
+
+
+def golden_sizes(z):
+    """Table sizes for replaying golden vector z through a dispatcher."""
+    W = int(z["W"])
+    max_e = max(1, int(np.diff(z["ev_off"]).max(initial=0)))
+    return dict(max_workers=2 * W + max_e, max_events=max_e + 1,
+                max_inflight=len(z["init_log"]) + len(z["exp_assign"]) + 64)
+
+
+def replay_golden(z, make_dispatcher, pipelines=True):
+    """Replay a reference-captured golden vector (tests/golden/*.npz) through the
+    dispatcher make_dispatcher(sizes, env) builds, checking every message, Redis
+    write, pending task, LRU queue entry and worker record per tick."""
     W = int(z["W"])
     T = int(z["n_ticks"])
-    max_e = max(1, int(np.diff(z["ev_off"]).max(initial=0)))
     env = FakeEnv(pipelines)
-    d = GpuPushDispatcher("127.0.0.1", 0, float(z["tte"]), max_workers=2 * W + max_e, max_events=max_e + 1,
-                          max_inflight=len(z["init_log"]) + len(z["exp_assign"]) + 64,
-                          redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+    d = make_dispatcher(golden_sizes(z), env)
     reg0 = z["init_reg"].astype(bool)
     # test-side model of the in-flight records (golden sequence numbering)
     seq_tid, seq_slot, inflight = {}, {}, set()
@@ -207,6 +221,7 @@ def test_dispatcher_replays_reference(path, dispatcher_cls, pipelines):
             w = workers[wid(s)]
             assert w.free_processes == int(z["exp_post_free"][t][s]), "tick %d slot %d free" % (t, s)
             assert w.last_heartbeat == float(z["exp_post_hb"][t][s]), "tick %d slot %d hb" % (t, s)
+    return d
 
 
 def test_dispatcher_log_compaction_keeps_results(dispatcher_cls):

@@ -77,7 +77,8 @@ def test_gpu_stream_1m_workers_matches_oracle():
     from oracle import Oracle
     W, T = 1 << 20, 65536
     st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
-    ticks = synth.stream_ticks(st, n_ticks=4, seed=2, tasks_per_tick=T, results_per_tick=T)
+    # 50 ms per tick: workers whose last heartbeat is 9.8+ s old expire along the way
+    ticks = synth.stream_ticks(st, n_ticks=4, seed=2, tasks_per_tick=T, results_per_tick=T, dt=0.05)
     cap = len(st["log"]) + 8 * T
     E = max(len(t["ev_kind"]) for t in ticks)
     g = GpuBalancer(W, cap, max_events=E, device=0)

@@ -180,3 +180,36 @@ def test_sharded_wide_sort_digits(world):
     a, _ = _group_tick(bals, *args)
     b = o.tick(*args)
     _cmp(bals, o, a, b, 0)
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_wide_free_counts(world):
+    """Free counts up to 10 000 (beyond the exchange byte and the 128-row round
+    table): every round below the fill level is exact, so the sharded ticks match
+    the oracle -- registrations with thousands of processes included."""
+    rng = np.random.default_rng(40 + world)
+    W, now = 600, 1000.0
+    reg = np.ones(W, np.uint8)
+    free = rng.integers(0, 10_001, W).astype(np.int32)
+    hb = now - rng.random(W) * 9.9
+    hb[rng.random(W) < 0.03] = now - 10.5
+    queue = rng.permutation(np.nonzero(free > 0)[0]).astype(np.int32)
+    log = rng.integers(-1, W, 20_000).astype(np.int32)
+    st = dict(reg=reg, free=free, hb=hb, epoch=np.zeros(W, np.uint32), queue=queue, log=log)
+    bals, o = _group(st, world, len(log) + 200_000, max_events=512)
+    carried = 0
+    for t in range(4):
+        t_now = now + 0.5 * t
+        E = 200
+        kind = rng.choice([synth.EV_REGISTER, synth.EV_HEARTBEAT, synth.EV_RESULT, synth.EV_RECONNECT], size=E,
+                          p=[0.2, 0.4, 0.3, 0.1]).astype(np.uint8)
+        slot = rng.integers(0, W, E).astype(np.int32)
+        val = rng.integers(0, 10_001, E).astype(np.int32)
+        ts = np.sort(t_now - 0.5 * rng.random(E))
+        n = carried + 25_000
+        args = (t_now, 10.0, kind, slot, val, ts, np.full(E, -1, np.int64), n)
+        a, r = _group_tick(bals, *args)
+        b = o.tick(*args)
+        assert o.export()["free"].max() > 255 and r["max_free"] == 255  # c travels clamped to a byte
+        _cmp(bals, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
