@@ -225,6 +225,10 @@ int fail(fb_ctx *c, int code, const char *fmt, ...) {
     } while (0)
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
+inline int getenv_int(const char *name) {
+    const char *v = getenv(name);
+    return v ? atoi(v) : 0;
+}
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 template <typename T>
@@ -533,6 +537,8 @@ int enqueue_tick(fb_ctx *c) {
     a.A = c->A;
     a.P = c->P;
     a.trash = c->trash;
+    a.arena = (char *)c->arena;
+    a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !getenv_int("FAASBAL_NO_ARENA32")) ? 1 : 0;
     a.log_slot = c->log_slot;
     a.free_out = c->free_[nxt];
     a.queue_out = c->queue[nxt];

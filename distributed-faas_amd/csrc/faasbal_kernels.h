@@ -168,6 +168,8 @@ struct TickArgs {
     // outputs
     int32_t *log_slot;
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
+    char *arena;        // base of the context's arena (every buffer above)
+    int arena32;        // 1: the arena spans < 4 GB (32-bit byte offsets from arena)
     int2 *free_out;     // next {free_processes (INT32_MIN: no live record), queued}
     int32_t *queue_out;
     int32_t *qfree_out;

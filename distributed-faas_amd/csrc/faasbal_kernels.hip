@@ -83,6 +83,12 @@ __device__ __forceinline__ void wt_store(T *p, T v) {
 #endif
 }
 
+// Fused ticks: orphan / eviction totals through atomics into the group rows (1), or
+// read back by every emit queue block from the per-block counts (0).
+#ifndef FAASBAL_GRP_OW
+#define FAASBAL_GRP_OW 1
+#endif
+
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
 __device__ __forceinline__ int popc_lt(uint64_t m) {
@@ -811,7 +817,7 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
         a.wcnt[blk] = n;
         // fused: evictions into column R + 2 of a group row (k_emit2 sums every row)
-        if (a.grp_on && n) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 2], n);
+        if (FAASBAL_GRP_OW && a.grp_on && n) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 2], n);
     }
 }
 
@@ -928,7 +934,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
             a.fcnt[b] = n;
             // fused: orphans into column R + 1 of a group row (k_emit2 sums every row)
-            if (a.grp_on && n) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], n);
+            if (FAASBAL_GRP_OW && a.grp_on && n) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], n);
             if (a.shard && n)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)n);
         }
@@ -1223,7 +1229,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
         cnt = wave_sum_u32(cnt);
         if (lane == 0) {
             a.fcnt[b] = cnt;
-            if (a.grp_on && cnt) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], cnt);
+            if (FAASBAL_GRP_OW && a.grp_on && cnt) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], cnt);
             if (a.shard && cnt)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)cnt);
         }
@@ -1698,6 +1704,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             mo = gin ? mg : 0u;
             fo = gin ? og : 0u;
             wo = gin ? eg : 0u;
+            if (!FAASBAL_GRP_OW) {
+                fo = wo = 0;
+                for (int i = threadIdx.x; i < a.nbf; i += kBS) fo += a.fcnt[i];
+                for (int i = threadIdx.x; i < a.nbw; i += kBS) wo += a.wcnt[i];
+            }
             fo = wave_sum_u32(fo);
             wo = wave_sum_u32(wo);
             mo = wave_max_u32(mo);
@@ -1797,6 +1808,24 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // the 19 rounds from 2.0 K to 3.6 K cycles: rejected.)
             // (one 1 KB trash row per block, 1024 rows: no line shared between blocks)
             int32_t *const tr = a.trash + (size_t)(blockIdx.x & (kTrashRows - 1)) * kBS + threadIdx.x;
+            if (!PLAN && a.arena32) {
+                // every buffer lies in the context's arena (< 4 GB): 32-bit byte offsets from
+                // one scalar base -- a select and a saddr store per round, no 64-bit math
+                char *const ab = a.arena;
+                const uint32_t oo = (uint32_t)((char *)out - ab), to = (uint32_t)((char *)tr - ab);
+                const uint32_t bo = oo + 4u * (uint32_t)basev[k];  // byte offset of each round's first store
+                for (; i + 3 < r1; i += 4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int r = 64 * k + i + u;
+                        const bool act = c > r;
+                        const uint64_t m = __ballot(act);
+                        const uint32_t po = __builtin_amdgcn_readlane(bo, i + u) + 4u * popc_lt(m);
+                        const uint32_t off = to + ((po - to) & (0u - (uint32_t)act));
+                        wt_store((int32_t *)(ab + off), s);
+                    }
+                }
+            }
             for (; i + 3 < r1; i += 4) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {

@@ -137,6 +137,14 @@ class GpuBalancer:
 
     # ----------------------------------------------------------------- ticks
     def launch(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0):
+        if not len(ev_kind) and not len(ev_slot):
+            # a tick without messages (the common idle / dispatch-only tick): straight to
+            # the C ABI, no array conversions (they cost more host time than the launch)
+            self._E = 0
+            rc = self.lib.fb_tick_launch(self.h, now, tte, 0, None, None, None, None, None, n_pending)
+            if rc:
+                self._chk(rc)
+            return
         k = _arr(ev_kind, np.uint8)
         s = _arr(ev_slot, np.int32)
         v = _arr(ev_val, np.int32)
