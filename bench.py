@@ -138,7 +138,8 @@ def bench_stream(args):
     T = 65536
     K, Wu = min(args.steps, 50), min(args.warmup, 5)  # 64K distinct results per tick from the initial log
     st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
-    ticks = synth.stream_ticks(st, n_ticks=Wu + 2 * K, seed=2, tasks_per_tick=T, results_per_tick=T)
+    ticks = synth.stream_ticks(st, n_ticks=Wu + 2 * K, seed=2, tasks_per_tick=T, results_per_tick=T,
+                               hb_frac=args.hb_frac)
     E = max(len(t["ev_kind"]) for t in ticks)
     g = GpuBalancer(W, len(st["log"]) + (Wu + 2 * K + 2) * 2 * T, max_events=E, device=0)
     g.load(st)
@@ -197,7 +198,7 @@ def bench_stream(args):
         "data": "synthetic (faasbal.synth.zipf_state(W, seed=0, dead_frac=0) + stream_ticks(seed=2))",
         "config": {"workload": "configs[4] per GPU: %d workers, %d new tasks + %d results + %d joins + %d heartbeats "
                                "per tick, 10 ms per tick, committed ticks" % (W, T, T, max(1, W // 1000),
-                                                                                max(1, W // 100)),
+                                                                                max(1, int(args.hb_frac * W))),
                    "workers": W, "events_per_tick": stats["events"] / K, "assigned_per_tick": stats["assigned"] / K,
                    "orphans_per_tick": stats["orphans"] / K, "evicted_per_tick": stats["evicted"] / K},
         "tick": {"device_us_per_tick": sum(per_tick.values()), "kernels_us_per_tick": per_tick,
@@ -279,6 +280,8 @@ def main():
                     help="deque: the loop without heartbeats (PushDispatcher.start), one GPU")
     ap.add_argument("--workload", default="tick", choices=("tick", "stream"),
                     help="stream: configs[4] per GPU -- committed ticks with churn and 64K results each (one GPU)")
+    ap.add_argument("--hb-frac", type=float, default=0.01,
+                    help="stream: heartbeats per tick as a fraction of the workers (1.0: a 1M-message storm)")
     args = ap.parse_args()
     if args.gpus < 1:
         raise SystemExit("--gpus must be >= 1")

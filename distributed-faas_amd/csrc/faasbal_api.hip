@@ -161,6 +161,7 @@ struct fb_ctx {
     int force_plan = 0;
     int emit_cfirst = 0;  // FAASBAL_EMIT_CFIRST: k_emit2 grid order (A/B knob)
     int rs_wide = 1;       // FAASBAL_RS_WIDE=0: 8-bit sort digits only (A/B knob)
+    int gplan = 1;         // FAASBAL_GPLAN=0: large k_emit2 tables through k_plan, not k_plan2 (A/B knob)
     int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
     int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
@@ -468,10 +469,16 @@ int enqueue_tick(fb_ctx *c) {
     // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
     a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
     a.cfirst = c->emit_cfirst;
-    if (a.fused) {
-        // group rows: about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads both)
+    // large tables for k_emit2: group rows too, scanned by k_plan2 (FAASBAL_GPLAN=0: k_plan)
+    const bool gplan = !a.fused && a.segw && !c->shard && c->gplan;
+    if (a.fused || gplan) {
+        // group rows: fused, about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads
+        // both); k_plan2, the smallest groups that make at most 64 rows (one workgroup each)
         int gs = 0;
-        while ((1 << (2 * gs)) < nbq) ++gs;
+        if (a.fused)
+            while ((1 << (2 * gs)) < nbq) ++gs;
+        else
+            while (cdiv(nbq, (int64_t)1 << gs) > 64) ++gs;
         a.grp_on = 1;
         a.gshift = gs;
         a.gstride = R + 4;
@@ -708,7 +715,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->vals[i], E);
     }
     // 8-bit passes: 256 x blocks; wide passes (a tick of <= kRsWideMaxBlocks blocks): 2048 x blocks
-    ap.add(&c->rs_hist, std::max((size_t)256 * cdiv(E, kRsTile), (size_t)2048 * (size_t)std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks)));
+    ap.add(&c->rs_hist, std::max((size_t)256 * (cdiv(E, kRsTile) + 1),
+                                 (size_t)2048 * (size_t)(std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks) + 1)));
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
     ap.add(&c->c_arr, Qlog);
@@ -767,6 +775,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_EMIT_CFIRST")) c->emit_cfirst = atoi(getenv("FAASBAL_EMIT_CFIRST"));
     if (!rc && getenv("FAASBAL_LOGSCAN")) c->logscan = atoi(getenv("FAASBAL_LOGSCAN"));
     if (!rc && getenv("FAASBAL_RS_WIDE")) c->rs_wide = atoi(getenv("FAASBAL_RS_WIDE"));
+    if (!rc && getenv("FAASBAL_GPLAN")) c->gplan = atoi(getenv("FAASBAL_GPLAN"));
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;

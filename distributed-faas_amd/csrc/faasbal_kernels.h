@@ -224,11 +224,19 @@ struct Stream {
     Stream(hipStream_t s_, hipEvent_t a, hipEvent_t b) : s(s_), e0(a), e1(b) {}
 };
 // One LSD pass (histogram + scatter launches) over `db`-bit digits at `shift`;
-// hist holds (1 << db rounded up to 256 / 1024 / 2048) x nblk counts.
+// hist holds (1 << db rounded up to 256 / 1024 / 2048) x (nblk + 1) counts (the
+// extra row: digit totals when nblk > kRsScanMin).
 void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
                     int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
                     Stream s);
-constexpr int kRsWideMaxBlocks = 256;  // wider digits only while the scatter prologue's table walk stays short
+#ifndef FAASBAL_RS_SCAN_MIN
+#define FAASBAL_RS_SCAN_MIN 64
+#endif
+// batches of more tiles than this get a column-prefix launch (k_rs_scan) before the
+// scatter instead of every scatter block walking the [tile][digit] table
+constexpr int kRsScanMin = FAASBAL_RS_SCAN_MIN;
+// wider digits (2 passes for 1 M workers) up to this many tiles: the table is 2048 x tiles words
+constexpr int kRsWideMaxBlocks = 4096;
 void launch_ev_apply(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 void launch_slots(const TickArgs &a, Stream st);

@@ -41,6 +41,13 @@ namespace fb {
 #define STAMPR(a, kernel_off, slot) \
     do {                            \
     } while (0)
+// after every outstanding vector memory operation of the wave completed (serialises
+// the loads before it against the ones after: diagnostic only)
+#define STAMPW(a, kernel_off, slot)                                 \
+    do {                                                            \
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");            \
+        STAMP(a, kernel_off, slot);                                 \
+    } while (0)
 // realtime at the very top of a kernel, before the argument block is copied (slot 12)
 #define STAMP_TOP(a_, kernel_off)                                                                   \
     do {                                                                                            \
@@ -56,6 +63,9 @@ namespace fb {
     } while (0)
 #define STAMP(a, kernel_off, slot) \
     do {                           \
+    } while (0)
+#define STAMPW(a, kernel_off, slot) \
+    do {                            \
     } while (0)
 #endif
 
@@ -355,11 +365,53 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ ke
     }
 }
 
+// Large batches (nblk > kRsScanMin): the column prefixes in their own launch, so a
+// scatter block reads its own row and the digit totals (O(NB)) instead of walking
+// the whole table (O(nblk NB) per block, O(nblk^2 NB) per pass).  Block j owns
+// digits 64 j .. 64 j + 63 (lane = digit, 256-B row segments); its 16 waves take
+// consecutive row groups of kRsScanRows, prefix in place, carry across chunks.
+constexpr int kRsScanWaves = 16, kRsScanRows = 8;
+__global__ __launch_bounds__(64 * kRsScanWaves) void k_rs_scan(uint32_t *__restrict__ hist, int nblk, int NB,
+                                                              uint32_t *__restrict__ tot) {
+    __shared__ uint32_t ws[kRsScanWaves][64];
+    const int lane = lane_id(), w = (int)threadIdx.x >> 6;
+    const int d = (int)blockIdx.x * 64 + lane;
+    uint32_t carry = 0;
+    for (int c0 = 0; c0 < nblk; c0 += kRsScanWaves * kRsScanRows) {
+        const int r0 = c0 + w * kRsScanRows;
+        uint32_t v[kRsScanRows], s = 0;
+#pragma unroll
+        for (int j = 0; j < kRsScanRows; ++j) {
+            v[j] = hist[(size_t)min(r0 + j, nblk - 1) * NB + d];
+            v[j] = r0 + j < nblk ? v[j] : 0u;
+            s += v[j];
+        }
+        ws[w][lane] = s;
+        __syncthreads();
+        uint32_t ex = carry, all = 0;
+#pragma unroll
+        for (int q = 0; q < kRsScanWaves; ++q) {
+            const uint32_t x = ws[q][lane];
+            ex += q < w ? x : 0u;
+            all += x;
+        }
+#pragma unroll
+        for (int j = 0; j < kRsScanRows; ++j) {
+            if (r0 + j < nblk) hist[(size_t)(r0 + j) * NB + d] = ex;
+            ex += v[j];
+        }
+        carry += all;
+        __syncthreads();  // ws reused by the next chunk
+    }
+    if (w == 0) tot[d] = carry;
+}
+
+// scanned: hist holds column prefixes (k_rs_scan) and tot the digit totals
 template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                     uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int n,
                                                     int shift, int db, const uint32_t *__restrict__ hist, int nblk,
-                                                    int identity_vals) {
+                                                    int identity_vals, const uint32_t *__restrict__ scanned) {
     constexpr int DPT = NB / kBS;       // digits per thread
     constexpr int CH = 64 / DPT;        // blocks per batch of 64 loads in flight
     __shared__ uint32_t base[NB];
@@ -374,7 +426,14 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
         uint32_t tot[DPT], pre[DPT];
 #pragma unroll
         for (int k = 0; k < DPT; ++k) tot[k] = pre[k] = 0;
-        for (int j0 = 0; j0 < nblk; j0 += CH) {
+        if (scanned) {
+#pragma unroll
+            for (int k = 0; k < DPT; ++k) {
+                tot[k] = scanned[k * kBS + t];
+                pre[k] = hist[(size_t)blockIdx.x * NB + k * kBS + t];
+            }
+        }
+        for (int j0 = 0; !scanned && j0 < nblk; j0 += CH) {
             uint32_t v[DPT][CH];
 #pragma unroll
             for (int k = 0; k < DPT; ++k)
@@ -1310,6 +1369,154 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     STAMP(a, SO, 15);
 }
 
+// ------------------------------------------------------------ k_plan2 (large grids, R <= 128)
+// k_plan for k_emit2 when k_scan's queue blocks also added their counts into
+// group rows (<= 64 groups of 2^gshift blocks): one workgroup per group reads
+// the group rows (totals A(r), the prefix of the earlier groups, max c, orphan
+// and eviction totals), finds the fill level L as k_emit2 does, and scans the
+// rows of its own group for rounds r <= L + 1 only -- the rounds k_emit2 reads
+// (a streaming tick: 2 of 64 columns) -- instead of k_plan's one workgroup per
+// round walking a column of every block.  Two more workgroups scan the orphan /
+// eviction tile counts.  Group 0 publishes the totals (A, P).
+constexpr int kGrpLd = 4;     // group / block row loads per thread per batch (k_plan2, k_emit2)
+constexpr int kP2Rows = kBS;  // rows per pass of a group's scan (one per thread)
+__global__ __launch_bounds__(kBS) void k_plan2(TickArgs a) {
+    __shared__ unsigned long long l4[kWaves];
+    __shared__ uint32_t gpre[kBS], gtot[kBS];
+    __shared__ uint32_t gp_r[kRFused];           // prefix of the earlier groups, round r
+    __shared__ uint32_t red[kWaves][4];
+    __shared__ uint32_t wtot[kWaves][4];
+    __shared__ int nr_s;
+    const int bid = blockIdx.x;
+    const int ng = a.ngrp;
+    if (bid >= ng) {
+        const bool f = bid == ng;
+        const unsigned long long tot =
+            f ? run_excl_scan(a.fcnt, 1, a.nbf, a.fpre, 1, l4) : run_excl_scan(a.wcnt, 1, a.nbw, a.wpre, 1, l4);
+        (void)tot;
+        return;
+    }
+    const int g = bid, R = a.R, gs = a.gstride;
+    const int lane = lane_id(), w = wave_id();
+    // ---- group rows: thread t sums round r = t mod R over parts p = t / R
+    {
+        const int P = kBS / R, r = (int)threadIdx.x & (R - 1), p = (int)threadIdx.x / R;
+        uint32_t pre = 0, tot = 0;
+        for (int j0 = 0; j0 * P < ng; j0 += kGrpLd) {
+            uint32_t v[kGrpLd];
+#pragma unroll
+            for (int j = 0; j < kGrpLd; ++j) v[j] = a.grp[min(p + P * (j0 + j), ng - 1) * gs + r];
+#pragma unroll
+            for (int j = 0; j < kGrpLd; ++j) {
+                const int gg = p + P * (j0 + j);
+                tot += gg < ng ? v[j] : 0u;
+                pre += gg < g ? v[j] : 0u;
+            }
+        }
+        gpre[threadIdx.x] = pre;
+        gtot[threadIdx.x] = tot;
+        // max c, orphans, evictions: columns R .. R + 2 (ng <= 64: wave 0 holds them)
+        const int gi = min((int)threadIdx.x, ng - 1) * gs + R;
+        const bool gin = (int)threadIdx.x < ng;
+        const uint32_t mg = gin ? a.grp[gi] : 0u, og = gin ? a.grp[gi + 1] : 0u, eg = gin ? a.grp[gi + 2] : 0u;
+        uint32_t fo = og, wo = eg;
+        if (!FAASBAL_GRP_OW) {  // A/B builds without the orphan / eviction atomics
+            fo = wo = 0;
+            for (int i = threadIdx.x; i < a.nbf; i += kBS) fo += a.fcnt[i];
+            for (int i = threadIdx.x; i < a.nbw; i += kBS) wo += a.wcnt[i];
+        }
+        const uint32_t mo = wave_max_u32(mg);
+        fo = wave_sum_u32(fo);
+        wo = wave_sum_u32(wo);
+        if (lane == 0) {
+            red[w][0] = fo;
+            red[w][1] = wo;
+            red[w][3] = mo;
+        }
+        lds_barrier();
+    }
+    const int64_t O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    const int64_t nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    const int maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
+    const int rlim = maxc < R ? maxc : R;
+    if (w == 0) {
+        // per round r (lane i of chunk k: r = 64 k + i): A(r), the earlier groups' prefix,
+        // S(r) and the fill level L -- k_emit2's computation
+        const int P = kBS / R;
+        int64_t carry = 0, S1v[2];
+        uint32_t Av[2];
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = 64 * k + lane;
+            uint32_t sp = 0, st_ = 0;
+            if (r < R)
+                for (int q = 0; q < P; ++q) {
+                    sp += gpre[q * R + r];
+                    st_ += gtot[q * R + r];
+                }
+            if (r < R) gp_r[r] = sp;
+            Av[k] = st_;
+            const uint32_t v = r < rlim ? st_ : 0u;
+            const uint32_t incl = wave_incl_scan_u32(v);
+            S1v[k] = carry + (int64_t)incl;
+            carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        const int64_t cap = maxc > R ? INT64_MAX : carry;
+        const int64_t N = (a.redist ? O : 0) + a.T;
+        const int64_t N_eff = N < cap ? N : cap;
+        int L = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) L += __popcll(__ballot(64 * k + lane < rlim && S1v[k] <= N_eff));
+        if (lane == 0) nr_s = min(L + 2, R);
+        if (g == 0) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k)
+                if (64 * k + lane < R) a.A[64 * k + lane] = (int64_t)(64 * k + lane < rlim ? Av[k] : 0u);
+            if (lane == 0) {
+                a.P->O = O;
+                a.P->O_local = O;
+                a.P->n_evicted = nev;
+                a.P->cap_total = cap;
+                a.P->maxc = maxc;
+            }
+        }
+    }
+    lds_barrier();
+    const int nr = nr_s;
+    // ---- this group's rows, rounds r < nr: prefix = earlier groups + earlier rows
+    const int gsz = 1 << a.gshift, b0 = g * gsz, b1 = min(b0 + gsz, a.nbq);
+    for (int r0 = 0; r0 < nr; r0 += 4) {
+        uint32_t carry4[4] = {0u, 0u, 0u, 0u};
+        for (int c0 = b0; c0 < b1; c0 += kP2Rows) {
+            const int b = c0 + (int)threadIdx.x;
+            const int bc = min(b, b1 - 1);
+            uint32_t v[4], x[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) v[u] = a.qcnt[(size_t)bc * R + min(r0 + u, R - 1)];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                v[u] = (b < b1 && r0 + u < nr) ? v[u] : 0u;
+                x[u] = wave_incl_scan_u32(v[u]);
+                if (lane == 63) wtot[w][u] = x[u];
+            }
+            lds_barrier();
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                uint32_t before = carry4[u], all = 0;
+#pragma unroll
+                for (int q = 0; q < kWaves; ++q) {
+                    before += q < w ? wtot[q][u] : 0u;
+                    all += wtot[q][u];
+                }
+                if (b < b1 && r0 + u < nr)
+                    a.qpre[(size_t)b * R + r0 + u] = (int64_t)gp_r[r0 + u] + (int64_t)(before + x[u] - v[u]);
+                carry4[u] += all;
+            }
+            lds_barrier();  // wtot reused
+        }
+    }
+}
+
 // Deque mode: the end of a token's tick.  Tokens of one worker share its count
 // (atomic), survivors carry their rank from before the round-L split plus the
 // part they sat in; per slot, x_w = highest rank served in round L and K_L =
@@ -1579,7 +1786,6 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
 // i) from the round prefix plus the earlier segments' counts that k_scan stored
 // per 64-position segment, and the emission.  F / W roles as k_emit's.
 // NCH: 64-round chunks kept per lane (rounds 0 .. L+1): 1 for R = 32, 3 up to R = 128.
-constexpr int kGrpLd = 4;   // group / block row loads per thread per batch
 
 template <int NCH, typename T>
 __device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
@@ -1603,10 +1809,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const int SO = a.nbw + a.nbf + a.nbq + (a.slots_in_scan ? a.nbw : 0);
     STAMP(a, SO, 0);
     const int lane = lane_id(), w = wave_id();
-    if constexpr (!PLAN) {
-        // the other parity's group rows, for the next launch's k_scan atomics
-        for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
-    }
+    // the other parity's group rows, for the next launch's k_scan atomics
+    for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
     // grid: queue blocks then compaction blocks, or (a.cfirst) compaction first
     const int nbf4 = (a.nbf + 3) >> 2, nbw4 = (a.nbw + 3) >> 2;
     const int qb0 = a.cfirst ? nbf4 + nbw4 : 0;  // first queue block
@@ -1639,6 +1843,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         uint32_t fo = 0, wo = 0, mo = 0;
         uint32_t prev[NCH], totv[NCH];  // lane i of chunk k, round 64 k + i: this block's prefix, A(r)
         if constexpr (PLAN) {
+            STAMPW(a, SO, 5);
             // this block's prefix and the total of every round, scanned by k_plan
             if ((int)threadIdx.x < R) {
                 pre_c[threadIdx.x] = (uint32_t)a.qpre[(size_t)b * R + threadIdx.x];
@@ -1652,6 +1857,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             for (int k = 0; k < NCH; ++k)
 #pragma unroll
                 for (int q = 0; q < kWaves - 1; ++q) segc[k] += (q < w && 64 * k + lane < R) ? sv[k][q] : 0u;
+            STAMPW(a, SO, 6);
             lds_barrier();
 #pragma unroll
             for (int k = 0; k < NCH; ++k) {
@@ -2180,8 +2386,14 @@ static void rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, ui
                     Stream s) {
     hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, kin, n, shift, db, hist, nblk,
                           zero0, zero1);
+    const uint32_t *tot = nullptr;
+    if (nblk > kRsScanMin) {
+        uint32_t *t = hist + (size_t)nblk * NB;
+        hipLaunchKernelGGL(k_rs_scan, dim3(NB / 64), dim3(64 * kRsScanWaves), 0, s.s, hist, nblk, NB, t);
+        tot = t;
+    }
     hipExtLaunchKernelGGL(k_rs_scatter<NB>, dim3(nblk), dim3(kBS), 0, s.s, s.e0, s.e1, 0, kin, vin, kout, vout, n,
-                          shift, db, hist, nblk, identity_vals);
+                          shift, db, hist, nblk, identity_vals, tot);
 }
 void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
                     int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
@@ -2222,7 +2434,10 @@ void launch_logscan(const TickArgs &a, int grid, Stream st) {
     hipExtLaunchKernelGGL(k_logscan, dim3(grid), dim3(kLsBS), lds, st.s, st.e0, st.e1, 0, a);
 }
 void launch_plan(const TickArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    if (a.grp_on)
+        hipExtLaunchKernelGGL(k_plan2, dim3(a.ngrp + 2), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    else
+        hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_emit(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);

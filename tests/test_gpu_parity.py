@@ -23,11 +23,11 @@ def _state(scen):
                 queue=scen["init_queue"], log=scen["init_log"])
 
 
-def _pair(st, log_cap, max_events=4096):
+def _pair(st, log_cap, max_events=4096, purge_mode=1):
     W = len(st["reg"])
     g = GpuBalancer(W, log_cap, max_events=max_events)
     g.load(st)
-    o = Oracle(W, log_cap)
+    o = Oracle(W, log_cap, purge_mode=purge_mode)
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
     return g, o
 
@@ -247,6 +247,23 @@ def test_golden_plan_path(force_plan):
 
 
 @pytest.fixture
+def column_plan(monkeypatch):
+    """The 3-launch path with k_plan's per-round column scans instead of k_plan2's
+    group rows (FAASBAL_GPLAN=0)."""
+    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "1")
+    monkeypatch.setenv("FAASBAL_GPLAN", "0")
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_multitick_column_plan(column_plan, seed):
+    test_random_multitick_vs_oracle(seed + 40)
+
+
+def test_config3_column_plan(column_plan):
+    test_config3_full_size()
+
+
+@pytest.fixture
 def force_chunked_emit(monkeypatch):
     """The 3-launch path with the chunked k_emit (used when R > 128) instead of
     k_emit2 after k_plan."""
@@ -388,10 +405,10 @@ def test_launch_staged_needs_stage():
         g.launch_staged(10.0, 100)
 
 
-def _sort_tick(W, E, hot_frac, seed):
+def _sort_tick(W, E, hot_frac, seed, purge_mode=1):
     """One tick of E messages (kinds mixed, clocks ascending) on a W-slot table,
     hot_frac of them on five hot slots; GPU vs oracle.  The oracle purges after
-    every message (O(W) each), so E * W stays around 1e9."""
+    every message (purge_mode 1: O(W) each, so E * W stays around 1e9; 2: heap)."""
     rng = np.random.default_rng(seed)
     st = synth.zipf_state(W=W, seed=seed % 7, dead_frac=0.02)
     hot = rng.choice(W, size=5, replace=False)
@@ -401,7 +418,7 @@ def _sort_tick(W, E, hot_frac, seed):
     val = rng.integers(0, 4, E).astype(np.int32)
     now = 1000.0  # zipf_state's clock
     ts = np.sort(now - rng.random(E)).astype(np.float64)
-    g, o = _pair(st, 2 * len(st["log"]) + 100_000, max_events=E)
+    g, o = _pair(st, 2 * len(st["log"]) + 100_000, max_events=E, purge_mode=purge_mode)
     args = (now, 10.0, kind, slot, val, ts, np.full(E, -1, np.int64), 20_000)
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
@@ -422,3 +439,13 @@ def test_event_sort_stable_on_repeated_slots(W, E):
     """90 % of the messages on five slots (equal-key runs across sort tiles): the
     per-slot arrival order the sort must keep decides every register / result."""
     _sort_tick(W, E, 0.9, W)
+
+
+@pytest.mark.parametrize("W,E,wide", [(1 << 20, 300_000, "1"), ((1 << 17) + 5, 1_200_000, "1"),
+                                      ((1 << 17) + 5, 1_200_000, "0"), (1 << 20, 2_000_000, "1")])
+def test_event_sort_large_batches(monkeypatch, W, E, wide):
+    """Batches of more than kRsScanMin sort tiles (E > 128 K): the column prefixes
+    of the [tile][digit] counts come from their own launch (k_rs_scan) before each
+    scatter; identical to the oracle (heap purge) up to 2 M messages in one tick."""
+    monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
+    _sort_tick(W, E, 0.3, W + E, purge_mode=2)

@@ -25,7 +25,12 @@ def main():
     ap.add_argument("--workers", type=int, default=65536)
     ap.add_argument("--tasks", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--stream", action="store_true", help="committed configs[4] ticks with messages")
+    ap.add_argument("--hb-frac", type=float, default=0.01)
+    ap.add_argument("--dump", default="", help="stream: save the raw stamp rows (npz)")
     args = ap.parse_args()
+    if args.stream:
+        return stream_main(args)
     st = synth.zipf_state(W=args.workers, seed=0)
     W, T = args.workers, args.tasks
     env = os.environ.get("FAASBAL_SPLIT_SLOTS", "-1")
@@ -44,7 +49,46 @@ def main():
         g.wait()
         d = g.debug_read()[: 4 * G1 * 16].reshape(4 * G1, 16).astype(np.int64)
         acc.append(d.copy())
-    d = np.stack(acc)  # reps x rows x 16
+    report(np.stack(acc), nbw, nbf, nbq, split, fsep)
+
+
+def stream_main(args):
+    """configs[4] ticks (bench.py --workload stream): staged messages, committed
+    ticks; the grid of each tick from its queue / log lengths before the launch."""
+    W, T = args.workers, 65536
+    st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
+    n = 5 + args.reps
+    ticks = synth.stream_ticks(st, n_ticks=n, seed=2, tasks_per_tick=T, results_per_tick=T, hb_frac=args.hb_frac)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g = GpuBalancer(W, len(st["log"]) + (n + 2) * 2 * T, max_events=E, lib_path=STAMPS_SO)
+    g.load(st)
+    carried = 0
+    groups = {}
+    for i, tk in enumerate(ticks):
+        s = g.read_state(with_log=False)
+        Qn, head = len(s["queue"]), int(s["head"])
+        Et = len(tk["ev_kind"])
+        nbw, nbf, nbq = -(-W // 256), -(-head // 2048), max(1, -(-(Qn + 2 * Et) // 256))
+        N = carried + tk["n_new"]
+        g.tick(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n_pending=N,
+               commit=False)
+        r = g.last
+        G1 = nbw + nbf + nbq
+        if i >= 5:
+            d = g.debug_read()[: (3 * G1 + 512 + 131) * 16].reshape(-1, 16).astype(np.int64)
+            groups.setdefault((nbw, nbf, nbq), []).append(d.copy())
+        g.commit()
+        carried = N + int(r["n_orphans"]) - int(r["n_assigned"])
+    (nbw, nbf, nbq), acc = max(groups.items(), key=lambda kv: len(kv[1]))
+    print("stream ticks with grid nbw %d nbf %d nbq %d: %d of %d" % (nbw, nbf, nbq, len(acc), args.reps))
+    if args.dump:
+        np.savez_compressed(args.dump, d=np.stack(acc), grid=np.array([nbw, nbf, nbq]))
+    report(np.stack(acc), nbw, nbf, nbq, False, True)
+
+
+def report(d, nbw, nbf, nbq, split, fsep):
+    """d: reps x rows x 16 stamps."""
+    G1 = nbw + nbf + nbq
     S = nbw  # k_scan rows start here
     E0 = G1 if split else G1 + nbw  # k_emit rows start here
     if fsep:
