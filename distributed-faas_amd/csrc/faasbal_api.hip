@@ -109,6 +109,7 @@ struct fb_ctx {
     uint32_t tick = 1;
     // per-tick sparse post-message records
     uint32_t *touched = nullptr;
+    uint32_t *tbits = nullptr;   // one GPU, heartbeat loop: touched bitmap (k_scan's queue role)
     uint8_t *post_reg = nullptr, *post_flags = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
     int32_t *post_free = nullptr;
@@ -397,7 +398,8 @@ int enqueue_tick(fb_ctx *c) {
             // pass 0 also clears the one-GPU front / back lists (sharded: zeroed with the exchange buffer)
             const bool z = ps == 0 && !c->shard;
             launch_rs_pass(kin, vin, kout, vout, E, db * ps, db, c->rs_hist, nb, z ? front : nullptr,
-                           z ? back : nullptr, ps == 0 ? 1 : 0, t.first(), t.last());
+                           z ? back : nullptr, z ? c->tbits : nullptr, z && c->tbits ? (int)cdiv(W, 32) : 0,
+                           ps == 0 ? 1 : 0, t.first(), t.last());
             kin = kout;
             vin = vout;
         }
@@ -435,6 +437,7 @@ int enqueue_tick(fb_ctx *c) {
         a.post_epoch = c->post_epoch;
         a.post_flags = c->post_flags;
         a.touched = c->touched;
+        a.tbits = c->tbits;
         a.front_list = front;
         a.back_list = back;
         Timer t(c, "ev_apply");
@@ -521,6 +524,7 @@ int enqueue_tick(fb_ctx *c) {
     a.qfree_in = c->qfree[cur];
     a.qhb_in = c->qhb[cur];
     a.touched = c->touched;
+    a.tbits = c->tbits;
     a.post_reg = c->post_reg;
     a.post_flags = c->post_flags;
     a.post_hb = c->post_hb;
@@ -694,6 +698,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->hb, W);
     ap.add(&c->epoch, W);
     ap.add(&c->touched, W);
+    if (!shard && !c->deque) ap.add(&c->tbits, (W + 31) / 32);
     ap.add(&c->post_reg, W);
     ap.add(&c->post_flags, W);
     ap.add(&c->st, W);
@@ -800,6 +805,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         c->ev_seq = c->evq[0];
     }
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
+    if (!rc && c->tbits && hipMemset(c->tbits, 0, (W + 31) / 32 * 4) != hipSuccess) rc = FB_EHIP;
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;

@@ -106,6 +106,7 @@ struct EvArgs {
     uint32_t *post_epoch;
     uint8_t *post_flags;
     uint32_t *touched;
+    uint32_t *tbits;   // one GPU: bit s = slot s got a message this tick (cleared by the first sort pass)
     int32_t *front_list, *back_list;  // slot + 1 (0 = empty), zeroed before the tick
 };
 
@@ -150,6 +151,7 @@ struct TickArgs {
     const double *qhb_in;
     // this tick's message results
     const uint32_t *touched;
+    const uint32_t *tbits;  // one GPU, message ticks: touched as a bitmap (L2-resident: 128 KB per 1M slots)
     const uint8_t *post_reg, *post_flags;
     const double *post_hb;
     const int32_t *post_free;
@@ -226,9 +228,10 @@ struct Stream {
 // One LSD pass (histogram + scatter launches) over `db`-bit digits at `shift`;
 // hist holds (1 << db rounded up to 256 / 1024 / 2048) x (nblk + 1) counts (the
 // extra row: digit totals when nblk > kRsScanMin).
+// zero0 / zero1 (n words each) and zbits (zwords) are cleared by the histogram launch.
 void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
-                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
-                    Stream s);
+                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, uint32_t *zbits, int zwords,
+                    int identity_vals, Stream h, Stream s);
 #ifndef FAASBAL_RS_SCAN_MIN
 #define FAASBAL_RS_SCAN_MIN 64
 #endif

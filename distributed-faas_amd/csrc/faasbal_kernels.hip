@@ -95,6 +95,9 @@ __device__ __forceinline__ void wt_store(T *p, T v) {
 
 // Fused ticks: orphan / eviction totals through atomics into the group rows (1), or
 // read back by every emit queue block from the per-block counts (0).
+#ifndef FAASBAL_EXP
+#define FAASBAL_EXP 0  // timing experiments only (results invalid when set)
+#endif
 #ifndef FAASBAL_GRP_OW
 #define FAASBAL_GRP_OW 1
 #endif
@@ -333,13 +336,14 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift, int db,
                                                  uint32_t *__restrict__ hist, int nblk, int32_t *__restrict__ zero0,
-                                                 int32_t *__restrict__ zero1) {
+                                                 int32_t *__restrict__ zero1, uint32_t *__restrict__ zbits, int zwords) {
     constexpr int DPT = NB / kBS;
     __shared__ uint32_t cnt[NB];
 #pragma unroll
     for (int k = 0; k < DPT; ++k) cnt[k * kBS + threadIdx.x] = 0;
     __syncthreads();
     const int base = blockIdx.x * kRsTile;
+    for (int i = blockIdx.x * kBS + (int)threadIdx.x; i < zwords; i += nblk * kBS) zbits[i] = 0;
     if (zero0) {
 #pragma unroll
         for (int j = 0; j < kRsItems; ++j) {
@@ -686,6 +690,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     a.post_epoch[s] = epoch;
     a.post_flags[s] = (uint8_t)(died_start | (qstat << 1));
     a.touched[s] = a.tick;
+    if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));
     if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)gs + 1;
     if (qstat == kQsBack) a.back_list[qidx] = (int32_t)gs + 1;
 }
@@ -694,7 +699,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 // ------------------------------------------------------------ slot state
 // Current record of slot s after this tick's messages (touched) or as committed.
 struct Cur {
-    int reg0, reg, flags;
+    int reg0, reg, flags, q0;  // q0: in the committed LRU queue
     bool t;
     double hb;
     int32_t fr;
@@ -704,7 +709,9 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
     Cur c;
     c.reg0 = a.reg[s];
     const double hb0 = a.hb[s];
-    const int32_t fr0 = a.free_in[s].x;
+    const int2 fq0 = a.free_in[s];
+    const int32_t fr0 = fq0.x;
+    c.q0 = fq0.y;
     if (a.E > 0) {
         // message tick: committed and post-message records loaded together and
         // selected afterwards (a load behind the touched test would wait for it)
@@ -860,7 +867,10 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
         evicted = !a.deque && (c.reg0 || c.t) && !alive;  // start() never deletes a record
         a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
-        a.free_out[s] = make_int2(alive ? c.fr : INT32_MIN, 0);
+        // queued: a live position of this tick's LRU queue (committed and kept, or a
+        // front / back insertion) -- k_emit2 then rewrites only the slots it serves
+        const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
+        a.free_out[s] = make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
         if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
             a.tokcnt_out[s] = 0;
             a.xw_out[s] = 0;
@@ -1062,14 +1072,31 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         int32_t raw = INT32_MIN;  // INT32_MIN: no live record (or not mine)
         double hbq = 0.0;
         const int64_t q = pos - a.E;  // committed queue position (fronts come first)
+        const bool inq = q >= 0 && q < a.Qn;
         const int64_t qc = q < 0 ? 0 : (q < a.Qn ? q : (a.Qn > 0 ? a.Qn - 1 : 0));
-        if (a.qaos && q >= 0 && q < a.Qn && (a.E == 0 || a.touched[a.queue_in[qc]] != a.tick)) {
-            // a committed entry whose slot got no message this tick: its record rides
-            // along by position (queued slots are registered) -- one coalesced pass
-            // plus one 4-byte stamp gather instead of the slot's record gathers
-            hbq = a.qhb_in[q];
-            const int32_t fq = a.qfree_in[q];
-            raw = ((a.now - hbq) > a.tte) ? INT32_MIN : fq;
+        if (a.qaos && inq) {
+            // a committed entry: slot, free count and heartbeat ride along by position
+            // (queued slots are registered) -- three coalesced loads issued together,
+            // then one 4-byte stamp gather; only slots that got a message this tick
+            // gather their post-message record
+            const int sq = a.queue_in[qc];
+            const double hq = a.qhb_in[qc];
+            const int32_t fq = a.qfree_in[qc];
+            // touched: the bitmap word (L2-resident) when there is one, else the slot's stamp
+            const bool tq = a.E > 0 && (a.tbits ? ((a.tbits[sq >> 5] >> (sq & 31)) & 1u) != 0u
+                                                : a.touched[sq] == a.tick);
+            if (!tq) {
+                hbq = hq;
+                raw = ((a.now - hq) > a.tte) ? INT32_MIN : fq;
+            } else {
+                const uint8_t pr = a.post_reg[sq], pf = a.post_flags[sq];
+                const double ph = a.post_hb[sq];
+                const int32_t pfr = a.post_free[sq];
+                hbq = ph;
+                raw = (pr && !((a.now - ph) > a.tte)) ? pfr : INT32_MIN;
+                // moved to the front, re-appended or removed by this tick's messages
+                if (((pf >> 1) & 3) != kQsKeep) raw = INT32_MIN;
+            }
         } else {
             s = lq_slot(a, pos);
             ls = s >= 0 ? own_slot(a, s) : -1;
@@ -1085,11 +1112,11 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                     hbq = (a.E > 0 && a.touched[ls] == a.tick) ? h1 : h0;
                 }
             }
+            // an old queue entry moved to the front, re-appended or removed by this tick's messages
+            if (raw != INT32_MIN && a.E > 0 && inq && a.touched[ls] == a.tick &&
+                ((a.post_flags[ls] >> 1) & 3) != kQsKeep)
+                raw = INT32_MIN;
         }
-        // an old queue entry moved to the front, re-appended or removed by this tick's messages
-        if (raw != INT32_MIN && a.E > 0 && pos >= a.E && pos < a.E + a.Qn && a.touched[ls] == a.tick &&
-            ((a.post_flags[ls] >> 1) & 3) != kQsKeep)
-            raw = INT32_MIN;
         if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
         a.c_arr[pos] = raw;
         if (!a.shard) a.c_hb[pos] = hbq;
@@ -1845,6 +1872,13 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         if constexpr (PLAN) {
             STAMPW(a, SO, 5);
             // this block's prefix and the total of every round, scanned by k_plan
+#if FAASBAL_EXP == 1
+            if ((int)threadIdx.x < R) {
+                pre_c[threadIdx.x] = (uint32_t)b * 256u;
+                tot_f[threadIdx.x] = 1000000u;
+            }
+            O = 0; nev = 0; cap = 1ll << 40; maxc = R;
+#else
             if ((int)threadIdx.x < R) {
                 pre_c[threadIdx.x] = (uint32_t)a.qpre[(size_t)b * R + threadIdx.x];
                 tot_f[threadIdx.x] = (uint32_t)a.A[threadIdx.x];
@@ -1853,6 +1887,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             nev = a.P->n_evicted;
             cap = a.P->cap_total;
             maxc = a.P->maxc;
+#endif
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
 #pragma unroll
@@ -2082,8 +2117,10 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 STAMP(a, SO, 15);
                 return;
             }
-            // the worker's next {free, queued}: one 8-byte store
-            wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
+            // the worker's next {free, queued}: one 8-byte store, only for the workers served
+            // this tick -- the slot role already wrote {free, 1} for every queued one (a
+            // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
+            if (n_q != 0 || np < 0) wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
             if (np >= 0) {
                 wt_store(a.queue_out + np, s);
                 wt_store(a.qfree_out + np, raw - (int32_t)n_q);
@@ -2382,10 +2419,10 @@ namespace fb {
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 template <int NB>
 static void rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
-                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
-                    Stream s) {
+                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, uint32_t *zbits, int zwords,
+                    int identity_vals, Stream h, Stream s) {
     hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, kin, n, shift, db, hist, nblk,
-                          zero0, zero1);
+                          zero0, zero1, zbits, zwords);
     const uint32_t *tot = nullptr;
     if (nblk > kRsScanMin) {
         uint32_t *t = hist + (size_t)nblk * NB;
@@ -2396,14 +2433,16 @@ static void rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, ui
                           shift, db, hist, nblk, identity_vals, tot);
 }
 void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
-                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, int identity_vals, Stream h,
-                    Stream s) {
+                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, uint32_t *zbits, int zwords,
+                    int identity_vals, Stream h, Stream s) {
     if (db <= 8)
-        rs_pass<256>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, identity_vals, h, s);
+        rs_pass<256>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, zbits, zwords, identity_vals, h, s);
     else if (db <= 10)
-        rs_pass<1024>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, identity_vals, h, s);
+        rs_pass<1024>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, zbits, zwords, identity_vals, h,
+                      s);
     else
-        rs_pass<2048>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, identity_vals, h, s);
+        rs_pass<2048>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, zbits, zwords, identity_vals, h,
+                      s);
 }
 void launch_ev_apply(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -7,6 +7,7 @@ from __future__ import annotations
 
 import ctypes as C
 import os
+import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfaasbal.so")
@@ -68,11 +69,14 @@ def load(path=None):
     # torch bundles its own HIP runtime under the same soname as /opt/rocm's.
     # Whichever loads first serves the whole process; when this library came
     # first, a later `import torch` (faasbal.sharded's exchange buffers) found no
-    # GPU on the box.  So torch, when installed, is imported before the library.
-    try:
-        import torch  # noqa: F401
-    except ImportError:
-        pass
+    # GPU on the box.  Processes that use torch import it first (faasbal.sharded,
+    # bench.py's ranks, tests/conftest.py) or set FAASBAL_TORCH=1; the one-GPU
+    # dispatcher and gateway never pay torch's import and bind /opt/rocm's runtime.
+    if "torch" not in sys.modules and os.environ.get("FAASBAL_TORCH") == "1":
+        try:
+            import torch  # noqa: F401
+        except Exception:  # a torch that fails to load must not stop the library
+            pass
     lib = C.CDLL(path)
     i32, i64, dbl = C.c_int32, C.c_int64, C.c_double
     proto = {

@@ -44,7 +44,7 @@ import time
 import numpy as np
 
 from . import codec
-from ._lib import FB_EVS_RECONNECT, FaasbalError
+from ._lib import FB_ENOSPC, FB_EVS_RECONNECT, FaasbalError
 from .balancer import GpuBalancer
 
 EV_REGISTER, EV_RECONNECT, EV_HEARTBEAT, EV_RESULT, EV_OTHER = 0, 1, 2, 3, 4
@@ -255,8 +255,17 @@ class GpuPushDispatcher:
         return keep, unknown
 
     def _run(self, msgs):
-        # room for every dispatch this tick can make (orphans + pending) before sequence numbers are taken
-        if self.head + len(self.pending) + len(self.inflight) > self.max_inflight:
+        # room for every dispatch this tick can make (orphans + pending) before sequence
+        # numbers are taken.  Compaction reclaims the finished entries (head - in-flight);
+        # when a backlog keeps the worst case above the log even after it, compacting
+        # every tick would cost a full log round trip per tick while the dispatches are
+        # bounded by the workers' free capacity -- so it runs then only when it reclaims a
+        # quarter of the log, and the tick itself decides (a real overflow, FB_ENOSPC,
+        # compacts and reruns the tick below).
+        need = len(self.pending) + len(self.inflight)
+        garbage = self.head - len(self.inflight)
+        if self.head + need > self.max_inflight and garbage > 0 and (
+                self.head - garbage + need <= self.max_inflight or 4 * garbage >= self.max_inflight):
             self.compact_log()
         now = self._stamp()
         arrived = msgs
@@ -282,8 +291,16 @@ class GpuPushDispatcher:
                 val[i] = v
             elif k == EV_RESULT:
                 seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
-        out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
-                                 n_pending=len(self.pending))
+        try:
+            out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
+                                     n_pending=len(self.pending))
+        except FaasbalError as e:
+            # in-flight log full: the launch committed nothing, so compact and rerun once
+            if e.code != FB_ENOSPC or self.head == len(self.inflight):
+                raise
+            self.compact_log()
+            out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
+                                     n_pending=len(self.pending))
         res = out["result"]
         # ---- per-message replies, in arrival order (:356-358, :374-387; start(): :284-288,
         #      where a result from an unknown identity is still HSET before the KeyError)

@@ -7,6 +7,15 @@ for p in (REPO, os.path.join(REPO, "distributed-faas_amd"), os.path.join(REPO, "
         sys.path.insert(0, p)
 
 
+# the suite mixes torch users (sharded groups, gloo ranks) with plain library
+# users in one process: torch's HIP runtime must be the first one loaded
+# (faasbal._lib.load)
+try:
+    import torch  # noqa: F401
+except Exception:
+    pass
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (run with -m gpu)")
     config.addinivalue_line("markers", "slow: larger CPU-side cases")

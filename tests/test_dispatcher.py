@@ -260,6 +260,39 @@ def test_dispatcher_log_compaction_keeps_results(dispatcher_cls):
     assert sum(len(x) for x in runs[0]) > 50
 
 
+def test_backlog_beyond_log_compacts_rarely(dispatcher_cls):
+    """A task backlog far larger than the in-flight log: dispatches are bounded by
+    the workers' free capacity (4 per tick here), so the log is compacted only when
+    that reclaims a quarter of it -- not on every tick -- and the dispatches equal a
+    run with a log large enough never to compact."""
+    runs, comp = [], []
+    for cap in (1 << 16, 64):
+        env = FakeEnv()
+        d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=8, max_events=64, max_inflight=cap,
+                           redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+        env.tasks.extend("b%d" % j for j in range(400))
+        sent, prev = [], []
+        for t in range(40):
+            env.now = 1000.0 + t
+            if t == 0:
+                for w in range(2):
+                    env.inbound.append((wid(w), codec.serialize(
+                        {"type": "register", "data": {"num_processes": 2}}).encode(), env.now))
+            for (dst, m) in prev:
+                if m["type"] == "task":
+                    env.inbound.append((dst, codec.serialize({"type": "result", "data": {
+                        "task_id": m["data"]["task_id"], "status": "COMPLETED", "result": 1}}).encode(), env.now))
+            env.sent.clear()
+            d.tick()
+            prev = list(env.sent)
+            sent.append(prev)
+        runs.append(sent)
+        comp.append(d.compactions)
+    assert runs[0] == runs[1]
+    assert sum(len(x) for x in runs[0]) >= 4 * 39
+    assert comp[0] == 0 and 0 < comp[1] <= 40 // 3, comp
+
+
 def test_purge_workers_evicts_without_dispatching(dispatcher_cls):
     """purge_workers() (task_dispatcher.py:241-249) deletes the expired records and
     sends nothing; the dead worker's in-flight tasks go to the front of the pending
