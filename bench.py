@@ -421,7 +421,8 @@ def main():
         tj = json.load(open(tp))
         if (tj.get("workers"), tj.get("tasks_per_tick"), tj.get("n_gpus")) == (W, T, world) and dom in tj["kernels"]:
             traffic = tj["kernels"][dom]["hbm_bytes"]
-            traffic_src = "profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch)" % tj["tag"]
+            traffic_src = "profiles/%s_pmc.csv, %s_pmc_summary.json (2*FETCH_SIZE + WRITE_SIZE per launch)" % (
+                tj["tag"], tj["tag"])
     line = {
         "metric": "task assignments/sec + % HBM roofline, 1M tasks x 64K workers, 1/2/4/8 GPU",
         "value": value,
@@ -441,8 +442,9 @@ def main():
                                ("configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
                                 "5%% dead -> %d orphans redistributed" % (T, W, O)) if world == 1 else
                                ("configs[2] per GPU, weak: one global tick of %d tasks x %d workers sharded by "
-                                "worker-id range over %d GPUs, exchange all-reduce of %d B per tick (RCCL), "
-                                "%d orphans redistributed" % (T, W, world, kt_x_bytes, O)),
+                                "worker-id range over %d GPUs, exchange all-reduce of %d B per tick (%s), "
+                                "%d orphans redistributed" % (T, W, world, kt_x_bytes,
+                                                              "RCCL" if args.backend == "nccl" else args.backend, O)),
                    "tasks_per_tick": T, "workers": W, "in_flight": F, "queue": Q,
                    "assigned_per_tick": n_assigned, "evicted": n_evicted,
                    "fill_level": int(res["fill_level"]),
