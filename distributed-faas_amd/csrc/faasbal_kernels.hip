@@ -98,6 +98,11 @@ __device__ __forceinline__ void wt_store(T *p, T v) {
 #ifndef FAASBAL_EXP
 #define FAASBAL_EXP 0  // timing experiments only (results invalid when set)
 #endif
+// k_emit2 after k_plan(2) counts the per-segment round counts of its block in LDS (1)
+// or reads the ones k_scan stored (0: 2 x 4.7 MB per streaming tick)
+#ifndef FAASBAL_SEG_LDS
+#define FAASBAL_SEG_LDS 1
+#endif
 #ifndef FAASBAL_GRP_OW
 #define FAASBAL_GRP_OW 1
 #endif
@@ -1213,7 +1218,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 }
                 wc[wave_id()][g * 64 + lane_id()] = cnt;
                 // per 64-position segment (k_emit2 derives its rank bases from these rows)
-                if (a.segw && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
+                if ((a.fused || !FAASBAL_SEG_LDS) && a.segw && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
                     a.segcnt[(size_t)(4 * b + wave_id()) * a.R + r0 + lane_id()] = cnt;
             }
             lds_barrier();
@@ -1855,6 +1860,34 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         // (all three earlier segments loaded unconditionally, clamped, then masked:
         // a loop bounded by the wave id would issue one load and wait per segment)
         uint32_t segc[NCH];
+        // large tables only: on the fused (configs[2]) path the histogram sits on the
+        // critical path between the loads and the barrier (11.13 -> 11.45 us per tick)
+        constexpr bool kSegLds = PLAN && FAASBAL_SEG_LDS;
+        __shared__ uint32_t shist[kWaves][kRFused + 1];
+        __shared__ uint32_t sseg[kWaves][kRFused];
+        if constexpr (kSegLds)
+        {
+            // ... counted here from this block's own c values: per wave a histogram of
+            // min(c, R) in LDS (k_scan's scheme), count(c > r) = 64 - its prefix; summed
+            // over the earlier waves after the block barrier below
+            const int32_t rw = pos < a.Qlog ? raw0 : INT32_MIN;
+            const int cc = rw != INT32_MIN ? (a.deque ? rw : (rw > 1 ? rw : 1)) : 0;
+            uint32_t *h = shist[w];
+            for (int i = lane; i <= R; i += 64) h[i] = 0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            atomicAdd(&h[cc < R ? cc : R], 1u);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            uint32_t carry = 0;
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int r = 64 * k + lane;
+                const uint32_t P = carry + wave_incl_scan_u32(r < R ? h[r] : 0u);
+                if (r < R) sseg[w][r] = 64u - P;
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+            }
+        }
         uint32_t sv[NCH][kWaves - 1];
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {
@@ -1862,7 +1895,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 #pragma unroll
             for (int q = 0; q < kWaves - 1; ++q) {
                 const int r = min(64 * k + lane, R - 1);
-                sv[k][q] = a.segcnt[(size_t)(4 * b + q) * R + r];
+                sv[k][q] = kSegLds ? 0u : a.segcnt[(size_t)(4 * b + q) * R + r];
             }
         }
         int64_t O, nev, cap = 0;
@@ -1977,6 +2010,14 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             }
         }
         STAMP(a, SO, 1);
+#pragma unroll
+        for (int k = 0; k < NCH && kSegLds; ++k) {
+            const int r = min(64 * k + lane, kRFused - 1);
+            uint32_t sc = 0;
+#pragma unroll
+            for (int q = 0; q < kWaves - 1; ++q) sc += (q < w && 64 * k + lane < R) ? sseg[q][r] : 0u;
+            segc[k] = sc;
+        }
         const int rlim = maxc < R ? maxc : R;
         // ---- per wave: S(r) (lane i of chunk k: round 64 k + i), capacity, fill level L
         int64_t Sv[NCH], S1v[NCH];

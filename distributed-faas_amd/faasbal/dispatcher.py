@@ -121,6 +121,18 @@ class GpuPushDispatcher:
         self.ticks = 0
         self.compactions = 0
 
+    @classmethod
+    def subclass_of(cls, base):
+        """This class as a subclass of the reference's ``PushDispatcher``
+        (``task_dispatcher.py:188``), for code that type-checks or extends it:
+        ``GpuPush = GpuPushDispatcher.subclass_of(PushDispatcher)``.  The methods
+        here come first in the MRO, so every method the reference defines --
+        ``bind_socket``, ``send_message``, ``receive_message``, ``query_redis``,
+        ``purge_workers``, ``start``, ``start_heartbeat`` -- is the GPU one, and the
+        reference's ``__init__`` (which binds a socket and opens Redis itself) is
+        never run; anything else the base adds is inherited unchanged."""
+        return type(cls.__name__, (cls, base), {"__doc__": cls.__doc__, "__module__": cls.__module__})
+
     def use_loop(self, mode):
         """Select the balancing loop before the first tick: ``"heartbeat"``
         (``start_heartbeat``, :324-419) or ``"deque"`` (``start``, :251-322).

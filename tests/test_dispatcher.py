@@ -133,6 +133,39 @@ def test_dispatcher_replays_reference(path, dispatcher_cls, pipelines):
         clock=env.clock), pipelines)
 
 
+class _ReferencePushDispatcher:
+    """Stand-in for task_dispatcher.PushDispatcher (:188-419), which imports zmq and
+    redis at module level: the reference's method names, each failing if the
+    subclass ever reaches it, plus one method only the base defines."""
+
+    def __init__(self, *args, **kwargs):
+        raise AssertionError("the reference __init__ must not run")
+
+    def _unreachable(self, *args, **kwargs):
+        raise AssertionError("a reference method was reached")
+
+    bind_socket = send_message = receive_message = query_redis = _unreachable
+    purge_workers = start = start_heartbeat = _unreachable
+
+    def base_only(self):
+        return "inherited"
+
+
+def test_subclass_of_the_reference_class(dispatcher_cls):
+    """GpuPushDispatcher.subclass_of(PushDispatcher): an instance of the
+    reference's class whose reference methods are all the GPU ones; the golden
+    replays pass through it unchanged."""
+    Sub = dispatcher_cls.subclass_of(_ReferencePushDispatcher)
+    for path in (GOLDEN[0], GOLDEN[-1]):
+        z = np.load(path)
+        d = replay_golden(z, lambda sizes, env: Sub(
+            "127.0.0.1", 0, float(z["tte"]), **sizes, redis_client=env, subscriber=env, socket=env, poller=env,
+            clock=env.clock))
+        assert isinstance(d, _ReferencePushDispatcher) and isinstance(d, dispatcher_cls)
+        assert d.base_only() == "inherited"
+        assert isinstance(d.purge_workers(), list)  # the GPU purge, not the base's
+
+
 def golden_sizes(z):
     """Table sizes for replaying golden vector z through a dispatcher."""
     W = int(z["W"])
