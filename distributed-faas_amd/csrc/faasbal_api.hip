@@ -1404,6 +1404,56 @@ int fb_get_event_status(fb_ctx *c, int32_t n, uint8_t *dst) {
     return FB_OK;
 }
 
+namespace {
+// wait for the launched tick, copy the requested outputs, commit
+int finish_tick(fb_ctx *c, int32_t n_events, fb_tick_result *res, uint8_t *ev_status, int32_t *assign,
+                int64_t *orphans, int32_t *evicted) {
+    int rc;
+    fb_tick_result r;
+    if ((rc = fb_tick_wait(c, &r))) return rc;
+    if (ev_status && (rc = fb_get_event_status(c, n_events, ev_status))) return rc;
+    if (assign && (rc = fb_get_assignments(c, 0, r.n_assigned, assign))) return rc;
+    if (orphans && (rc = fb_get_orphans(c, r.n_orphans, orphans))) return rc;
+    if (evicted && (rc = fb_get_evicted(c, r.n_evicted, evicted))) return rc;
+    if (res) *res = r;
+    return fb_tick_commit(c);
+}
+}  // namespace
+
+int fb_apply_events(fb_ctx *c, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+                    const int32_t *val, const double *ts, const int64_t *seq, fb_tick_result *res,
+                    uint8_t *ev_status, int64_t *orphans, int32_t *evicted) {
+    if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "fb_apply_events on a sharded context (use the two-phase tick)");
+    if (n_events < 0 || (n_events && !ts)) return fail(c, FB_EINVAL, "event arrays");
+    if (res) *res = fb_tick_result{};
+    if (!n_events) return FB_OK;
+    // the messages, each after the purge at its own clock, then the purge that follows
+    // the last one (:390) at that clock; nothing dispatched, orphans reported
+    int rc = fb_tick_stage(c, ts[n_events - 1], n_events, kind, slot, val, ts, seq);
+    if (rc) return rc;
+    c->next_purge_only = true;
+    if ((rc = fb_tick_launch_staged(c, tte, 0))) return rc;
+    return finish_tick(c, n_events, res, ev_status, nullptr, orphans, evicted);
+}
+
+int fb_purge(fb_ctx *c, double now, double tte, fb_tick_result *res, int64_t *orphans, int32_t *evicted) {
+    if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "fb_purge on a sharded context (fb_purge_launch + exchange)");
+    int rc = fb_purge_launch(c, now, tte);
+    if (rc) return rc;
+    return finish_tick(c, 0, res, nullptr, nullptr, orphans, evicted);
+}
+
+int fb_assign(fb_ctx *c, double now, double tte, int64_t n_tasks, fb_tick_result *res, int32_t *assign,
+              int64_t *orphans, int32_t *evicted) {
+    if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "fb_assign on a sharded context (use the two-phase tick)");
+    int rc = fb_tick_launch(c, now, tte, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n_tasks);
+    if (rc) return rc;
+    return finish_tick(c, 0, res, nullptr, assign, orphans, evicted);
+}
+
 int fb_tick(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
             const int32_t *val, const double *ts, const int64_t *seq, int64_t n_pending, fb_tick_result *res,
             uint8_t *ev_status, int32_t *assign, int64_t *orphans, int32_t *evicted) {

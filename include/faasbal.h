@@ -149,6 +149,26 @@ int fb_tick(fb_ctx *ctx, double now, double tte, int32_t n_events, const uint8_t
             int64_t n_pending, fb_tick_result *res, uint8_t *ev_status, int32_t *assign,
             int64_t *orphans, int32_t *evicted);
 
+/* Per-operation forms (one-GPU contexts; each is one synchronous tick and commits).
+ *
+ * fb_apply_events: the inbound branches (task_dispatcher.py:343-387) for n messages
+ *   in arrival order, each after the purge at its own clock (:390), then the purge
+ *   after the last message at ts[n-1]; nothing is dispatched.  Records that expired
+ *   are evicted (evicted), their in-flight tasks reported (orphans) for the caller to
+ *   keep pending; ev_status as fb_get_event_status.
+ * fb_purge: purge_workers at `now` (:241-249) = fb_purge_launch + wait + outputs + commit.
+ * fb_assign: the dispatch block (:393-419) for n_tasks pending tasks after the purge at
+ *   `now` (:390); orphans of that purge first (build-defined), then the tasks; assign
+ *   gets res->n_assigned slots (fewer than requested when capacity runs out: the rest
+ *   stay pending, as at :393).
+ * Output arrays may be NULL; sizes as fb_get_* (res->n_*). */
+int fb_apply_events(fb_ctx *ctx, double tte, int32_t n_events, const uint8_t *kind, const int32_t *slot,
+                    const int32_t *val, const double *ts, const int64_t *seq, fb_tick_result *res,
+                    uint8_t *ev_status, int64_t *orphans, int32_t *evicted);
+int fb_purge(fb_ctx *ctx, double now, double tte, fb_tick_result *res, int64_t *orphans, int32_t *evicted);
+int fb_assign(fb_ctx *ctx, double now, double tte, int64_t n_tasks, fb_tick_result *res, int32_t *assign,
+              int64_t *orphans, int32_t *evicted);
+
 int fb_device_view_get(fb_ctx *ctx, fb_device_view *view);
 
 /* Per-kernel device timing with HIP events on the context stream.
