@@ -768,6 +768,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->oA, 128);
     }
     int rc = arena_commit(c, ap);
+    if (!rc && getenv_int("FAASBAL_PRINT_ARENA"))  // diagnostics: placement of the arena
+        fprintf(stderr, "faasbal arena %p, %zu bytes\n", c->arena, c->arena_bytes);
     if (!rc) {
         c->table_cap = tab;
         c->R_cap = 128;
