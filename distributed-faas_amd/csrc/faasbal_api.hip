@@ -121,7 +121,7 @@ struct fb_ctx {
     double *ev_ts = nullptr;
     int64_t *ev_seq = nullptr;
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
-    uint32_t *rs_hist = nullptr;
+    uint32_t *rs_hist[4] = {nullptr, nullptr, nullptr, nullptr};  // per sort pass: [tile][digit] counts
     int32_t *front_list = nullptr, *back_list = nullptr;
     void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
     // device event arrays, double-buffered like the pinned halves: fb_tick_stage copies
@@ -163,6 +163,7 @@ struct fb_ctx {
     int emit_cfirst = 0;  // FAASBAL_EMIT_CFIRST: k_emit2 grid order (A/B knob)
     int rs_wide = 1;       // FAASBAL_RS_WIDE=0: 8-bit sort digits only (A/B knob)
     int gplan = 1;         // FAASBAL_GPLAN=0: large k_emit2 tables through k_plan, not k_plan2 (A/B knob)
+    int rs_fuse = 0;       // FAASBAL_RS_FUSE=1: next-pass histograms from the scatters' atomics (A/B knob)
     int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
     int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
@@ -391,17 +392,43 @@ int enqueue_tick(fb_ctx *c) {
         const bool wide = c->rs_wide && nb <= kRsWideMaxBlocks;
         const int passes = wide ? (bits + 10) / 11 : (bits + 7) / 8;
         const int db = wide ? (bits + passes - 1) / passes : 8;
+        if (passes > 4) return fail(c, FB_ERANGE, "event sort of %d passes", passes);
+        const int NBw = db <= 8 ? 256 : db <= 10 ? 1024 : 2048;
         const uint32_t *kin = (const uint32_t *)c->ev_slot, *vin = nullptr;
         for (int ps = 0; ps < passes; ++ps) {
             Timer t(c, "rs_sort");
-            uint32_t *kout = c->keys[ps & 1], *vout = c->vals[ps & 1];
-            // pass 0 also clears the one-GPU front / back lists (sharded: zeroed with the exchange buffer)
-            const bool z = ps == 0 && !c->shard;
-            launch_rs_pass(kin, vin, kout, vout, E, db * ps, db, c->rs_hist, nb, z ? front : nullptr,
-                           z ? back : nullptr, z ? c->tbits : nullptr, z && c->tbits ? (int)cdiv(W, 32) : 0,
-                           ps == 0 ? 1 : 0, t.first(), t.last());
-            kin = kout;
-            vin = vout;
+            RsPass p{};
+            p.kin = kin;
+            p.vin = vin;
+            p.kout = c->keys[ps & 1];
+            p.vout = c->vals[ps & 1];
+            p.n = E;
+            p.shift = db * ps;
+            p.db = db;
+            p.nblk = nb;
+            // FAASBAL_RS_FUSE=1: each scatter adds the next pass's histogram with one global
+            // atomic per key instead of a histogram launch per pass -- measured slower at
+            // configs[4] (77 K messages: scatter 10.8 -> 14.0 us, the launch saved 4.7 us)
+            const bool fuse = c->rs_fuse != 0;
+            p.hist = c->rs_hist[fuse ? ps : 0];
+            p.hnext = fuse && ps + 1 < passes ? c->rs_hist[ps + 1] : nullptr;
+            p.first = (ps == 0 || !fuse) ? 1 : 0;
+            p.identity_vals = ps == 0 ? 1 : 0;
+            if (ps == 0) {
+                // pass 0 also clears the one-GPU front / back lists (sharded: zeroed with the
+                // exchange buffer), the touched bitmap and the later passes' count tables
+                if (!c->shard) {
+                    p.zero0 = front;
+                    p.zero1 = back;
+                    p.zbits = c->tbits;
+                    p.zwords = c->tbits ? (int)cdiv(W, 32) : 0;
+                }
+                for (int q = 1; q < 4; ++q) p.zhist[q - 1] = fuse && passes > q ? c->rs_hist[q] : nullptr;
+                p.zhwords = fuse && passes > 1 ? nb * NBw : 0;
+            }
+            launch_rs_pass(p, t.first(), t.last());
+            kin = p.kout;
+            vin = p.vout;
         }
         EvArgs a{};
         a.E = E;
@@ -719,9 +746,12 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->keys[i], E);
         ap.add(&c->vals[i], E);
     }
-    // 8-bit passes: 256 x blocks; wide passes (a tick of <= kRsWideMaxBlocks blocks): 2048 x blocks
-    ap.add(&c->rs_hist, std::max((size_t)256 * (cdiv(E, kRsTile) + 1),
-                                 (size_t)2048 * (size_t)(std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks) + 1)));
+    // 8-bit passes: 256 x blocks; wide passes (a tick of <= kRsWideMaxBlocks blocks): 2048 x blocks;
+    // one table per pass only with FAASBAL_RS_FUSE (read here: the arena is planned before the knobs)
+    c->rs_fuse = getenv_int("FAASBAL_RS_FUSE");
+    for (int i = 0; i < (c->rs_fuse ? 4 : 1); ++i)
+        ap.add(&c->rs_hist[i], std::max((size_t)256 * (cdiv(E, kRsTile) + 1),
+                                        (size_t)2048 * (size_t)(std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks) + 1)));
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
     ap.add(&c->c_arr, Qlog);
@@ -1113,6 +1143,22 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     // pinned memory; fb_tick_launch_staged issues one async copy per array.
     const uint32_t Wv = (uint32_t)(c->shard ? c->W_global : c->W);
     int32_t vmax = 0;
+    // Zero-copy: when the caller's arrays are pinned host memory (fb_host_alloc, e.g. a
+    // dispatcher that parses messages straight into them) the pass only validates, and
+    // the H2D copies read the caller's arrays; they must stay unchanged until the tick
+    // that uses them has been waited for.
+    bool direct = E > 0;
+    if (direct) {
+        const void *ptrs[5] = {kind, slot, val, ts, seq};
+        for (int j = 0; j < 5 && direct; ++j) {
+            if (!ptrs[j]) continue;  // seq may be NULL: filled with -1 on the device
+            hipPointerAttribute_t at;
+            if (hipPointerGetAttributes(&at, ptrs[j]) != hipSuccess || at.type != hipMemoryTypeHost) {
+                (void)hipGetLastError();
+                direct = false;
+            }
+        }
+    }
     if (E) {
         const size_t ecap = (size_t)c->E_cap;
         char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
@@ -1122,7 +1168,7 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
         double *ht = (double *)(h + ecap * 9);
         int64_t *hq = (int64_t *)(h + ecap * 17);
         HIPCHK(c, hipSetDevice(c->device));
-        if (c->stage_rec[half]) HIPCHK(c, hipEventSynchronize(c->stage_ev[half]));  // staging buffer reuse
+        if (!direct && c->stage_rec[half]) HIPCHK(c, hipEventSynchronize(c->stage_ev[half]));  // staging buffer reuse
         // parts of the batch on the pool's workers when it is large (the pass reads and
         // writes ~25 B per event, mostly cold caller memory: memory-latency bound)
         const int np = (c->pool && E >= kStagePar) ? c->pool->size() : 1;
@@ -1141,11 +1187,13 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
                        (uint32_t)(t < prev);
                 prev = t;
                 vm = std::max(vm, k <= FB_EV_RECONNECT ? v : 0);
-                hk[i] = k;
-                hs[i] = sl;
-                hv[i] = v;
-                ht[i] = t;
-                hq[i] = seq ? seq[i] : -1;
+                if (!direct) {
+                    hk[i] = k;
+                    hs[i] = sl;
+                    hv[i] = v;
+                    ht[i] = t;
+                    hq[i] = seq ? seq[i] : -1;
+                }
             }
             pbad[pi] = bad;
             pvmax[pi] = vm;
@@ -1171,11 +1219,22 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
         const size_t ecap = (size_t)c->E_cap;
         char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
         if (c->use_rec[half]) HIPCHK(c, hipStreamWaitEvent(c->cp_s, c->use_ev[half], 0));
-        HIPCHK(c, hipMemcpyAsync(c->evk[half], h, E, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evsl[half], h + ecap, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evv[half], h + ecap * 5, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evt[half], h + ecap * 9, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evq[half], h + ecap * 17, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+        const void *sk = h, *ss = h + ecap, *sv = h + ecap * 5, *st = h + ecap * 9, *sq = h + ecap * 17;
+        if (direct) {
+            sk = kind;
+            ss = slot;
+            sv = val;
+            st = ts;
+            sq = seq;
+        }
+        HIPCHK(c, hipMemcpyAsync(c->evk[half], sk, E, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evsl[half], ss, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evv[half], sv, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
+        HIPCHK(c, hipMemcpyAsync(c->evt[half], st, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+        if (sq)
+            HIPCHK(c, hipMemcpyAsync(c->evq[half], sq, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+        else
+            HIPCHK(c, hipMemsetAsync(c->evq[half], 0xff, (size_t)E * 8, c->cp_s));  // -1 for every event
         HIPCHK(c, hipEventRecord(c->stage_ev[half], c->cp_s));
         c->stage_rec[half] = true;
     }

@@ -228,10 +228,25 @@ struct Stream {
 // One LSD pass (histogram + scatter launches) over `db`-bit digits at `shift`;
 // hist holds (1 << db rounded up to 256 / 1024 / 2048) x (nblk + 1) counts (the
 // extra row: digit totals when nblk > kRsScanMin).
-// zero0 / zero1 (n words each) and zbits (zwords) are cleared by the histogram launch.
-void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
-                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, uint32_t *zbits, int zwords,
-                    int identity_vals, Stream h, Stream s);
+// Only the first pass launches a histogram kernel: every scatter adds the next
+// pass's [tile][digit] counts (hnext) while it places the keys, so a pass after the
+// first is one launch (plus k_rs_scan past kRsScanMin tiles).  The first pass's
+// histogram launch clears zero0 / zero1 (n words each), zbits (zwords) and the later
+// passes' tables zhist[0..2] (zhwords each).
+struct RsPass {
+    const uint32_t *kin, *vin;
+    uint32_t *kout, *vout;
+    int n, shift, db, nblk;
+    uint32_t *hist;   // this pass's counts (filled by the histogram launch or the previous scatter)
+    uint32_t *hnext;  // the next pass's counts, or null on the last pass
+    int first, identity_vals;
+    int32_t *zero0, *zero1;
+    uint32_t *zbits;
+    int zwords;
+    uint32_t *zhist[3];
+    int zhwords;
+};
+void launch_rs_pass(const RsPass &p, Stream h, Stream s);
 #ifndef FAASBAL_RS_SCAN_MIN
 #define FAASBAL_RS_SCAN_MIN 64
 #endif

@@ -341,7 +341,9 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift, int db,
                                                  uint32_t *__restrict__ hist, int nblk, int32_t *__restrict__ zero0,
-                                                 int32_t *__restrict__ zero1, uint32_t *__restrict__ zbits, int zwords) {
+                                                 int32_t *__restrict__ zero1, uint32_t *__restrict__ zbits, int zwords,
+                                                 uint32_t *__restrict__ zh0, uint32_t *__restrict__ zh1,
+                                                 uint32_t *__restrict__ zh2, int zhwords) {
     constexpr int DPT = NB / kBS;
     __shared__ uint32_t cnt[NB];
 #pragma unroll
@@ -349,6 +351,12 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ ke
     __syncthreads();
     const int base = blockIdx.x * kRsTile;
     for (int i = blockIdx.x * kBS + (int)threadIdx.x; i < zwords; i += nblk * kBS) zbits[i] = 0;
+    // the later passes' count tables, filled by atomics in the scatters before them
+    for (int i = blockIdx.x * kBS + (int)threadIdx.x; i < zhwords; i += nblk * kBS) {
+        if (zh0) zh0[i] = 0;
+        if (zh1) zh1[i] = 0;
+        if (zh2) zh2[i] = 0;
+    }
     if (zero0) {
 #pragma unroll
         for (int j = 0; j < kRsItems; ++j) {
@@ -420,7 +428,8 @@ template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                     uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int n,
                                                     int shift, int db, const uint32_t *__restrict__ hist, int nblk,
-                                                    int identity_vals, const uint32_t *__restrict__ scanned) {
+                                                    int identity_vals, const uint32_t *__restrict__ scanned,
+                                                    uint32_t *__restrict__ hnext) {
     constexpr int DPT = NB / kBS;       // digits per thread
     constexpr int CH = 64 / DPT;        // blocks per batch of 64 loads in flight
     __shared__ uint32_t base[NB];
@@ -526,6 +535,8 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
             for (int q = 0; q < w; ++q) off += wcnt[q][d];
             kout[off] = key;
             vout[off] = val;
+            // the next pass's histogram: this key's next digit in its destination tile
+            if (hnext) atomicAdd(&hnext[(size_t)(off / kRsTile) * NB + ((key >> (shift + db)) & mask)], 1u);
         }
         __syncthreads();
         if constexpr (NB == 256) {
@@ -2459,31 +2470,31 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
 namespace fb {
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 template <int NB>
-static void rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
-                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, uint32_t *zbits, int zwords,
-                    int identity_vals, Stream h, Stream s) {
-    hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, kin, n, shift, db, hist, nblk,
-                          zero0, zero1, zbits, zwords);
+static void rs_pass(const RsPass &p, Stream h, Stream s) {
+    if (p.first)
+        hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(p.nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, p.kin, p.n, p.shift,
+                              p.db, p.hist, p.nblk, p.zero0, p.zero1, p.zbits, p.zwords, p.zhist[0], p.zhist[1],
+                              p.zhist[2], p.zhwords);
+    // timing: the pass starts with its first launch (histogram, scan or scatter)
+    hipEvent_t start = p.first ? nullptr : h.e0;
     const uint32_t *tot = nullptr;
-    if (nblk > kRsScanMin) {
-        uint32_t *t = hist + (size_t)nblk * NB;
-        hipLaunchKernelGGL(k_rs_scan, dim3(NB / 64), dim3(64 * kRsScanWaves), 0, s.s, hist, nblk, NB, t);
+    if (p.nblk > kRsScanMin) {
+        uint32_t *t = p.hist + (size_t)p.nblk * NB;
+        hipExtLaunchKernelGGL(k_rs_scan, dim3(NB / 64), dim3(64 * kRsScanWaves), 0, s.s, start, nullptr, 0, p.hist,
+                              p.nblk, NB, t);
+        start = nullptr;
         tot = t;
     }
-    hipExtLaunchKernelGGL(k_rs_scatter<NB>, dim3(nblk), dim3(kBS), 0, s.s, s.e0, s.e1, 0, kin, vin, kout, vout, n,
-                          shift, db, hist, nblk, identity_vals, tot);
+    hipExtLaunchKernelGGL(k_rs_scatter<NB>, dim3(p.nblk), dim3(kBS), 0, s.s, start, s.e1, 0, p.kin, p.vin, p.kout,
+                          p.vout, p.n, p.shift, p.db, p.hist, p.nblk, p.identity_vals, tot, p.hnext);
 }
-void launch_rs_pass(const uint32_t *kin, const uint32_t *vin, uint32_t *kout, uint32_t *vout, int n, int shift,
-                    int db, uint32_t *hist, int nblk, int32_t *zero0, int32_t *zero1, uint32_t *zbits, int zwords,
-                    int identity_vals, Stream h, Stream s) {
-    if (db <= 8)
-        rs_pass<256>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, zbits, zwords, identity_vals, h, s);
-    else if (db <= 10)
-        rs_pass<1024>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, zbits, zwords, identity_vals, h,
-                      s);
+void launch_rs_pass(const RsPass &p, Stream h, Stream s) {
+    if (p.db <= 8)
+        rs_pass<256>(p, h, s);
+    else if (p.db <= 10)
+        rs_pass<1024>(p, h, s);
     else
-        rs_pass<2048>(kin, vin, kout, vout, n, shift, db, hist, nblk, zero0, zero1, zbits, zwords, identity_vals, h,
-                      s);
+        rs_pass<2048>(p, h, s);
 }
 void launch_ev_apply(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -91,6 +91,22 @@ class GpuBalancer:
         buf = (C.c_char * max(int(n) * dtype.itemsize, 1)).from_address(p.value)
         return np.frombuffer(buf, dtype=dtype, count=int(n))
 
+    def pin_events(self, ev_kind, ev_slot, ev_val, ev_ts, ev_seq=None):
+        """Copies of a tick's message arrays in pinned host memory: ``stage()`` of
+        pinned arrays validates them in place and the H2D copies read them directly
+        (no staging copy); they must stay unchanged until that tick was waited for."""
+        out = []
+        for a, dt in ((ev_kind, np.uint8), (ev_slot, np.int32), (ev_val, np.int32), (ev_ts, np.float64),
+                      (ev_seq, np.int64)):
+            if a is None:
+                out.append(None)
+                continue
+            a = np.asarray(a, dt)
+            b = self.pinned(len(a), dt)
+            b[:] = a
+            out.append(b)
+        return out
+
     def __del__(self):
         try:
             self.close()

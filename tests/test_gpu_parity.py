@@ -366,12 +366,23 @@ def test_stream_ticks_vs_oracle():
         carried = n + len(b["orphans"]) - len(b["assign"])
 
 
-def test_stream_ticks_staged_pipeline_vs_oracle():
+@pytest.mark.parametrize("pinned", [False, True], ids=["copied", "zero-copy"])
+def test_stream_ticks_staged_pipeline_vs_oracle(pinned):
     """fb_tick_stage of tick t+1 while tick t runs (double-buffered pinned staging),
-    then fb_tick_launch_staged: the same outputs and states as the oracle."""
+    then fb_tick_launch_staged: the same outputs and states as the oracle.  Zero-copy:
+    the messages already sit in pinned host memory (GpuBalancer.pin_events), staging
+    validates them in place and the H2D copies read them (one tick's without seq)."""
     st = synth.zipf_state(W=8192, seed=0, dead_frac=0.0)
     ticks = synth.stream_ticks(st, n_ticks=6, seed=3, tasks_per_tick=4096, results_per_tick=4096, dt=1.5)
     g, o = _pair(st, len(st["log"]) + 6 * 8192 + 16, max_events=8192)
+    if pinned:
+        for i, tk in enumerate(ticks):
+            (tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq) = g.pin_events(
+                tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
+            if i == 2:  # no sequence numbers: results of tasks the balancer never saw
+                tk["ev_seq"] = None
+            else:
+                tk["ev_seq"] = seq
 
     def stage(tk):
         g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
@@ -386,7 +397,8 @@ def test_stream_ticks_staged_pipeline_vs_oracle():
         g.wait()
         a = dict(reconnect=g.event_status(), assign=g.assignments(), orphans=g.orphans(), evicted=g.evicted())
         g.commit()
-        b = o.tick(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        seq = tk["ev_seq"] if tk["ev_seq"] is not None else np.full(len(tk["ev_kind"]), -1, np.int64)
+        b = o.tick(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
         _cmp_out(a, b, t)
         _cmp_state(g, o, t)
         carried = n + len(b["orphans"]) - len(b["assign"])
@@ -449,3 +461,13 @@ def test_event_sort_large_batches(monkeypatch, W, E, wide):
     scatter; identical to the oracle (heap purge) up to 2 M messages in one tick."""
     monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
     _sort_tick(W, E, 0.3, W + E, purge_mode=2)
+
+
+@pytest.mark.parametrize("W,E,wide", [(1 << 20, 2000, "1"), ((1 << 17) + 5, 12000, "0"), (1 << 20, 300_000, "1")])
+def test_event_sort_fused_histograms(monkeypatch, W, E, wide):
+    """FAASBAL_RS_FUSE=1: every pass after the first takes its histogram from the
+    previous scatter's atomics (no histogram launch); identical to the oracle with
+    two and three passes, and past the column-prefix launch's threshold."""
+    monkeypatch.setenv("FAASBAL_RS_FUSE", "1")
+    monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
+    _sort_tick(W, E, 0.3, W + E + 1, purge_mode=2)
