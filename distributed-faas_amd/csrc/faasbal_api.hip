@@ -1441,6 +1441,25 @@ int fb_get_evicted(fb_ctx *c, int32_t n, int32_t *dst) {
     return copy_out(c, dst, c->evicted, (size_t)n * 4);
 }
 
+int fb_get_outputs(fb_ctx *c, int32_t *assign, int64_t *orphans, int32_t *evicted) {
+    if (!c) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (assign && c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_get_local_assignments");
+    HIPCHK(c, hipSetDevice(c->device));
+    // the three copies back to back on the stream, one synchronisation
+    if (assign && c->last.n_assigned)
+        HIPCHK(c, hipMemcpyAsync(assign, c->log_slot + c->l_head, (size_t)c->last.n_assigned * 4,
+                                 hipMemcpyDeviceToHost, c->stream));
+    if (orphans && c->last.n_orphans_local)
+        HIPCHK(c, hipMemcpyAsync(orphans, c->orphans, (size_t)c->last.n_orphans_local * 8, hipMemcpyDeviceToHost,
+                                 c->stream));
+    if (evicted && c->last.n_evicted)
+        HIPCHK(c, hipMemcpyAsync(evicted, c->evicted, (size_t)c->last.n_evicted * 4, hipMemcpyDeviceToHost,
+                                 c->stream));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
+}
+
 int fb_host_alloc(fb_ctx *c, int64_t bytes, void **ptr) {
     if (!c || !ptr || bytes < 0) return FB_EINVAL;
     *ptr = nullptr;

@@ -24,7 +24,7 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_selftest", "fb_debug_read", "fb_sync", "fb_set_stream", "fb_get_local_assignments",
            "fb_create_sharded", "fb_load_shard", "fb_read_shard_log", "fb_exchange_bytes", "fb_bind_exchange",
            "fb_tick_continue", "fb_create_deque", "fb_tick_stage", "fb_tick_launch_staged", "fb_host_alloc",
-           "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign")
+           "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign", "fb_get_outputs")
 
 
 class TickResult(C.Structure):
@@ -96,6 +96,7 @@ def load(path=None):
                               _P, _P, _P, _P]),
         "fb_apply_events": (C.c_int, [_P, dbl, i32, _P, _P, _P, _P, _P, C.POINTER(TickResult), _P, _P, _P]),
         "fb_purge": (C.c_int, [_P, dbl, dbl, C.POINTER(TickResult), _P, _P]),
+        "fb_get_outputs": (C.c_int, [_P, _P, _P, _P]),
         "fb_assign": (C.c_int, [_P, dbl, dbl, i64, C.POINTER(TickResult), _P, _P, _P]),
         "fb_device_view_get": (C.c_int, [_P, C.POINTER(DeviceView)]),
         "fb_timing_enable": (C.c_int, [_P, C.c_int]),

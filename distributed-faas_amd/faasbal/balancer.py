@@ -212,6 +212,22 @@ class GpuBalancer:
         self._chk(self.lib.fb_get_assignments(self.h, int(first), int(n), out.ctypes.data_as(C.c_void_p)))
         return out[:n]
 
+    def outputs(self, assign=None, orphans=None, evicted=None):
+        """The waited tick's assignments, orphans and evicted slots into the given
+        arrays (int32 / int64 / int32, e.g. ``pinned()`` ones; None skips a list) with
+        one synchronisation; returns the filled views."""
+        r = self.last
+        for a, n, dt in ((assign, r["n_assigned"], np.int32), (orphans, r["n_orphans_local"], np.int64),
+                         (evicted, r["n_evicted"], np.int32)):
+            if a is not None and (len(a) < n or a.dtype != dt or not a.flags["C_CONTIGUOUS"]):
+                raise ValueError("output array too small or of the wrong type")
+        self._chk(self.lib.fb_get_outputs(self.h, None if assign is None else _p(assign),
+                                          None if orphans is None else _p(orphans),
+                                          None if evicted is None else _p(evicted)))
+        return (None if assign is None else assign[: r["n_assigned"]],
+                None if orphans is None else orphans[: r["n_orphans_local"]],
+                None if evicted is None else evicted[: r["n_evicted"]])
+
     def local_assignments(self, first=0, n=None):
         """(task index, slot) of the tasks given to this context's workers."""
         n = self.last["n_local"] - first if n is None else n

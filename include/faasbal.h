@@ -138,6 +138,11 @@ int fb_get_orphans(fb_ctx *ctx, int64_t n, int64_t *dst);   /* old sequence numb
 int fb_get_evicted(fb_ctx *ctx, int32_t n, int32_t *dst);   /* slots, ascending                */
 int fb_get_event_status(fb_ctx *ctx, int32_t n, uint8_t *dst); /* FB_EVS_* per event          */
 
+/* All three of the waited tick's lists (each may be NULL; sizes res->n_assigned,
+ * n_orphans, n_evicted) with one synchronisation: into pinned memory, three DMA
+ * transfers back to back. */
+int fb_get_outputs(fb_ctx *ctx, int32_t *assign, int64_t *orphans, int32_t *evicted);
+
 /* Pinned host memory: fb_get_* copies into it are single DMA transfers on the
  * context stream (the drop-in's readback of a tick's assignments). */
 int fb_host_alloc(fb_ctx *ctx, int64_t bytes, void **ptr);

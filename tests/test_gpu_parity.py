@@ -159,6 +159,25 @@ def test_churn_stream_vs_oracle():
         carried = n + len(b["orphans"]) - len(b["assign"])
 
 
+def test_outputs_in_one_sync_match_the_single_copies():
+    """fb_get_outputs (three DMA transfers, one sync) into pinned buffers returns the
+    same lists as fb_get_assignments / fb_get_orphans / fb_get_evicted."""
+    st = synth.zipf_state(W=4096, seed=3)
+    g = GpuBalancer(4096, 2 * len(st["log"]) + 60000)
+    g.load(st)
+    g.launch(1000.0, 10.0, n_pending=50000)
+    r = g.wait()
+    a = g.pinned(r["n_assigned"] + 3, np.int32)
+    o = g.pinned(r["n_orphans_local"] + 3, np.int64)
+    e = g.pinned(r["n_evicted"] + 3, np.int32)
+    ga, go, ge = g.outputs(a, o, e)
+    assert r["n_orphans"] > 0 and r["n_evicted"] > 0
+    np.testing.assert_array_equal(ga, g.assignments())
+    np.testing.assert_array_equal(go, g.orphans())
+    np.testing.assert_array_equal(ge, g.evicted())
+    assert g.outputs(None, o, None)[1] is not None
+
+
 def test_relaunch_without_commit_is_identical():
     st = synth.zipf_state(W=4096, seed=5)
     g = GpuBalancer(4096, len(st["log"]) * 2 + 200_000)
