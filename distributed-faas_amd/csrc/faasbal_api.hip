@@ -123,6 +123,13 @@ struct fb_ctx {
     uint32_t *keys[2] = {nullptr, nullptr}, *vals[2] = {nullptr, nullptr};
     uint32_t *rs_hist[4] = {nullptr, nullptr, nullptr, nullptr};  // per sort pass: [tile][digit] counts
     int32_t *front_list = nullptr, *back_list = nullptr;
+    // one GPU, heartbeat loop: messages grouped per slot by linked lists (k_ev_link)
+    unsigned long long *ev_head = nullptr;  // per slot {link stamp, last linked message}
+    int32_t *ev_next = nullptr;             // per message
+    uint32_t link = 0;                      // stamp of the last k_ev_link launch
+    int ev_ll = 1;                          // FAASBAL_EV_LL=0: always the radix sort (A/B knob)
+    bool l_resort = false;                  // this tick reruns through the sort (a slot had > kLinkMax messages)
+    bool l_used_ll = false;                 // the last enqueue grouped by linked lists
     void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
     // device event arrays, double-buffered like the pinned halves: fb_tick_stage copies
     // half h on its own stream (overlapping a running tick), the launch waits for it
@@ -253,15 +260,27 @@ struct ArenaPlan {
     }
 };
 
+// FAASBAL_ARENA_SKEW (default 1): buffer i starts (i mod 16) x 4.25 KB after the end of
+// buffer i - 1, so arrays read by position side by side (c_arr, c_hb, queue, qfree,
+// qhb: power-of-two sizes at 1 M workers) do not start at the same offset modulo the
+// memory channel interleave (diagnostic A/B knob)
+size_t arena_skew(int i) {
+    static const int on = getenv("FAASBAL_ARENA_SKEW") ? atoi(getenv("FAASBAL_ARENA_SKEW")) : 1;
+    return on ? (size_t)(i % 16) * 4352 : 0;
+}
+
 int arena_commit(fb_ctx *c, ArenaPlan &ap) {
     size_t total = 0;
-    for (auto &r : ap.req) total += (r.second + 255) & ~(size_t)255;
+    int i = 0;
+    for (auto &r : ap.req) total += ((r.second + 255) & ~(size_t)255) + arena_skew(i++);
     total = (total + ((size_t)2 << 20) - 1) & ~(((size_t)2 << 20) - 1);
     hipError_t e = hipMalloc(&c->arena, total);
     if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(arena %zu B) failed: %s", total, hipGetErrorString(e));
     c->arena_bytes = total;
     char *p = (char *)c->arena;
+    i = 0;
     for (auto &r : ap.req) {
+        p += arena_skew(i++);
         *r.first = p;
         p += (r.second + 255) & ~(size_t)255;
     }
@@ -381,7 +400,49 @@ int enqueue_tick(fb_ctx *c) {
         evs = c->xbuf + xl.evs;
         if (c->phase != 2) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
     }
-    if (E > 0 && !(c->shard && c->phase == 2)) {
+    c->l_used_ll = false;
+    if (E > 0 && c->ev_head && c->ev_ll && !c->l_resort) {
+        // group the messages per slot by linked lists (no sort): two launches
+        EvArgs a{};
+        a.E = E;
+        a.W = W;
+        a.tick = c->tick;
+        a.tte = c->l_tte;
+        a.head_in = head;
+        a.ev_kind = c->ev_kind;
+        a.ev_val = c->ev_val;
+        a.ev_ts = c->ev_ts;
+        a.ev_seq = c->ev_seq;
+        a.ev_status = evs;
+        a.reg = c->reg;
+        a.free_in = c->free_[cur];
+        a.hb = c->hb;
+        a.epoch = c->epoch;
+        a.log_slot = c->log_slot;
+        a.post_reg = c->post_reg;
+        a.post_free = c->post_free;
+        a.post_hb = c->post_hb;
+        a.post_epoch = c->post_epoch;
+        a.post_flags = c->post_flags;
+        a.touched = c->touched;
+        a.tbits = c->tbits;
+        a.tbits_words = c->tbits ? (int)cdiv(W, 32) : 0;
+        a.front_list = front;
+        a.back_list = back;
+        a.ev_slot = c->ev_slot;
+        a.ev_head = c->ev_head;
+        a.ev_next = c->ev_next;
+        if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
+        a.link = c->link;
+        a.hout = c->hout_dev;
+        c->l_used_ll = true;
+        {
+            Timer t(c, "ev_link");
+            launch_ev_link(a, t.st());
+        }
+        Timer t(c, "ev_apply");
+        launch_ev_apply_ll(a, t.st());
+    } else if (E > 0 && !(c->shard && c->phase == 2)) {
 
         // stable radix sort of events by slot
         int bits = 1;
@@ -754,6 +815,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
                                         (size_t)2048 * (size_t)(std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks) + 1)));
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
+    if (!shard && !c->deque) {
+        ap.add(&c->ev_head, W);
+        ap.add(&c->ev_next, E);
+    }
     ap.add(&c->c_arr, Qlog);
     if (!shard) {
         ap.add(&c->c_hb, Qlog);
@@ -813,6 +878,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_LOGSCAN")) c->logscan = atoi(getenv("FAASBAL_LOGSCAN"));
     if (!rc && getenv("FAASBAL_RS_WIDE")) c->rs_wide = atoi(getenv("FAASBAL_RS_WIDE"));
     if (!rc && getenv("FAASBAL_GPLAN")) c->gplan = atoi(getenv("FAASBAL_GPLAN"));
+    if (!rc && getenv("FAASBAL_EV_LL")) c->ev_ll = atoi(getenv("FAASBAL_EV_LL"));
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;
@@ -841,6 +907,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
+    if (!rc && c->ev_head && hipMemset(c->ev_head, 0, W * 8) != hipSuccess) rc = FB_EHIP;  // stamp 0: never a launch's
     if (rc) {
         fb_destroy(c);
         return rc;
@@ -1276,6 +1343,7 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     // to a byte, 255 > 128), so only a fill level reaching the table fails the tick
     if (c->shard) c->l_R = std::min(c->l_R, kRFused);
     c->reruns = 0;
+    c->l_resort = false;
     c->launched = true;
     c->waited = false;
     c->l_purge_only = c->next_purge_only;
@@ -1316,6 +1384,16 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     HIPCHK(c, hipSetDevice(c->device));
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->l_used_ll && c->hout->resort) {
+            // a slot got more messages than k_ev_apply_ll sorts in registers: the same
+            // functional tick again, grouped by the radix sort
+            if (c->reruns > 4) return fail(c, FB_EHIP, "event regrouping did not converge");
+            c->l_resort = true;
+            c->reruns++;
+            int rc = enqueue_tick(c);
+            if (rc) return rc;
+            continue;
+        }
         if (c->hout->status == 0) break;
         if (c->hout->status == 2)
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",

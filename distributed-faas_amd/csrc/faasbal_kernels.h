@@ -64,8 +64,8 @@ struct HostOut {
     int32_t maxc;       // max c
     int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
                         // (deque contexts: new_qlen > token capacity is checked by the host)
-    int32_t pad;
-    int64_t n_local;    // sharded: tasks appended to this rank's log shard
+    int32_t resort;     // k_ev_apply_ll: a slot got too many messages, rerun through the sort
+    int64_t n_local;   // sharded: tasks appended to this rank's log shard
     int64_t O_local;    // sharded: this rank's orphans
 };
 
@@ -108,6 +108,13 @@ struct EvArgs {
     uint32_t *touched;
     uint32_t *tbits;   // one GPU: bit s = slot s got a message this tick (cleared by the first sort pass)
     int32_t *front_list, *back_list;  // slot + 1 (0 = empty), zeroed before the tick
+    // linked-list grouping (k_ev_link / k_ev_apply_ll; one GPU, heartbeat loop)
+    const int32_t *ev_slot;
+    unsigned long long *ev_head;  // per slot: {link stamp, last linked message}
+    int32_t *ev_next;             // per message: the message it displaced, -1 = first of its slot
+    uint32_t link;                // this launch's stamp (never 0)
+    int tbits_words;
+    HostOut *hout;                // resort: a slot had more than kLinkMax messages
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -256,6 +263,8 @@ constexpr int kRsScanMin = FAASBAL_RS_SCAN_MIN;
 // wider digits (2 passes for 1 M workers) up to this many tiles: the table is 2048 x tiles words
 constexpr int kRsWideMaxBlocks = 4096;
 void launch_ev_apply(const EvArgs &a, Stream st);
+void launch_ev_link(const EvArgs &a, Stream st);
+void launch_ev_apply_ll(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);

@@ -630,36 +630,30 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
     a.post_nf[s] = nf;
 }
 
-__global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
-    const int j = blockIdx.x * kBS + threadIdx.x;
-    if (j >= a.E) return;
-    // this position's key, its neighbours and its event index in one load round
-    const uint32_t gs = a.skeys[j], gprev = a.skeys[max(j - 1, 0)], gnext = a.skeys[min(j + 1, a.E - 1)];
-    const int i0 = (int)a.svals[j];
-    if (j > 0 && gprev == gs) return;
-    if (a.deque) {
-        ev_apply_deque(a, j, gs);
-        return;
+// One slot's record while its messages are applied in arrival order
+// (task_dispatcher.py:343-390 per message, the purge of the preceding loop
+// iteration at the message's own clock first).  s: local slot, gs: global slot.
+struct SlotRun {
+    int reg, inq, qstat, qidx, cur_is_start, died_start;
+    int32_t fr;
+    double hb;
+    uint32_t epoch;
+    __device__ __forceinline__ void init(const EvArgs &a, uint32_t s) {
+        reg = a.reg[s];
+        const int2 fq = a.free_in[s];
+        fr = fq.x;
+        hb = a.hb[s];
+        epoch = a.epoch[s];
+        inq = fq.y;
+        qstat = inq ? kQsKeep : kQsOut;
+        qidx = -1;
+        cur_is_start = reg;
+        died_start = 0;
     }
-    if (a.shard && ((int)gs < a.slot_base || (int)gs >= a.slot_base + a.W)) return;  // another rank's worker
-    const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
-    // the first message's payload, loaded alongside the slot record (most slots
-    // get one message: the chain is key -> {record, payload} -> log entry)
-    int kind = a.ev_kind[i0];
-    int32_t val = a.ev_val[i0];
-    double ts = a.ev_ts[i0];
-    int64_t seq = a.ev_seq[i0];
-    int i = i0;
-    int reg = a.reg[s];
-    const int2 fq = a.free_in[s];
-    int32_t fr = fq.x;
-    double hb = a.hb[s];
-    uint32_t epoch = a.epoch[s];
-    int inq = fq.y;
-    int qstat = inq ? kQsKeep : kQsOut;
-    int qidx = -1;
-    int cur_is_start = reg, died_start = 0;
-    for (int k = j;;) {
+    // PF: logv = log_slot[seq] loaded by the caller (one GPU only)
+    template <bool PF = false>
+    __device__ __forceinline__ void step(const EvArgs &a, uint32_t gs, int i, int kind, int32_t val, double ts,
+                                         int64_t seq, int32_t logv = 0) {
         // purge at ts before the message is polled (:390 of the previous iteration)
         if (reg && (ts - hb) > a.tte) {
             reg = 0;
@@ -687,12 +681,54 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
             hb = ts;
             const int64_t q = seq;
             if (q >= 0 && q < a.head_in) {
-                const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
-                if (li >= 0 && a.log_slot[li] == (int32_t)gs) a.log_slot[li] = -1;
+                if (PF) {  // one GPU, the entry's slot loaded ahead (clearing it twice is harmless)
+                    if (logv == (int32_t)gs) a.log_slot[q] = -1;
+                } else {
+                    const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
+                    if (li >= 0 && a.log_slot[li] == (int32_t)gs) a.log_slot[li] = -1;
+                }
             }
             if (fr == 1 && !inq) { inq = 1; qstat = kQsBack; qidx = i; }
         }
         a.ev_status[i] = status;
+    }
+    __device__ __forceinline__ void finish(const EvArgs &a, uint32_t s, uint32_t gs) {
+        a.post_reg[s] = (uint8_t)reg;
+        a.post_free[s] = fr;
+        a.post_hb[s] = hb;
+        a.post_epoch[s] = epoch;
+        a.post_flags[s] = (uint8_t)(died_start | (qstat << 1));
+        a.touched[s] = a.tick;
+        if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));
+        if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)gs + 1;
+        if (qstat == kQsBack) a.back_list[qidx] = (int32_t)gs + 1;
+    }
+};
+
+__global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
+    const int j = blockIdx.x * kBS + threadIdx.x;
+    if (j >= a.E) return;
+    // this position's key, its neighbours and its event index in one load round
+    const uint32_t gs = a.skeys[j], gprev = a.skeys[max(j - 1, 0)], gnext = a.skeys[min(j + 1, a.E - 1)];
+    const int i0 = (int)a.svals[j];
+    if (j > 0 && gprev == gs) return;
+    if (a.deque) {
+        ev_apply_deque(a, j, gs);
+        return;
+    }
+    if (a.shard && ((int)gs < a.slot_base || (int)gs >= a.slot_base + a.W)) return;  // another rank's worker
+    const uint32_t s = a.shard ? gs - (uint32_t)a.slot_base : gs;
+    // the first message's payload, loaded alongside the slot record (most slots
+    // get one message: the chain is key -> {record, payload} -> log entry)
+    int kind = a.ev_kind[i0];
+    int32_t val = a.ev_val[i0];
+    double ts = a.ev_ts[i0];
+    int64_t seq = a.ev_seq[i0];
+    int i = i0;
+    SlotRun r;
+    r.init(a, s);
+    for (int k = j;;) {
+        r.step(a, gs, i, kind, val, ts, seq);
         if (++k >= a.E || (k == j + 1 ? gnext : a.skeys[k]) != gs) break;
         i = (int)a.svals[k];
         kind = a.ev_kind[i];
@@ -700,15 +736,132 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
         ts = a.ev_ts[i];
         seq = a.ev_seq[i];
     }
-    a.post_reg[s] = (uint8_t)reg;
-    a.post_free[s] = fr;
-    a.post_hb[s] = hb;
-    a.post_epoch[s] = epoch;
-    a.post_flags[s] = (uint8_t)(died_start | (qstat << 1));
-    a.touched[s] = a.tick;
-    if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));
-    if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)gs + 1;
-    if (qstat == kQsBack) a.back_list[qidx] = (int32_t)gs + 1;
+    r.finish(a, s, gs);
+}
+
+// ------------------------------------------------------------ event grouping without a sort
+// One GPU, heartbeat loop: the messages of a slot are grouped by a linked list
+// instead of the radix sort.  k_ev_link: every message exchanges its index into
+// its slot's head word (tagged with a per-launch stamp, so nothing is cleared);
+// next[e] is the index it displaced, or -1 when it was the first of its slot --
+// that message's thread owns the slot in k_ev_apply_ll, walks head -> ... -> itself
+// (at most kLinkMax messages), sorts the indices (arrival order) in registers and
+// applies them.  A slot with more messages sets hout->resort and the host reruns
+// the tick through the sort (fb_tick_wait).  Also does the sort's first-pass
+// clears: this tick's front / back lists and the touched bitmap.
+constexpr int kLinkMax = 16;
+__global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
+    const int t = blockIdx.x * kBS + (int)threadIdx.x, nt = (int)gridDim.x * kBS;
+    if (t == 0) a.hout->resort = 0;
+    for (int w = t; w < a.tbits_words; w += nt) a.tbits[w] = 0u;
+    if (t < a.E) {
+        const uint32_t s = (uint32_t)a.ev_slot[t];
+        a.front_list[t] = 0;
+        a.back_list[t] = 0;
+        const unsigned long long old =
+            atomicExch(&a.ev_head[s], ((unsigned long long)a.link << 32) | (unsigned long long)(uint32_t)t);
+        a.ev_next[t] = (uint32_t)(old >> 32) == a.link ? (int32_t)(uint32_t)old : -1;
+    }
+}
+
+// log_slot[seq] of a result, loaded branch-free (clamped index; the value is only
+// compared when seq is a dispatched sequence)
+__device__ __forceinline__ int32_t log_peek(const EvArgs &a, int64_t seq) {
+    const int64_t q = seq < 0 ? 0 : (seq >= a.head_in ? (a.head_in > 0 ? a.head_in - 1 : 0) : seq);
+    return a.head_in > 0 ? a.log_slot[q] : -1;
+}
+
+__global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
+    const int e = blockIdx.x * kBS + threadIdx.x;
+    if (e >= a.E) return;
+    // slot, link and payload of this message in one load round
+    const uint32_t s = (uint32_t)a.ev_slot[e];
+    const int32_t nx = a.ev_next[e];
+    const int kind0 = a.ev_kind[e];
+    const int32_t val0 = a.ev_val[e];
+    const double ts0 = a.ev_ts[e];
+    const int64_t seq0 = a.ev_seq[e];
+    if (nx >= 0) return;  // another message of this slot owns it
+    // second round: the slot's head, its record and this message's log entry together
+    const int hidx = (int)(uint32_t)a.ev_head[s];
+    const int32_t logv0 = log_peek(a, seq0);
+    SlotRun r;
+    r.init(a, s);
+    if (hidx == e) {  // the slot's only message (most slots)
+        r.step<true>(a, s, e, kind0, val0, ts0, seq0, logv0);
+        r.finish(a, s, s);
+        return;
+    }
+    // walk head -> ... -> e (link order), each message's payload loaded with its link
+    int idx[kLinkMax], kd[kLinkMax];
+    int32_t vl[kLinkMax];
+    double tt[kLinkMax];
+    int64_t sq[kLinkMax];
+    int n = 0, cur = hidx;
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k < kLinkMax; ++k) {
+        const bool own = cur == e;
+        const int c = done ? e : cur;
+        idx[k] = done ? INT32_MAX : cur;
+        kd[k] = own ? kind0 : a.ev_kind[c];
+        vl[k] = own ? val0 : a.ev_val[c];
+        tt[k] = own ? ts0 : a.ev_ts[c];
+        sq[k] = own ? seq0 : a.ev_seq[c];
+        if (!done) {
+            ++n;
+            if (own) done = true;
+            else cur = a.ev_next[cur];
+        }
+    }
+    if (!done) {  // too many messages for the registers: the host reruns through the sort
+        a.hout->resort = 1;
+        return;
+    }
+    // sort the messages into arrival order (bitonic network, static register indices;
+    // padding entries carry INT32_MAX and stay last).  n <= 4: the first four suffice.
+    auto cx = [&](int i, int l, bool up) {
+        const bool sw = up ? (idx[i] > idx[l]) : (idx[i] < idx[l]);
+        int t = idx[i]; idx[i] = sw ? idx[l] : t; idx[l] = sw ? t : idx[l];
+        t = kd[i]; kd[i] = sw ? kd[l] : t; kd[l] = sw ? t : kd[l];
+        int32_t v = vl[i]; vl[i] = sw ? vl[l] : v; vl[l] = sw ? v : vl[l];
+        double d = tt[i]; tt[i] = sw ? tt[l] : d; tt[l] = sw ? d : tt[l];
+        int64_t q = sq[i]; sq[i] = sw ? sq[l] : q; sq[l] = sw ? q : sq[l];
+    };
+    if (n <= 4) {
+#pragma unroll
+        for (int k = 2; k <= 4; k <<= 1)
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    if ((i ^ j) > i) cx(i, i ^ j, (i & k) == 0);
+    } else {
+#pragma unroll
+        for (int k = 2; k <= kLinkMax; k <<= 1)
+#pragma unroll
+            for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+                for (int i = 0; i < kLinkMax; ++i)
+                    if ((i ^ j) > i) cx(i, i ^ j, (i & k) == 0);
+    }
+    // every result's log entry in one load round, then the messages in order
+    int32_t lv[kLinkMax];
+#pragma unroll
+    for (int k = 0; k < kLinkMax; ++k) lv[k] = k < n ? log_peek(a, sq[k]) : -1;
+    for (int m = 0; m < n; ++m) {
+        r.step<true>(a, s, idx[0], kd[0], vl[0], tt[0], sq[0], lv[0]);
+#pragma unroll
+        for (int k = 0; k + 1 < kLinkMax; ++k) {
+            idx[k] = idx[k + 1];
+            kd[k] = kd[k + 1];
+            vl[k] = vl[k + 1];
+            tt[k] = tt[k + 1];
+            sq[k] = sq[k + 1];
+            lv[k] = lv[k + 1];
+        }
+    }
+    r.finish(a, s, s);
 }
 
 
@@ -2498,6 +2651,13 @@ void launch_rs_pass(const RsPass &p, Stream h, Stream s) {
 }
 void launch_ev_apply(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+}
+void launch_ev_link(const EvArgs &a, Stream st) {
+    const int grid = (int)std::max<int64_t>(cdiv(a.E, kBS), std::min<int64_t>(cdiv(a.tbits_words, kBS), 1024));
+    hipExtLaunchKernelGGL(k_ev_link, dim3(std::max(grid, 1)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+}
+void launch_ev_apply_ll(const EvArgs &a, Stream st) {
+    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
     hipExtLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st.s, st.e0, st.e1, 0, err, seed);

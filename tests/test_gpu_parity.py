@@ -436,14 +436,14 @@ def test_launch_staged_needs_stage():
         g.launch_staged(10.0, 100)
 
 
-def _sort_tick(W, E, hot_frac, seed, purge_mode=1):
+def _sort_tick(W, E, hot_frac, seed, purge_mode=1, hot_n=5, expect_reruns=None):
     """One tick of E messages (kinds mixed, clocks ascending) on a W-slot table,
-    hot_frac of them on five hot slots; GPU vs oracle.  The oracle purges after
+    hot_frac of them on hot_n hot slots; GPU vs oracle.  The oracle purges after
     every message (purge_mode 1: O(W) each, so E * W stays around 1e9; 2: heap)."""
     rng = np.random.default_rng(seed)
     st = synth.zipf_state(W=W, seed=seed % 7, dead_frac=0.02)
-    hot = rng.choice(W, size=5, replace=False)
-    slot = np.where(rng.random(E) < hot_frac, hot[rng.integers(0, 5, E)], rng.integers(0, W, E)).astype(np.int32)
+    hot = rng.choice(W, size=hot_n, replace=False)
+    slot = np.where(rng.random(E) < hot_frac, hot[rng.integers(0, hot_n, E)], rng.integers(0, W, E)).astype(np.int32)
     kind = rng.choice([synth.EV_REGISTER, synth.EV_HEARTBEAT, synth.EV_RESULT, synth.EV_RECONNECT], size=E,
                       p=[0.1, 0.4, 0.4, 0.1]).astype(np.int32)
     val = rng.integers(0, 4, E).astype(np.int32)
@@ -454,11 +454,19 @@ def _sort_tick(W, E, hot_frac, seed, purge_mode=1):
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
     _cmp_state(g, o, 0)
+    if expect_reruns is not None:
+        assert (a["result"]["reruns"] > 0) == expect_reruns, a["result"]["reruns"]
+
+
+@pytest.fixture
+def radix(monkeypatch):
+    """FAASBAL_EV_LL=0: every message tick groups its events by the radix sort."""
+    monkeypatch.setenv("FAASBAL_EV_LL", "0")
 
 
 @pytest.mark.parametrize("W,E,wide", [((1 << 17) + 5, 12000, "1"), (1 << 20, 2000, "1"), (1 << 21, 1000, "1"),
                                       ((1 << 17) + 5, 12000, "0"), (1 << 20, 2000, "0")])
-def test_event_sort_wide_digits(monkeypatch, W, E, wide):
+def test_event_sort_wide_digits(radix, monkeypatch, W, E, wide):
     """Slot spaces of 17-22 bits: the event sort runs two passes of 9-11-bit
     digits (FAASBAL_RS_WIDE=0: three of 8 bits); identical to the oracle."""
     monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
@@ -468,13 +476,46 @@ def test_event_sort_wide_digits(monkeypatch, W, E, wide):
 @pytest.mark.parametrize("W,E", [(300, 30000), (5000, 30000), ((1 << 19) + 3, 2000)])
 def test_event_sort_stable_on_repeated_slots(W, E):
     """90 % of the messages on five slots (equal-key runs across sort tiles): the
-    per-slot arrival order the sort must keep decides every register / result."""
-    _sort_tick(W, E, 0.9, W)
+    per-slot arrival order the sort must keep decides every register / result.
+    The linked-list grouping gives up on these slots (> 16 messages) and the tick
+    reruns through the sort."""
+    _sort_tick(W, E, 0.9, W, expect_reruns=True)
+
+
+@pytest.mark.parametrize("W,E,hot_frac,hot_n", [((1 << 20), 77_000, 0.0, 5), (4096, 20_000, 0.0, 5),
+                                                (1 << 17, 30_000, 0.02, 128), (1 << 17, 3_000, 0.05, 20)])
+def test_event_link_grouping(W, E, hot_frac, hot_n):
+    """The default grouping of a message tick on one GPU: per-slot linked lists
+    (k_ev_link), each slot's messages (up to 16) sorted into arrival order in
+    registers by k_ev_apply_ll -- no radix sort and no rerun; identical to the oracle.
+    (4096 slots x 20 K messages: about 5 per slot, 0.2 % of slots with 13-16.)"""
+    _sort_tick(W, E, hot_frac, W + E + 3, purge_mode=2, hot_n=hot_n, expect_reruns=False)
+
+
+@pytest.mark.parametrize("n_hot", [16, 17])
+def test_event_link_limit(n_hot):
+    """Exactly 16 messages on one slot stay on the linked-list path; 17 rerun the
+    tick through the sort.  Both identical to the oracle."""
+    W, E = 1000, 600
+    rng = np.random.default_rng(n_hot)
+    st = synth.zipf_state(W=W, seed=3, dead_frac=0.02)
+    slot = rng.permutation(np.concatenate([np.full(n_hot, 7), rng.choice(np.arange(8, W), E - n_hot,
+                                                                          replace=False)])).astype(np.int32)
+    kind = rng.choice([synth.EV_REGISTER, synth.EV_HEARTBEAT, synth.EV_RESULT, synth.EV_RECONNECT], size=E,
+                      p=[0.1, 0.4, 0.4, 0.1]).astype(np.int32)
+    val = rng.integers(0, 4, E).astype(np.int32)
+    ts = np.sort(1000.0 - rng.random(E)).astype(np.float64)
+    g, o = _pair(st, 2 * len(st["log"]) + 100_000, max_events=E)
+    args = (1000.0, 10.0, kind, slot, val, ts, np.full(E, -1, np.int64), 3000)
+    a, b = g.tick(*args), o.tick(*args)
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+    assert (a["result"]["reruns"] > 0) == (n_hot > 16)
 
 
 @pytest.mark.parametrize("W,E,wide", [(1 << 20, 300_000, "1"), ((1 << 17) + 5, 1_200_000, "1"),
                                       ((1 << 17) + 5, 1_200_000, "0"), (1 << 20, 2_000_000, "1")])
-def test_event_sort_large_batches(monkeypatch, W, E, wide):
+def test_event_sort_large_batches(radix, monkeypatch, W, E, wide):
     """Batches of more than kRsScanMin sort tiles (E > 128 K): the column prefixes
     of the [tile][digit] counts come from their own launch (k_rs_scan) before each
     scatter; identical to the oracle (heap purge) up to 2 M messages in one tick."""
@@ -483,7 +524,7 @@ def test_event_sort_large_batches(monkeypatch, W, E, wide):
 
 
 @pytest.mark.parametrize("W,E,wide", [(1 << 20, 2000, "1"), ((1 << 17) + 5, 12000, "0"), (1 << 20, 300_000, "1")])
-def test_event_sort_fused_histograms(monkeypatch, W, E, wide):
+def test_event_sort_fused_histograms(radix, monkeypatch, W, E, wide):
     """FAASBAL_RS_FUSE=1: every pass after the first takes its histogram from the
     previous scatter's atomics (no histogram launch); identical to the oracle with
     two and three passes, and past the column-prefix launch's threshold."""
