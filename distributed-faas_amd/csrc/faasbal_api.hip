@@ -110,11 +110,9 @@ struct fb_ctx {
     // per-tick sparse post-message records
     uint32_t *touched = nullptr;
     uint32_t *tbits = nullptr;   // one GPU, heartbeat loop: touched bitmap (k_scan's queue role)
-    uint8_t *post_reg = nullptr, *post_flags = nullptr, *st = nullptr;
+    PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
+    uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
-    int32_t *post_free = nullptr;
-    double *post_hb = nullptr;
-    uint32_t *post_epoch = nullptr;
     // events
     uint8_t *ev_kind = nullptr, *ev_status = nullptr;
     int32_t *ev_val = nullptr, *ev_slot = nullptr;
@@ -419,11 +417,8 @@ int enqueue_tick(fb_ctx *c) {
         a.hb = c->hb;
         a.epoch = c->epoch;
         a.log_slot = c->log_slot;
-        a.post_reg = c->post_reg;
-        a.post_free = c->post_free;
-        a.post_hb = c->post_hb;
-        a.post_epoch = c->post_epoch;
-        a.post_flags = c->post_flags;
+        a.post = c->post;
+        a.post_rf = c->post_rf;
         a.touched = c->touched;
         a.tbits = c->tbits;
         a.tbits_words = c->tbits ? (int)cdiv(W, 32) : 0;
@@ -519,11 +514,8 @@ int enqueue_tick(fb_ctx *c) {
         a.hb = c->hb;
         a.epoch = c->epoch;
         a.log_slot = c->log_slot;
-        a.post_reg = c->post_reg;
-        a.post_free = c->post_free;
-        a.post_hb = c->post_hb;
-        a.post_epoch = c->post_epoch;
-        a.post_flags = c->post_flags;
+        a.post = c->post;
+        a.post_rf = c->post_rf;
         a.touched = c->touched;
         a.tbits = c->tbits;
         a.front_list = front;
@@ -613,10 +605,8 @@ int enqueue_tick(fb_ctx *c) {
     a.qhb_in = c->qhb[cur];
     a.touched = c->touched;
     a.tbits = c->tbits;
-    a.post_reg = c->post_reg;
-    a.post_flags = c->post_flags;
-    a.post_hb = c->post_hb;
-    a.post_free = c->post_free;
+    a.post = c->post;
+    a.post_rf = c->post_rf;
     a.front_list = front;
     a.back_list = back;
     a.st = c->st;
@@ -787,14 +777,11 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->epoch, W);
     ap.add(&c->touched, W);
     if (!shard && !c->deque) ap.add(&c->tbits, (W + 31) / 32);
-    ap.add(&c->post_reg, W);
-    ap.add(&c->post_flags, W);
+    ap.add(&c->post_rf, W);
     ap.add(&c->st, W);
     ap.add(&c->trash, (size_t)kTrashRows * kBS);
     ap.add(&c->dmask, (W + 63) / 64);
-    ap.add(&c->post_free, W);
-    ap.add(&c->post_hb, W);
-    ap.add(&c->post_epoch, W);
+    ap.add(&c->post, W);
     ap.add(&c->ev_status, E);
     for (int i = 0; i < 2; ++i) {
         ap.add(&c->evk[i], E);
@@ -1443,8 +1430,9 @@ int fb_tick_commit(fb_ctx *c) {
         a.tick = c->tick;
         a.st = c->st;
         a.touched = c->touched;
-        a.post_hb = c->post_hb;
-        a.post_epoch = c->post_epoch;
+        a.post = c->post;
+        a.tbits = c->tbits;
+        a.E = c->l_E;
         a.reg = c->reg;
         a.hb = c->hb;
         a.epoch = c->epoch;

@@ -40,7 +40,7 @@ constexpr uint8_t kEvsUnknown = 2;  // deque mode: result from an id without a r
 constexpr uint8_t kStAlive = 1;      // registered and alive after the final purge
 constexpr uint8_t kStDiedStart = 2;  // the registration alive at tick start died this tick
 constexpr uint8_t kStEvicted = 4;    // record deleted during the tick and not re-created
-// post_flags: bit0 died_start, bits 1-2 queue status after the tick's messages
+// post flags (post_rf >> 1): bit0 died_start, bits 1-2 queue status after the tick's messages
 constexpr int kPfDiedStart = 1;
 constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 
@@ -50,6 +50,15 @@ constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 // lives in its own array (epoch) that no scan reads.  Log entries of a dead
 // registration are cleared (-1) when the tick that redistributed them commits,
 // so every live entry belongs to its slot's current registration.
+
+// Post-message record of a slot that got messages this tick (k_ev_apply*): one
+// 16-byte store per slot; its registered flag and queue flags ride in post_rf
+// (bit 0 registered, bit 1 died_start, bits 2-3 queue status: rf >> 1 = post flags).
+struct alignas(16) PostRec {
+    double hb;
+    int32_t free;
+    uint32_t epoch;
+};
 
 // results of a tick, written by k_emit into host-mapped pinned memory
 struct HostOut {
@@ -100,12 +109,9 @@ struct EvArgs {
     const double *hb;
     const uint32_t *epoch;
     int32_t *log_slot;
-    uint8_t *post_reg;
-    int32_t *post_free;
-    double *post_hb;
-    uint32_t *post_epoch;
-    uint8_t *post_flags;
-    uint32_t *touched;
+    PostRec *post;
+    uint8_t *post_rf;
+    uint32_t *touched;  // tick stamp of a slot that got messages (written only without tbits)
     uint32_t *tbits;   // one GPU: bit s = slot s got a message this tick (cleared by the first sort pass)
     int32_t *front_list, *back_list;  // slot + 1 (0 = empty), zeroed before the tick
     // linked-list grouping (k_ev_link / k_ev_apply_ll; one GPU, heartbeat loop)
@@ -159,9 +165,8 @@ struct TickArgs {
     // this tick's message results
     const uint32_t *touched;
     const uint32_t *tbits;  // one GPU, message ticks: touched as a bitmap (L2-resident: 128 KB per 1M slots)
-    const uint8_t *post_reg, *post_flags;
-    const double *post_hb;
-    const int32_t *post_free;
+    const PostRec *post;
+    const uint8_t *post_rf;
     const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates
     uint8_t *st;
@@ -209,8 +214,9 @@ struct CommitArgs {
     uint32_t tick;
     const uint8_t *st;
     const uint32_t *touched;
-    const double *post_hb;
-    const uint32_t *post_epoch;
+    const PostRec *post;
+    const uint32_t *tbits;     // one GPU heartbeat loop: slots that got messages (valid when E > 0)
+    int E;                     // messages of the committed tick (0: no slot was touched)
     uint8_t *reg;
     double *hb;
     uint32_t *epoch;

@@ -620,11 +620,8 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
         }                                                // other kinds: no branch in start()
         a.ev_status[i] = status;
     }
-    a.post_reg[s] = (uint8_t)reg;
-    a.post_free[s] = fr;
-    a.post_hb[s] = hb;
-    a.post_epoch[s] = epoch;
-    a.post_flags[s] = (uint8_t)(kQsKeep << 1);
+    a.post[s] = PostRec{hb, fr, epoch};
+    a.post_rf[s] = (uint8_t)(reg | ((kQsKeep << 1) << 1));
     a.touched[s] = a.tick;
     a.post_tok[s] = k_old + nf + nb;
     a.post_nf[s] = nf;
@@ -693,13 +690,10 @@ struct SlotRun {
         a.ev_status[i] = status;
     }
     __device__ __forceinline__ void finish(const EvArgs &a, uint32_t s, uint32_t gs) {
-        a.post_reg[s] = (uint8_t)reg;
-        a.post_free[s] = fr;
-        a.post_hb[s] = hb;
-        a.post_epoch[s] = epoch;
-        a.post_flags[s] = (uint8_t)(died_start | (qstat << 1));
-        a.touched[s] = a.tick;
-        if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));
+        a.post[s] = PostRec{hb, fr, epoch};
+        a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1));
+        if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));  // the bitmap is the stamp
+        else a.touched[s] = a.tick;
         if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)gs + 1;
         if (qstat == kQsBack) a.back_list[qidx] = (int32_t)gs + 1;
     }
@@ -866,6 +860,12 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
 
 
 // ------------------------------------------------------------ slot state
+// Slot s got messages this tick (message ticks only: one GPU's bitmap, else the stamp).
+template <class A>
+__device__ __forceinline__ bool got_msg(const A &a, int s) {
+    return a.tbits ? ((a.tbits[s >> 5] >> (s & 31)) & 1u) != 0u : a.touched[s] == a.tick;
+}
+
 // Current record of slot s after this tick's messages (touched) or as committed.
 struct Cur {
     int reg0, reg, flags, q0;  // q0: in the committed LRU queue
@@ -884,15 +884,14 @@ __device__ __forceinline__ Cur cur_slot(const TickArgs &a, int s) {
     if (a.E > 0) {
         // message tick: committed and post-message records loaded together and
         // selected afterwards (a load behind the touched test would wait for it)
-        const uint32_t tk = a.touched[s];
-        const uint8_t pr = a.post_reg[s], pf = a.post_flags[s];
-        const double ph = a.post_hb[s];
-        const int32_t pfr = a.post_free[s];
-        c.t = tk == a.tick;
-        c.reg = c.t ? pr : c.reg0;
-        c.hb = c.t ? ph : hb0;
-        c.fr = c.t ? pfr : fr0;
-        c.flags = c.t ? pf : 0;
+        const bool tk = got_msg(a, s);
+        const uint8_t rf = a.post_rf[s];
+        const PostRec pr = a.post[s];
+        c.t = tk;
+        c.reg = c.t ? (rf & 1) : c.reg0;
+        c.hb = c.t ? pr.hb : hb0;
+        c.fr = c.t ? pr.free : fr0;
+        c.flags = c.t ? (rf >> 1) : 0;
     } else {
         c.t = false;
         c.reg = c.reg0;
@@ -1073,8 +1072,9 @@ __global__ __launch_bounds__(kBS) void k_slots(TickArgs a_) {
 // Committed hb is NaN for unregistered slots, so the untouched case is one load.
 __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
     if (!a.reg[s]) return false;
-    if (a.post_flags[s] & kPfDiedStart) return true;
-    return a.post_reg[s] && ((a.now - a.post_hb[s]) > a.tte);
+    const uint8_t rf = a.post_rf[s];
+    if ((rf >> 1) & kPfDiedStart) return true;
+    return (rf & 1) && ((a.now - a.post[s].hb) > a.tte);
 }
 
 // ------------------------------------------------------------ k_scan
@@ -1127,12 +1127,12 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             for (int j = 0; j < kFItems; ++j) {
                 const int sj = v[j] < 0 ? 0 : v[j];
                 h[j] = a.hb[sj];
-                tc[j] = a.E > 0 ? a.touched[sj] : 0u;
+                tc[j] = a.E > 0 ? (got_msg(a, sj) ? 1u : 0u) : 0u;
             }
 #pragma unroll
             for (int j = 0; j < kFItems; ++j) {
                 bool d = false;
-                if (v[j] >= 0) d = (a.E > 0 && tc[j] == a.tick) ? died_touched(a, v[j]) : ((a.now - h[j]) > a.tte);
+                if (v[j] >= 0) d = (a.E > 0 && tc[j] != 0u) ? died_touched(a, v[j]) : ((a.now - h[j]) > a.tte);
                 died |= d ? (1u << j) : 0u;
             }
         } else {
@@ -1252,19 +1252,17 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             const double hq = a.qhb_in[qc];
             const int32_t fq = a.qfree_in[qc];
             // touched: the bitmap word (L2-resident) when there is one, else the slot's stamp
-            const bool tq = a.E > 0 && (a.tbits ? ((a.tbits[sq >> 5] >> (sq & 31)) & 1u) != 0u
-                                                : a.touched[sq] == a.tick);
+            const bool tq = a.E > 0 && got_msg(a, sq);
             if (!tq) {
                 hbq = hq;
                 raw = ((a.now - hq) > a.tte) ? INT32_MIN : fq;
             } else {
-                const uint8_t pr = a.post_reg[sq], pf = a.post_flags[sq];
-                const double ph = a.post_hb[sq];
-                const int32_t pfr = a.post_free[sq];
-                hbq = ph;
-                raw = (pr && !((a.now - ph) > a.tte)) ? pfr : INT32_MIN;
+                const uint8_t rf = a.post_rf[sq];
+                const PostRec pr = a.post[sq];
+                hbq = pr.hb;
+                raw = ((rf & 1) && !((a.now - pr.hb) > a.tte)) ? pr.free : INT32_MIN;
                 // moved to the front, re-appended or removed by this tick's messages
-                if (((pf >> 1) & 3) != kQsKeep) raw = INT32_MIN;
+                if (((rf >> 2) & 3) != kQsKeep) raw = INT32_MIN;
             }
         } else {
             s = lq_slot(a, pos);
@@ -1277,13 +1275,13 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 } else {
                     raw = a.free_out[ls].x;
                     // the heartbeat after this tick's messages rides along into the next queue
-                    const double h0 = a.hb[ls], h1 = a.post_hb[ls];
-                    hbq = (a.E > 0 && a.touched[ls] == a.tick) ? h1 : h0;
+                    const double h0 = a.hb[ls], h1 = a.post[ls].hb;
+                    hbq = (a.E > 0 && got_msg(a, ls)) ? h1 : h0;
                 }
             }
             // an old queue entry moved to the front, re-appended or removed by this tick's messages
-            if (raw != INT32_MIN && a.E > 0 && inq && a.touched[ls] == a.tick &&
-                ((a.post_flags[ls] >> 1) & 3) != kQsKeep)
+            if (raw != INT32_MIN && a.E > 0 && inq && got_msg(a, ls) &&
+                ((a.post_rf[ls] >> 2) & 3) != kQsKeep)
                 raw = INT32_MIN;
         }
         if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
@@ -2606,11 +2604,12 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
     if (s >= a.W) return;
     const uint8_t stt = a.st[s];
     // committed hb is NaN for slots without a record (k_scan's log role relies on it)
-    if (a.touched[s] == a.tick) {
+    if (a.E > 0 && got_msg(a, s)) {
         const bool alive = (stt & kStAlive) != 0;
+        const PostRec pr = a.post[s];
         a.reg[s] = alive ? 1 : 0;
-        a.hb[s] = alive ? a.post_hb[s] : __builtin_nan("");
-        a.epoch[s] = a.post_epoch[s];
+        a.hb[s] = alive ? pr.hb : __builtin_nan("");
+        a.epoch[s] = pr.epoch;
     } else if (stt & kStEvicted) {
         a.reg[s] = 0;
         a.hb[s] = __builtin_nan("");
