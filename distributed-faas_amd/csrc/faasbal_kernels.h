@@ -167,10 +167,12 @@ struct TickArgs {
     const uint32_t *tbits;  // one GPU, message ticks: touched as a bitmap (L2-resident: 128 KB per 1M slots)
     const PostRec *post;
     const uint8_t *post_rf;
+    int post_lazy;  // 1: the slot purge loads post records only for touched slots (large tables)
     const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates
     uint8_t *st;
     unsigned long long *dmask;  // bit s: the registration alive at tick start died this tick
+    uint8_t *dcoarse;           // byte per dmask word: 1 when the word is nonzero (k_logscan's LDS level)
     int32_t *c_arr;  // raw free_processes of a live LRU position, INT32_MIN otherwise
     uint8_t *ofl;    // orphan flags, one byte per F-thread (8 log entries)
     uint32_t *wcnt, *fcnt, *qcnt;
@@ -274,7 +276,10 @@ void launch_ev_apply_ll(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
-void launch_logscan(const TickArgs &a, int grid, Stream st);
+#ifndef FAASBAL_LS_SPARSE
+#define FAASBAL_LS_SPARSE 1
+#endif
+void launch_logscan(const TickArgs &a, int grid, int max_lds, Stream st);
 void launch_plan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);

@@ -23,7 +23,7 @@ def main(d):
     for k in sorted(acc):
         ds = dur.get(k, [])
         avg = sum(ds) / len(ds) / 1e3 if ds else float("nan")
-        cs = " ".join("%s=%.0f" % (c.replace("TCP_UTCL1_", "").replace("TCP_TCC_", "").replace("_sum", ""), acc[k][c] / n[k][c])
+        cs = " ".join("%s=%.0f" % (c.replace("TCP_UTCL1_", "").replace("TCP_TCC_", "").replace("SQ_", "").replace("_sum", ""), acc[k][c] / n[k][c])
                       for c in sorted(acc[k]))
         print("%-28s %6.1f us  %s" % (k[:28], avg, cs))
 
