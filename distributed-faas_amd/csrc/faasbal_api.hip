@@ -109,7 +109,14 @@ struct fb_ctx {
     uint32_t tick = 1;
     // per-tick sparse post-message records
     uint32_t *touched = nullptr;
-    uint32_t *tbits = nullptr;   // one GPU, heartbeat loop: touched bitmap (k_scan's queue role)
+    uint32_t *tbits = nullptr;   // one GPU, heartbeat loop: touched bitmap of this launch (tbitsb[tick & 1])
+    uint32_t *tbitsb[2] = {nullptr, nullptr};  // by launch parity: a deferred commit reads the last tick's
+    // fb_tick_commit of a one-GPU heartbeat context is deferred into the next launch's
+    // k_ev_link (extra blocks) or flushed as its own launch by the next call that needs it
+    bool cm_pending = false;
+    CommitArgs cm{};
+    int cm_grid = 0;
+    int commit_now = 0;        // FAASBAL_COMMIT_NOW=1: never defer (A/B knob)
     PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
     uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
@@ -372,6 +379,17 @@ int choose_R(int32_t maxc) {
     return R;
 }
 
+// The deferred commit of the last tick as its own launch (when no k_ev_link takes it).
+int flush_commit(fb_ctx *c) {
+    if (!c->cm_pending) return FB_OK;
+    c->cm_pending = false;
+    HIPCHK(c, hipSetDevice(c->device));
+    Timer t(c, "commit");
+    launch_commit(c->cm, c->cm_grid, t.st());
+    HIPCHK(c, hipGetLastError());
+    return FB_OK;
+}
+
 // Enqueue every kernel of the tick described by c->l_* (events already on device).
 int enqueue_tick(fb_ctx *c) {
 
@@ -400,7 +418,9 @@ int enqueue_tick(fb_ctx *c) {
         if (c->phase != 2) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
     }
     c->l_used_ll = false;
-    if (E > 0 && c->ev_head && c->ev_ll && !c->l_resort) {
+    const bool ll = E > 0 && c->ev_head && c->ev_ll && !c->l_resort;
+    if (!ll && (rc = flush_commit(c))) return rc;
+    if (ll) {
         // group the messages per slot by linked lists (no sort): two launches
         EvArgs a{};
         a.E = E;
@@ -431,6 +451,11 @@ int enqueue_tick(fb_ctx *c) {
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         a.link = c->link;
         a.hout = c->hout_dev;
+        if (c->cm_pending) {  // the previous tick's commit rides in this launch
+            a.cm = c->cm;
+            a.cm_blocks = c->cm_grid;
+            c->cm_pending = false;
+        }
         c->l_used_ll = true;
         {
             Timer t(c, "ev_link");
@@ -609,6 +634,7 @@ int enqueue_tick(fb_ctx *c) {
     a.post = c->post;
     a.post_rf = c->post_rf;
     // past the L2-resident sizes the purge is bandwidth-bound: skip untouched post records
+    a.ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
     a.post_lazy = (W > kLdsBitmapSlots && getenv_int("FAASBAL_POST_EAGER") == 0) ? 1 : 0;
     a.front_list = front;
     a.back_list = back;
@@ -780,7 +806,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->hb, W);
     ap.add(&c->epoch, W);
     ap.add(&c->touched, W);
-    if (!shard && !c->deque) ap.add(&c->tbits, (W + 31) / 32);
+    if (!shard && !c->deque) {
+        ap.add(&c->tbitsb[0], (W + 31) / 32);
+        ap.add(&c->tbitsb[1], (W + 31) / 32);
+    }
     ap.add(&c->post_rf, W);
     ap.add(&c->st, W);
     ap.add(&c->trash, (size_t)kTrashRows * kBS);
@@ -895,7 +924,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         c->ev_seq = c->evq[0];
     }
     if (!rc && hipMemset(c->touched, 0, W * 4) != hipSuccess) rc = FB_EHIP;
-    if (!rc && c->tbits && hipMemset(c->tbits, 0, (W + 31) / 32 * 4) != hipSuccess) rc = FB_EHIP;
+    for (int p = 0; p < 2 && !rc; ++p)
+        if (c->tbitsb[p] && hipMemset(c->tbitsb[p], 0, (W + 31) / 32 * 4) != hipSuccess) rc = FB_EHIP;
+    if (!rc) c->tbits = c->tbitsb[c->tick & 1];
+    if (!rc && getenv("FAASBAL_COMMIT_NOW")) c->commit_now = atoi(getenv("FAASBAL_COMMIT_NOW"));
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
@@ -961,6 +993,7 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
                   const double *last_heartbeat, const uint32_t *epoch, const int32_t *queue, int64_t queue_len,
                   const int32_t *log_slot, int64_t log_len) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     if (c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_load_shard");
     if (n_workers < 0 || n_workers > c->W_cap) return fail(c, FB_EINVAL, "n_workers %d outside [0, %d]", n_workers, c->W_cap);
     if (log_len < 0 || log_len > c->log_cap) return fail(c, FB_EINVAL, "log_len %lld exceeds capacity", (long long)log_len);
@@ -1043,6 +1076,7 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
 int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, double *last_heartbeat, uint32_t *epoch,
                   int32_t *queue, int64_t *queue_len, int32_t *log_slot, int64_t *log_len) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     const size_t W = (size_t)c->W;
@@ -1069,6 +1103,7 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
                   const int32_t *queue, int64_t queue_len, const int32_t *log_slot, const uint32_t *log_seq,
                   int64_t log_len, int64_t log_head) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     if (!c->shard) return fail(c, FB_ESTATE, "fb_load_shard on a one-GPU context");
     if (n_workers < 0 || n_workers > c->W_cap || slot_base < 0 || (int64_t)slot_base + n_workers > c->W_global)
         return fail(c, FB_EINVAL, "slot range [%d, %d + %d) outside the %d-slot table", slot_base, slot_base, n_workers,
@@ -1141,6 +1176,7 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
 
 int fb_read_shard_log(fb_ctx *c, uint32_t *log_seq, int64_t *log_len, int64_t *log_head) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     if (!c->shard) return fail(c, FB_ESTATE, "fb_read_shard_log on a one-GPU context");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
@@ -1330,6 +1366,7 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->l_Qn = c->Qn;
     c->phase = 1;
     c->tick += 1;  // per-launch stamp: a relaunch with other messages never sees this launch's marks
+    if (c->tbitsb[0]) c->tbits = c->tbitsb[c->tick & 1];  // the last tick's bits stay for its deferred commit
     c->l_R = choose_R(std::max(c->maxc_hint, c->st_vmax));
     // sharded: a round table of at most 128 rows whatever the free counts (k_emit_shard);
     // counts beyond it are exact for every round below the table (the exchange clamps c
@@ -1448,9 +1485,16 @@ int fb_tick_commit(fb_ctx *c) {
         a.lseq = c->lseq;
         a.head_local = c->l_head_local;
         a.shard = c->shard;
-        Timer t(c, "commit");
-        launch_commit(a, a.nbw + (int)cdiv(n_orph, kBS), t.st());
-        HIPCHK(c, hipGetLastError());
+        if (c->ev_head && c->ev_ll && !c->commit_now) {
+            // deferred: the next launch's k_ev_link runs it (or flush_commit)
+            c->cm = a;
+            c->cm_grid = a.nbw + (int)cdiv(n_orph, kBS);
+            c->cm_pending = true;
+        } else {
+            Timer t(c, "commit");
+            launch_commit(a, a.nbw + (int)cdiv(n_orph, kBS), t.st());
+            HIPCHK(c, hipGetLastError());
+        }
     }
     c->cur = 1 - c->cur;
     c->head = c->last.log_head;
@@ -1464,6 +1508,7 @@ int fb_tick_commit(fb_ctx *c) {
 
 int fb_get_local_assignments(fb_ctx *c, int64_t first, int64_t n, int64_t *task, int32_t *slot) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (first < 0 || n < 0 || first + n > c->last.n_local) return fail(c, FB_EINVAL, "assignment range");
     if (!n) return FB_OK;
@@ -1622,6 +1667,8 @@ int fb_tick(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *
 }
 
 int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
+    if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     if (!c || !v) return FB_EINVAL;
     v->free_processes = &c->free_[c->cur]->x;
     v->free_processes_stride = (int32_t)sizeof(int2);
@@ -1698,6 +1745,7 @@ int fb_selftest(fb_ctx *c, int32_t *errors) {
 // Diagnostic: copy the stamp buffer (meaningful only in FAASBAL_STAMPS builds).
 int fb_debug_read(fb_ctx *c, unsigned long long *dst, int64_t n, int64_t *n_total) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (n_total) *n_total = (int64_t)c->dbg_n;
     if (dst && n > 0) HIPCHK(c, hipMemcpy(dst, c->dbg, (size_t)std::min<int64_t>(n, c->dbg_n) * 8, hipMemcpyDeviceToHost));
@@ -1706,6 +1754,7 @@ int fb_debug_read(fb_ctx *c, unsigned long long *dst, int64_t n, int64_t *n_tota
 
 int fb_sync(fb_ctx *c) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return FB_OK;

@@ -85,6 +85,27 @@ struct DevTotals {
     int64_t O_local;                  // sharded: this rank's orphans
 };
 
+struct CommitArgs {
+    int W;
+    int slot_base;
+    int nbw;            // slot blocks; blocks [nbw, nbw + ceil(n_orph / 256)) clear orphaned log entries
+    uint32_t tick;
+    const uint8_t *st;
+    const uint32_t *touched;
+    const PostRec *post;
+    const uint32_t *tbits;     // one GPU heartbeat loop: slots that got messages (valid when E > 0)
+    int E;                     // messages of the committed tick (0: no slot was touched)
+    uint8_t *reg;
+    double *hb;
+    uint32_t *epoch;
+    int64_t n_orph;            // orphans of the committed tick (this rank's, sharded)
+    const int64_t *orphans;    // their sequence numbers (global, sharded)
+    int32_t *log_slot;
+    const uint32_t *lseq;      // sharded: global sequence of each local entry (ascending)
+    int64_t head_local;        // sharded: local entries
+    int shard;
+};
+
 struct EvArgs {
     int E;
     int deque;          // 1: PushDispatcher.start semantics (no liveness, deque with repeated ids)
@@ -121,6 +142,9 @@ struct EvArgs {
     uint32_t link;                // this launch's stamp (never 0)
     int tbits_words;
     HostOut *hout;                // resort: a slot had more than kLinkMax messages
+    // the previous tick's deferred commit, run by k_ev_link's blocks past the link grid
+    int cm_blocks;
+    CommitArgs cm;
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -167,6 +191,7 @@ struct TickArgs {
     const uint32_t *tbits;  // one GPU, message ticks: touched as a bitmap (L2-resident: 128 KB per 1M slots)
     const PostRec *post;
     const uint8_t *post_rf;
+    int ffirst;     // k_scan: log blocks before queue blocks in the grid (A/B knob FAASBAL_SCAN_FFIRST)
     int post_lazy;  // 1: the slot purge loads post records only for touched slots (large tables)
     const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates
@@ -209,26 +234,6 @@ struct TickArgs {
     int64_t *opre, *oA;
 };
 
-struct CommitArgs {
-    int W;
-    int slot_base;
-    int nbw;            // slot blocks; blocks [nbw, nbw + ceil(n_orph / 256)) clear orphaned log entries
-    uint32_t tick;
-    const uint8_t *st;
-    const uint32_t *touched;
-    const PostRec *post;
-    const uint32_t *tbits;     // one GPU heartbeat loop: slots that got messages (valid when E > 0)
-    int E;                     // messages of the committed tick (0: no slot was touched)
-    uint8_t *reg;
-    double *hb;
-    uint32_t *epoch;
-    int64_t n_orph;            // orphans of the committed tick (this rank's, sharded)
-    const int64_t *orphans;    // their sequence numbers (global, sharded)
-    int32_t *log_slot;
-    const uint32_t *lseq;      // sharded: global sequence of each local entry (ascending)
-    int64_t head_local;        // sharded: local entries
-    int shard;
-};
 
 // Host-side launchers (defined in faasbal_kernels.hip; grid sizes are the caller's).
 // A launch target: the stream, plus optional dispatch-packet timing events

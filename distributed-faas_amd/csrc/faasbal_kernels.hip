@@ -573,6 +573,12 @@ __device__ __forceinline__ int64_t lseq_find(const uint32_t *lseq, int64_t n, in
     return (lo < n && (int64_t)lseq[lo] == q) ? lo : -1;
 }
 
+// Slot s got messages this tick (message ticks only: one GPU's bitmap, else the stamp).
+template <class A>
+__device__ __forceinline__ bool got_msg(const A &a, int s) {
+    return a.tbits ? ((a.tbits[s >> 5] >> (s & 31)) & 1u) != 0u : a.touched[s] == a.tick;
+}
+
 // The loop without heartbeats, PushDispatcher.start (task_dispatcher.py:251-322), for
 // one slot's messages: no liveness; every register(n > 0) inserts a new token at the
 // left of the deque (:280-281), a result that brings free to 1 appends one at the
@@ -733,6 +739,36 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
     r.finish(a, s, gs);
 }
 
+// ------------------------------------------------------------ commit
+__device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
+    if (blk >= a.nbw) {
+        // the committed tick redistributed these entries: their tasks now run under new
+        // sequence numbers, so the old entries leave the in-flight log
+        const int64_t i = (int64_t)(blk - a.nbw) * kBS + threadIdx.x;
+        if (i >= a.n_orph) return;
+        const int64_t q = a.orphans[i];
+        const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
+        if (li >= 0) a.log_slot[li] = -1;
+        return;
+    }
+    const int s = blk * kBS + threadIdx.x;
+    if (s >= a.W) return;
+    const uint8_t stt = a.st[s];
+    // committed hb is NaN for slots without a record (k_scan's log role relies on it)
+    if (a.E > 0 && got_msg(a, s)) {
+        const bool alive = (stt & kStAlive) != 0;
+        const PostRec pr = a.post[s];
+        a.reg[s] = alive ? 1 : 0;
+        a.hb[s] = alive ? pr.hb : __builtin_nan("");
+        a.epoch[s] = pr.epoch;
+    } else if (stt & kStEvicted) {
+        a.reg[s] = 0;
+        a.hb[s] = __builtin_nan("");
+    }
+}
+
+__global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) { commit_body(a, blockIdx.x); }
+
 // ------------------------------------------------------------ event grouping without a sort
 // One GPU, heartbeat loop: the messages of a slot are grouped by a linked list
 // instead of the radix sort.  k_ev_link: every message exchanges its index into
@@ -745,7 +781,12 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 // clears: this tick's front / back lists and the touched bitmap.
 constexpr int kLinkMax = 16;
 __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
-    const int t = blockIdx.x * kBS + (int)threadIdx.x, nt = (int)gridDim.x * kBS;
+    const int lb = (int)gridDim.x - a.cm_blocks;  // link blocks; the rest commit the previous tick
+    if ((int)blockIdx.x >= lb) {
+        commit_body(a.cm, (int)blockIdx.x - lb);
+        return;
+    }
+    const int t = blockIdx.x * kBS + (int)threadIdx.x, nt = lb * kBS;
     if (t == 0) a.hout->resort = 0;
     for (int w = t; w < a.tbits_words; w += nt) a.tbits[w] = 0u;
     if (t < a.E) {
@@ -860,11 +901,6 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
 
 
 // ------------------------------------------------------------ slot state
-// Slot s got messages this tick (message ticks only: one GPU's bitmap, else the stamp).
-template <class A>
-__device__ __forceinline__ bool got_msg(const A &a, int s) {
-    return a.tbits ? ((a.tbits[s >> 5] >> (s & 31)) & 1u) != 0u : a.touched[s] == a.tick;
-}
 
 // Current record of slot s after this tick's messages (touched) or as committed.
 struct Cur {
@@ -1098,9 +1134,11 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     __shared__ int32_t m4[kWaves];
     __shared__ unsigned long long s4[kWaves];
     __shared__ uint32_t wc[kWaves][kBS];
-    const int bid = blockIdx.x;
-    const int SO = a.nbw;
     const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
+    // a.ffirst: log blocks first in hardware order (logical ids unchanged)
+    int bid = blockIdx.x;
+    if (a.ffirst) bid = bid < nbf ? bid + a.nbq : (bid < nbf + a.nbq ? bid - nbf : bid);
+    const int SO = a.nbw;
     STAMP(a, SO, 0);
     // grid: queue blocks first (the critical path: their loads go out before the log
     // role's gathers fill the memory queues), then log blocks, then slot blocks
@@ -2627,33 +2665,6 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     }
 }
 
-// ------------------------------------------------------------ commit
-__global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
-    if ((int)blockIdx.x >= a.nbw) {
-        // the committed tick redistributed these entries: their tasks now run under new
-        // sequence numbers, so the old entries leave the in-flight log
-        const int64_t i = (int64_t)(blockIdx.x - a.nbw) * kBS + threadIdx.x;
-        if (i >= a.n_orph) return;
-        const int64_t q = a.orphans[i];
-        const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
-        if (li >= 0) a.log_slot[li] = -1;
-        return;
-    }
-    const int s = blockIdx.x * kBS + threadIdx.x;
-    if (s >= a.W) return;
-    const uint8_t stt = a.st[s];
-    // committed hb is NaN for slots without a record (k_scan's log role relies on it)
-    if (a.E > 0 && got_msg(a, s)) {
-        const bool alive = (stt & kStAlive) != 0;
-        const PostRec pr = a.post[s];
-        a.reg[s] = alive ? 1 : 0;
-        a.hb[s] = alive ? pr.hb : __builtin_nan("");
-        a.epoch[s] = pr.epoch;
-    } else if (stt & kStEvicted) {
-        a.reg[s] = 0;
-        a.hb[s] = __builtin_nan("");
-    }
-}
 
 }  // namespace fb
 
@@ -2691,8 +2702,8 @@ void launch_ev_apply(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_ev_link(const EvArgs &a, Stream st) {
-    const int grid = (int)std::max<int64_t>(cdiv(a.E, kBS), std::min<int64_t>(cdiv(a.tbits_words, kBS), 1024));
-    hipExtLaunchKernelGGL(k_ev_link, dim3(std::max(grid, 1)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    const int grid = std::max(1, (int)std::max<int64_t>(cdiv(a.E, kBS), std::min<int64_t>(cdiv(a.tbits_words, kBS), 1024)));
+    hipExtLaunchKernelGGL(k_ev_link, dim3(grid + a.cm_blocks), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

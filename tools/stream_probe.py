@@ -13,6 +13,10 @@ st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
 ticks = synth.stream_ticks(st, n_ticks=K + 6, seed=2, tasks_per_tick=T, results_per_tick=T)
 g = GpuBalancer(W, len(st["log"]) + (K + 8) * 2 * T, max_events=max(len(t["ev_kind"]) for t in ticks), device=0)
 g.load(st)
+if "--pinned" in sys.argv:  # as bench.py: messages in pinned memory, staging only validates
+    for tk in ticks:
+        (tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"]) = g.pin_events(
+            tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
 carried = 0
 acc = np.zeros(5)
 pc = time.perf_counter
