@@ -120,7 +120,6 @@ struct fb_ctx {
     PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
     uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
-    uint8_t *dcoarse = nullptr;
     // events
     uint8_t *ev_kind = nullptr, *ev_status = nullptr;
     int32_t *ev_val = nullptr, *ev_slot = nullptr;
@@ -640,7 +639,6 @@ int enqueue_tick(fb_ctx *c) {
     a.back_list = back;
     a.st = c->st;
     a.dmask = c->dmask;
-    a.dcoarse = c->dcoarse;
     a.c_arr = c->c_arr;
     a.ofl = c->ofl;
     a.wcnt = c->wcnt;
@@ -710,7 +708,7 @@ int enqueue_tick(fb_ctx *c) {
         }
         if (a.f_sep) {
             Timer t(c, "logscan");
-            launch_logscan(a, ls_grid, c->max_lds, t.st());
+            launch_logscan(a, ls_grid, t.st());
         }
         HIPCHK(c, hipGetLastError());
         return FB_OK;
@@ -740,7 +738,7 @@ int enqueue_tick(fb_ctx *c) {
     }
     if (a.f_sep) {
         Timer t(c, "logscan");
-        launch_logscan(a, ls_grid, c->max_lds, t.st());
+        launch_logscan(a, ls_grid, t.st());
     }
     if (!a.fused) {
         Timer t(c, "plan");
@@ -814,7 +812,6 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->st, W);
     ap.add(&c->trash, (size_t)kTrashRows * kBS);
     ap.add(&c->dmask, (W + 63) / 64);
-    ap.add(&c->dcoarse, (W + 63) / 64 + 16);
     ap.add(&c->post, W);
     ap.add(&c->ev_status, E);
     for (int i = 0; i < 2; ++i) {
@@ -931,8 +928,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
-    if (!rc && c->ev_head && hipMemset(c->ev_head, 0, W * 8) != hipSuccess) rc = FB_EHIP;
-    if (!rc && hipMemset(c->dcoarse, 0, (W + 63) / 64 + 16) != hipSuccess) rc = FB_EHIP;  // tail bytes stay 0  // stamp 0: never a launch's
+    if (!rc && c->ev_head && hipMemset(c->ev_head, 0, W * 8) != hipSuccess) rc = FB_EHIP;  // stamp 0: never a launch's
     if (rc) {
         fb_destroy(c);
         return rc;

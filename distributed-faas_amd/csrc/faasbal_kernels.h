@@ -197,7 +197,6 @@ struct TickArgs {
     // intermediates
     uint8_t *st;
     unsigned long long *dmask;  // bit s: the registration alive at tick start died this tick
-    uint8_t *dcoarse;           // byte per dmask word: 1 when the word is nonzero (k_logscan's LDS level)
     int32_t *c_arr;  // raw free_processes of a live LRU position, INT32_MIN otherwise
     uint8_t *ofl;    // orphan flags, one byte per F-thread (8 log entries)
     uint32_t *wcnt, *fcnt, *qcnt;
@@ -281,10 +280,7 @@ void launch_ev_apply_ll(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
-#ifndef FAASBAL_LS_SPARSE
-#define FAASBAL_LS_SPARSE 1
-#endif
-void launch_logscan(const TickArgs &a, int grid, int max_lds, Stream st);
+void launch_logscan(const TickArgs &a, int grid, Stream st);
 void launch_plan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);

@@ -1089,7 +1089,6 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
     const uint64_t dm = __ballot(died_start);
     if ((!a.slots_in_scan || a.f_sep) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) {
         a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
-        if (a.f_sep) a.dcoarse[(blk * kBS) / 64 + wave_id()] = dm != 0ull ? 1 : 0;  // k_logscan<true>
     }
     const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
     if (lane_id() == 0) l4[wave_id()] = ev;
@@ -1467,56 +1466,26 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
 // then every wave flags the orphans of whole 2048-entry tiles alone (lane: 4
 // groups of 8 consecutive entries, 8 int4 loads in flight), with k_scan's
 // per-tile ofl / fcnt layout so k_emit's orphan compaction is unchanged.
-// The died bitmap in LDS.  SPARSE (it fits: W / 64 + W / 8 bytes <= LDS): a byte
-// per 64 slots (nonzero bitmap word, written by the slot role) is copied whole --
-// 16 KB at 1 M slots -- and only the bitmap words whose byte is set (a tick kills
-// hundreds of workers: a few hundred words, not 16 K) are copied into their place
-// in an LDS image of the bitmap; the entries test the byte, then the word.  Else
-// the whole bitmap (W / 8 bytes) is copied.
-template <bool SPARSE>
 __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long bm[];
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows
     STAMP(a, SO, 0);
-    const int nwords = (a.W + 63) >> 6;
-    const int ncb16 = (nwords + 15) >> 4;                  // uint4 of coarse bytes
-    uint8_t *cb = reinterpret_cast<uint8_t *>(bm);         // SPARSE: [0, 16 ncb16) coarse bytes
-    unsigned long long *fw = SPARSE ? bm + 2 * ncb16 : bm;  // bitmap image (SPARSE: sparse)
-    if constexpr (SPARSE) {
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.dcoarse);
-        for (int i = (int)threadIdx.x; i < ncb16; i += kLsBS) {
-            const uint4 t = src[i];
-            reinterpret_cast<uint4 *>(cb)[i] = t;
-            const uint32_t wv[4] = {t.x, t.y, t.z, t.w};
+    const int n4 = (((a.W + 63) >> 6) + 1) >> 1;
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
+    for (int i0 = 0; i0 < n4; i0 += kLsBS * 8) {
+        uint4 t[8];
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                uint32_t m = wv[q];
-                while (m) {  // each nonzero byte: its bitmap word into the image
-                    const int bp = __builtin_ctz(m) & ~7;
-                    m &= ~(0xffu << bp);
-                    const int w = 16 * i + 4 * q + (bp >> 3);
-                    if (w < nwords) fw[w] = a.dmask[w];
-                }
-            }
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kLsBS + (int)threadIdx.x;
+            t[k] = src[i < n4 ? i : n4 - 1];
         }
-    } else {
-        const int n4 = (nwords + 1) >> 1;
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
-        for (int i0 = 0; i0 < n4; i0 += kLsBS * 8) {
-            uint4 t[8];
+        // stores past the bitmap go to one spare slot, not behind a branch: a
+        // guarded store lets the compiler sink its load into the branch, one
+        // round trip per load
 #pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int i = i0 + k * kLsBS + (int)threadIdx.x;
-                t[k] = src[i < n4 ? i : n4 - 1];
-            }
-            // stores past the bitmap go to one spare slot, not behind a branch: a
-            // guarded store lets the compiler sink its load into the branch, one
-            // round trip per load
-#pragma unroll
-            for (int k = 0; k < 8; ++k) {
-                const int i = i0 + k * kLsBS + (int)threadIdx.x;
-                reinterpret_cast<uint4 *>(bm)[i < n4 ? i : n4] = t[k];
-            }
+        for (int k = 0; k < 8; ++k) {
+            const int i = i0 + k * kLsBS + (int)threadIdx.x;
+            reinterpret_cast<uint4 *>(bm)[i < n4 ? i : n4] = t[k];
         }
     }
     __syncthreads();
@@ -1550,8 +1519,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
                 int sj = v[k][j];
                 if (a.shard && sj >= 0) sj -= a.slot_base;  // log slots are global ids
                 const int sc = sj < 0 ? 0 : sj;
-                const bool any = !SPARSE || cb[sc >> 6] != 0;
-                flags |= (sj >= 0 && any && ((fw[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
+                flags |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
             }
             a.ofl[(size_t)b * kBS + k * 64 + lane] = (uint8_t)flags;
             cnt += (uint32_t)__popc(flags);
@@ -2729,19 +2697,10 @@ void launch_scan(const TickArgs &a, Stream st) {
     const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;
     FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
 }
-size_t logscan_lds(int W, bool sparse) {
-    const size_t nwords = ((size_t)W + 63) / 64;
-    return sparse ? (nwords + 15) / 16 * 16 + nwords * 8 : ((nwords + 1) / 2 + 1) * 16;  // + the spare slot
-}
-void launch_logscan(const TickArgs &a, int grid, int max_lds, Stream st) {
-    // the sparse image when coarse bytes + bitmap fit (W <= 1.13 M slots on gfx950)
-    const bool sparse = logscan_lds(a.W, true) <= (size_t)max_lds && FAASBAL_LS_SPARSE;
-    if (sparse)
-        hipExtLaunchKernelGGL(k_logscan<true>, dim3(grid), dim3(kLsBS), logscan_lds(a.W, true), st.s, st.e0, st.e1, 0, a);
-    else
-        hipExtLaunchKernelGGL(k_logscan<false>, dim3(grid), dim3(kLsBS), logscan_lds(a.W, false), st.s, st.e0, st.e1, 0, a);
-}
-void launch_plan(const TickArgs &a, Stream st) {
+void launch_logscan(const TickArgs &a, int grid, Stream st) {
+    const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
+    hipExtLaunchKernelGGL(k_logscan, dim3(grid), dim3(kLsBS), lds, st.s, st.e0, st.e1, 0, a);
+}void launch_plan(const TickArgs &a, Stream st) {
     if (a.grp_on)
         hipExtLaunchKernelGGL(k_plan2, dim3(a.ngrp + 2), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
     else

@@ -58,7 +58,9 @@ typedef struct fb_tick_result {
 } fb_tick_result;
 
 /* Device pointers of the context's state (for zero-copy consumers, e.g.
- * torch tensors built from data_ptr).  Valid until the next fb_tick_commit. */
+ * torch tensors built from data_ptr).  Valid until the next fb_tick_commit;
+ * after a commit, call fb_sync (or fetch the view again) before reading through
+ * it, so that the deferred part of the commit has run. */
 typedef struct fb_device_view {
     int32_t *free_processes; /* [n_workers]  PushWorker.free_processes (:205), every
                               * free_processes_stride bytes                    */
@@ -129,7 +131,12 @@ int fb_purge_launch(fb_ctx *ctx, double now, double tte);
  * with a wider round table when free counts exceeded the launch's estimate. */
 int fb_tick_wait(fb_ctx *ctx, fb_tick_result *res);
 
-/* Make the waited tick's post-state the committed state. */
+/* Make the waited tick's post-state the committed state.  On a one-GPU
+ * heartbeat context the device part (registered / last_heartbeat / epoch of the
+ * slots the tick touched or evicted, orphaned log entries) is deferred: the
+ * next launch's first kernel runs it, and any call that reads or replaces
+ * state first (fb_read_state, fb_load_state, fb_device_view_get, fb_sync, ...)
+ * enqueues it on its own.  Observably the same as an immediate commit. */
 int fb_tick_commit(fb_ctx *ctx);
 
 /* Copy outputs of the waited tick to host memory. */
