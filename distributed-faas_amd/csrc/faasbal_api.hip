@@ -163,6 +163,9 @@ struct fb_ctx {
     int gpar = 0;                           // parity of the last fused launch
     int gdirty[2] = {0, 0};                 // words of grp[p] written since it was last zeroed
     int64_t *qpre = nullptr, *A = nullptr;
+    int64_t *A_rep = nullptr;     // k_plan2 path: per-group copies of A and the totals
+    DevTotals *P_rep = nullptr;
+    int repl = 1;                 // FAASBAL_REPL=0: one shared copy (A/B knob)
     size_t table_cap = 0;  // entries of qcnt / qpre
     int R_cap = 0;         // entries of A
     int64_t *orphans = nullptr;
@@ -653,6 +656,9 @@ int enqueue_tick(fb_ctx *c) {
     a.qpre = c->qpre;
     a.A = c->A;
     a.P = c->P;
+    a.A_rep = c->A_rep;
+    a.P_rep = c->P_rep;
+    a.repl = (gplan && c->repl) ? 1 : 0;  // k_plan2 writes a copy per group
     a.trash = c->trash;
     a.arena = (char *)c->arena;
     a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !getenv_int("FAASBAL_NO_ARENA32")) ? 1 : 0;
@@ -858,6 +864,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->grp[1], kGrpWords);
     ap.add(&c->qpre, tab);
     ap.add(&c->A, 128);
+    ap.add(&c->A_rep, (size_t)64 * kRFused);
+    ap.add(&c->P_rep, 64);
     ap.add(&c->log_slot, F);
     ap.add(&c->orphans, F);
     if (c->deque) {
@@ -897,6 +905,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_RS_WIDE")) c->rs_wide = atoi(getenv("FAASBAL_RS_WIDE"));
     if (!rc && getenv("FAASBAL_GPLAN")) c->gplan = atoi(getenv("FAASBAL_GPLAN"));
     if (!rc && getenv("FAASBAL_EV_LL")) c->ev_ll = atoi(getenv("FAASBAL_EV_LL"));
+    if (!rc && getenv("FAASBAL_REPL")) c->repl = atoi(getenv("FAASBAL_REPL"));
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;

@@ -205,6 +205,11 @@ struct TickArgs {
     unsigned long long *csum;
     int64_t *fpre, *wpre, *qpre, *A;
     DevTotals *P;
+    // k_plan2 path: every group's workgroup writes its own copy of A and the totals, and
+    // a k_emit2 queue block reads its group's copy (no line read by every block of the grid)
+    int repl;
+    int64_t *A_rep;     // [64][128]
+    DevTotals *P_rep;   // [64]
     // outputs
     int32_t *log_slot;
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here

@@ -1707,16 +1707,18 @@ __global__ __launch_bounds__(kBS) void k_plan2(TickArgs a) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) L += __popcll(__ballot(64 * k + lane < rlim && S1v[k] <= N_eff));
         if (lane == 0) nr_s = min(L + 2, R);
-        if (g == 0) {
+        if (g == 0 || a.repl) {
+            int64_t *Ad = a.repl ? a.A_rep + (size_t)g * kRFused : a.A;
+            DevTotals *Pd = a.repl ? a.P_rep + g : a.P;
 #pragma unroll
             for (int k = 0; k < 2; ++k)
-                if (64 * k + lane < R) a.A[64 * k + lane] = (int64_t)(64 * k + lane < rlim ? Av[k] : 0u);
+                if (64 * k + lane < R) Ad[64 * k + lane] = (int64_t)(64 * k + lane < rlim ? Av[k] : 0u);
             if (lane == 0) {
-                a.P->O = O;
-                a.P->O_local = O;
-                a.P->n_evicted = nev;
-                a.P->cap_total = cap;
-                a.P->maxc = maxc;
+                Pd->O = O;
+                Pd->O_local = O;
+                Pd->n_evicted = nev;
+                Pd->cap_total = cap;
+                Pd->maxc = maxc;
             }
         }
     }
@@ -2119,14 +2121,16 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             }
             O = 0; nev = 0; cap = 1ll << 40; maxc = R;
 #else
+            const int64_t *Ar = a.repl ? a.A_rep + (size_t)(b >> a.gshift) * kRFused : a.A;
+            const DevTotals *Pr = a.repl ? a.P_rep + (b >> a.gshift) : a.P;
             if ((int)threadIdx.x < R) {
                 pre_c[threadIdx.x] = (uint32_t)a.qpre[(size_t)b * R + threadIdx.x];
-                tot_f[threadIdx.x] = (uint32_t)a.A[threadIdx.x];
+                tot_f[threadIdx.x] = (uint32_t)Ar[threadIdx.x];
             }
-            O = a.P->O;
-            nev = a.P->n_evicted;
-            cap = a.P->cap_total;
-            maxc = a.P->maxc;
+            O = Pr->O;
+            nev = Pr->n_evicted;
+            cap = Pr->cap_total;
+            maxc = Pr->maxc;
 #endif
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
