@@ -135,6 +135,7 @@ struct fb_ctx {
     int ev_ll = 1;                          // FAASBAL_EV_LL=0: always the radix sort (A/B knob)
     bool l_resort = false;                  // this tick reruns through the sort (a slot had > kLinkMax messages)
     bool l_used_ll = false;                 // the last enqueue grouped by linked lists
+    int purge_apply = 1;                    // FAASBAL_PURGE_APPLY=0: the slot purge stays in k_scan (A/B knob)
     void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
     // device event arrays, double-buffered like the pinned halves: fb_tick_stage copies
     // half h on its own stream (overlapping a running tick), the launch waits for it
@@ -419,52 +420,128 @@ int enqueue_tick(fb_ctx *c) {
         evs = c->xbuf + xl.evs;
         if (c->phase != 2) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
     }
+    TickArgs a{};
+    a.W = W;
+    a.E = E;
+    a.R = R;
+    a.nbw = nbw;
+    a.nbf = c->deque ? 0 : nbf;  // start(): nobody dies, no log scan
+    a.nbq = nbq;
+    a.deque = c->deque;
+    a.redist = c->l_purge_only ? 0 : 1;
+    a.q_cap = c->Wq_cap;
+    a.tokcnt_in = c->tokcnt[cur];
+    a.xw_in = c->xw[cur];
+    a.kl_in = c->kl[cur];
+    a.qrank_in = c->qrank[cur];
+    a.front_rank = c->front_rank;
+    a.back_rank = c->back_rank;
+    a.post_tok = c->post_tok;
+    a.post_nf = c->post_nf;
+    a.c_tok = c->c_tok;
+    a.tokcnt_out = c->tokcnt[nxt];
+    a.xw_out = c->xw[nxt];
+    a.kl_out = c->kl[nxt];
+    a.qrank_out = c->qrank[nxt];
+    // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
+    // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
+    a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
+    // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
+    a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
+    a.cfirst = c->emit_cfirst;
+    // large tables for k_emit2: group rows too, scanned by k_plan2 (FAASBAL_GPLAN=0: k_plan)
+    const bool gplan = !a.fused && a.segw && !c->shard && c->gplan;
+    if (a.fused || gplan) {
+        // group rows: fused, about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads
+        // both); k_plan2, the smallest groups that make at most 64 rows (one workgroup each)
+        int gs = 0;
+        if (a.fused)
+            while ((1 << (2 * gs)) < nbq) ++gs;
+        else
+            while (cdiv(nbq, (int64_t)1 << gs) > 64) ++gs;
+        a.grp_on = 1;
+        a.gshift = gs;
+        a.gstride = R + 4;
+        a.ngrp = (int)cdiv(nbq, 1 << gs);
+        if (a.ngrp > 64 || (int64_t)a.ngrp * a.gstride > kGrpWords)
+            return fail(c, FB_ERANGE, "group rows (%d x %d words) exceed the reservation", a.ngrp, a.gstride);
+        c->gpar ^= 1;
+        a.grp = c->grp[c->gpar];  // zero: its last user's k_emit2 cleared it
+        a.grp_zero = c->grp[c->gpar ^ 1];
+        a.zero_words = c->gdirty[c->gpar ^ 1];
+        c->gdirty[c->gpar ^ 1] = 0;
+        c->gdirty[c->gpar] = a.ngrp * a.gstride;
+    }
+    a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
+    // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
+    // (2 MB of records) those gathers miss L2, so k_slots first writes the
+    // died bitmap (W/8 bytes, L2-resident) and the scan tests bits instead
+    a.slots_in_scan = (c->split_slots > 0 || (c->split_slots < 0 && W > kLdsBitmapSlots)) ? 0 : 1;
+    // ... or better, while the bitmap fits in one workgroup's LDS: the W-role of
+    // k_scan writes it and k_logscan tests every entry against an LDS copy
+    const size_t bm_bytes = (size_t)(((W + 63) / 64 + 1) / 2 + 1) * 16;
+    a.f_sep = (head > 0 && !c->deque && (c->logscan > 0 || (c->logscan < 0 && W > kLdsBitmapSlots)) &&
+               bm_bytes <= (size_t)c->max_lds && !(c->shard && c->phase == 2)) ? 1 : 0;
+    if (a.f_sep) a.slots_in_scan = 1;
+    const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
     c->l_used_ll = false;
     const bool ll = E > 0 && c->ev_head && c->ev_ll && !c->l_resort;
     if (!ll && (rc = flush_commit(c))) return rc;
     if (ll) {
         // group the messages per slot by linked lists (no sort): two launches
-        EvArgs a{};
-        a.E = E;
-        a.W = W;
-        a.tick = c->tick;
-        a.tte = c->l_tte;
-        a.head_in = head;
-        a.ev_kind = c->ev_kind;
-        a.ev_val = c->ev_val;
-        a.ev_ts = c->ev_ts;
-        a.ev_seq = c->ev_seq;
-        a.ev_status = evs;
-        a.reg = c->reg;
-        a.free_in = c->free_[cur];
-        a.hb = c->hb;
-        a.epoch = c->epoch;
-        a.log_slot = c->log_slot;
-        a.post = c->post;
-        a.post_rf = c->post_rf;
-        a.touched = c->touched;
-        a.tbits = c->tbits;
-        a.tbits_words = c->tbits ? (int)cdiv(W, 32) : 0;
-        a.front_list = front;
-        a.back_list = back;
-        a.ev_slot = c->ev_slot;
-        a.ev_head = c->ev_head;
-        a.ev_next = c->ev_next;
+        EvArgs ea{};
+        ea.E = E;
+        ea.W = W;
+        ea.tick = c->tick;
+        ea.tte = c->l_tte;
+        ea.head_in = head;
+        ea.ev_kind = c->ev_kind;
+        ea.ev_val = c->ev_val;
+        ea.ev_ts = c->ev_ts;
+        ea.ev_seq = c->ev_seq;
+        ea.ev_status = evs;
+        ea.reg = c->reg;
+        ea.free_in = c->free_[cur];
+        ea.hb = c->hb;
+        ea.epoch = c->epoch;
+        ea.log_slot = c->log_slot;
+        ea.post = c->post;
+        ea.post_rf = c->post_rf;
+        ea.touched = c->touched;
+        ea.tbits = c->tbits;
+        ea.tbits_words = c->tbits ? (int)cdiv(W, 32) : 0;
+        ea.front_list = front;
+        ea.back_list = back;
+        ea.ev_slot = c->ev_slot;
+        ea.ev_head = c->ev_head;
+        ea.ev_next = c->ev_next;
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
-        a.link = c->link;
-        a.hout = c->hout_dev;
+        ea.link = c->link;
+        ea.hout = c->hout_dev;
         if (c->cm_pending) {  // the previous tick's commit rides in this launch
-            a.cm = c->cm;
-            a.cm_blocks = c->cm_grid;
+            ea.cm = c->cm;
+            ea.cm_blocks = c->cm_grid;
             c->cm_pending = false;
         }
+        // the slot purge (k_scan's W role) runs in k_ev_apply_ll's launch: extra blocks for
+        // the untouched slots, each owner thread for its touched slot
+        ea.nbw = c->purge_apply ? nbw : 0;
+        ea.now = c->l_now;
+        ea.st = c->st;
+        ea.free_out = c->free_[nxt];
+        ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep)) ? c->dmask : nullptr;
+        ea.wcnt = c->wcnt;
+        ea.grp = a.grp_on ? a.grp : nullptr;
+        ea.ngrp = a.ngrp;
+        ea.gstride = a.gstride;
+        ea.R = R;
         c->l_used_ll = true;
         {
             Timer t(c, "ev_link");
-            launch_ev_link(a, t.st());
+            launch_ev_link(ea, t.st());
         }
         Timer t(c, "ev_apply");
-        launch_ev_apply_ll(a, t.st());
+        launch_ev_apply_ll(ea, t.st());
     } else if (E > 0 && !(c->shard && c->phase == 2)) {
 
         // stable radix sort of events by slot
@@ -551,70 +628,7 @@ int enqueue_tick(fb_ctx *c) {
         Timer t(c, "ev_apply");
         launch_ev_apply(a, t.st());
     }
-    TickArgs a{};
-    a.W = W;
-    a.E = E;
-    a.R = R;
-    a.nbw = nbw;
-    a.nbf = c->deque ? 0 : nbf;  // start(): nobody dies, no log scan
-    a.nbq = nbq;
-    a.deque = c->deque;
-    a.redist = c->l_purge_only ? 0 : 1;
-    a.q_cap = c->Wq_cap;
-    a.tokcnt_in = c->tokcnt[cur];
-    a.xw_in = c->xw[cur];
-    a.kl_in = c->kl[cur];
-    a.qrank_in = c->qrank[cur];
-    a.front_rank = c->front_rank;
-    a.back_rank = c->back_rank;
-    a.post_tok = c->post_tok;
-    a.post_nf = c->post_nf;
-    a.c_tok = c->c_tok;
-    a.tokcnt_out = c->tokcnt[nxt];
-    a.xw_out = c->xw[nxt];
-    a.kl_out = c->kl[nxt];
-    a.qrank_out = c->qrank[nxt];
-    // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
-    // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
-    a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
-    // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
-    a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
-    a.cfirst = c->emit_cfirst;
-    // large tables for k_emit2: group rows too, scanned by k_plan2 (FAASBAL_GPLAN=0: k_plan)
-    const bool gplan = !a.fused && a.segw && !c->shard && c->gplan;
-    if (a.fused || gplan) {
-        // group rows: fused, about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads
-        // both); k_plan2, the smallest groups that make at most 64 rows (one workgroup each)
-        int gs = 0;
-        if (a.fused)
-            while ((1 << (2 * gs)) < nbq) ++gs;
-        else
-            while (cdiv(nbq, (int64_t)1 << gs) > 64) ++gs;
-        a.grp_on = 1;
-        a.gshift = gs;
-        a.gstride = R + 4;
-        a.ngrp = (int)cdiv(nbq, 1 << gs);
-        if (a.ngrp > 64 || (int64_t)a.ngrp * a.gstride > kGrpWords)
-            return fail(c, FB_ERANGE, "group rows (%d x %d words) exceed the reservation", a.ngrp, a.gstride);
-        c->gpar ^= 1;
-        a.grp = c->grp[c->gpar];  // zero: its last user's k_emit2 cleared it
-        a.grp_zero = c->grp[c->gpar ^ 1];
-        a.zero_words = c->gdirty[c->gpar ^ 1];
-        c->gdirty[c->gpar ^ 1] = 0;
-        c->gdirty[c->gpar] = a.ngrp * a.gstride;
-    }
-    a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
-    // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
-    // (2 MB of records) those gathers miss L2, so k_slots first writes the
-    // died bitmap (W/8 bytes, L2-resident) and the scan tests bits instead
-    a.slots_in_scan = (c->split_slots > 0 || (c->split_slots < 0 && W > kLdsBitmapSlots)) ? 0 : 1;
-    // ... or better, while the bitmap fits in one workgroup's LDS: the W-role of
-    // k_scan writes it and k_logscan tests every entry against an LDS copy
-    const size_t bm_bytes = (size_t)(((W + 63) / 64 + 1) / 2 + 1) * 16;
-    a.f_sep = (head > 0 && !c->deque && (c->logscan > 0 || (c->logscan < 0 && W > kLdsBitmapSlots)) &&
-               bm_bytes <= (size_t)c->max_lds && !(c->shard && c->phase == 2)) ? 1 : 0;
-    if (a.f_sep) a.slots_in_scan = 1;
-    const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
+    a.slots_in_apply = (c->l_used_ll && c->purge_apply) ? 1 : 0;
     a.dbg_stop = c->dbg_stop;
     a.tick = c->tick;
     a.now = c->l_now;
@@ -734,7 +748,7 @@ int enqueue_tick(fb_ctx *c) {
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
-    if (!a.slots_in_scan) {
+    if (!a.slots_in_scan && !a.slots_in_apply) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
     }
@@ -906,6 +920,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_GPLAN")) c->gplan = atoi(getenv("FAASBAL_GPLAN"));
     if (!rc && getenv("FAASBAL_EV_LL")) c->ev_ll = atoi(getenv("FAASBAL_EV_LL"));
     if (!rc && getenv("FAASBAL_REPL")) c->repl = atoi(getenv("FAASBAL_REPL"));
+    if (!rc && getenv("FAASBAL_PURGE_APPLY")) c->purge_apply = atoi(getenv("FAASBAL_PURGE_APPLY"));
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;

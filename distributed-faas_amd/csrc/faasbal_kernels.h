@@ -145,6 +145,16 @@ struct EvArgs {
     // the previous tick's deferred commit, run by k_ev_link's blocks past the link grid
     int cm_blocks;
     CommitArgs cm;
+    // the slot purge (k_scan's W role) in k_ev_apply_ll's launch: nbw blocks past the
+    // apply grid purge the untouched slots, each owner thread its touched slot
+    int nbw;
+    double now;
+    uint8_t *st;
+    int2 *free_out;
+    unsigned long long *dmask;  // died bitmap (null: not needed), zeroed by k_ev_link, atomicOr
+    uint32_t *wcnt;             // evictions per 256-slot tile, zeroed by k_ev_link, atomicAdd
+    uint32_t *grp;              // group rows (null: none); evictions into column R + 2
+    int ngrp, gstride, R;
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -192,6 +202,7 @@ struct TickArgs {
     const PostRec *post;
     const uint8_t *post_rf;
     int ffirst;     // k_scan: log blocks before queue blocks in the grid (A/B knob FAASBAL_SCAN_FFIRST)
+    int slots_in_apply;  // the slot purge ran in k_ev_apply_ll's launch: k_scan has no W blocks
     int post_lazy;  // 1: the slot purge loads post records only for touched slots (large tables)
     const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates

@@ -695,6 +695,8 @@ struct SlotRun {
         }
         a.ev_status[i] = status;
     }
+    // the purge at the tick's clock of this touched slot (k_ev_apply_ll's launch)
+    __device__ __forceinline__ void purge(const EvArgs &a, uint32_t s, int reg0);
     __device__ __forceinline__ void finish(const EvArgs &a, uint32_t s, uint32_t gs) {
         a.post[s] = PostRec{hb, fr, epoch};
         a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1));
@@ -789,6 +791,10 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
     const int t = blockIdx.x * kBS + (int)threadIdx.x, nt = lb * kBS;
     if (t == 0) a.hout->resort = 0;
     for (int w = t; w < a.tbits_words; w += nt) a.tbits[w] = 0u;
+    // the counters k_ev_apply_ll's slot purge accumulates with atomics
+    for (int w = t; w < a.nbw; w += nt) a.wcnt[w] = 0u;
+    if (a.dmask)
+        for (int w = t; w < (a.W + 63) >> 6; w += nt) a.dmask[w] = 0ull;
     if (t < a.E) {
         const uint32_t s = (uint32_t)a.ev_slot[t];
         a.front_list[t] = 0;
@@ -806,7 +812,54 @@ __device__ __forceinline__ int32_t log_peek(const EvArgs &a, int64_t seq) {
     return a.head_in > 0 ? a.log_slot[q] : -1;
 }
 
+// purge_workers (:241-249) at the tick's clock for one slot, as k_scan's slots_body
+// (task_dispatcher.py:209-212 for liveness): status byte, next {free, queued}, the
+// died-at-start bit and the eviction count.  Untouched slots (t = false) from the
+// committed record, touched ones from the owner thread's post-message registers.
+__device__ __forceinline__ void purge_slot(const EvArgs &a, int s, bool t, int reg0, int reg, double hb, int32_t fr,
+                                           int died_flag, bool queued_if_alive, bool &died, bool &evicted) {
+    const bool dead = reg && ((a.now - hb) > a.tte);
+    const bool alive = reg && !dead;
+    died = reg0 && (dead || died_flag);
+    evicted = (reg0 || t) && !alive;
+    a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
+    a.free_out[s] = make_int2(alive ? fr : INT32_MIN, (alive && queued_if_alive) ? 1 : 0);
+}
+__device__ __forceinline__ void count_evicted(const EvArgs &a, int tile, uint32_t n) {
+    atomicAdd(&a.wcnt[tile], n);
+    if (FAASBAL_GRP_OW && a.grp) atomicAdd(&a.grp[(tile % a.ngrp) * a.gstride + a.R + 2], n);
+}
+
+__device__ __forceinline__ void SlotRun::purge(const EvArgs &a, uint32_t s, int reg0) {
+    bool died, evicted;
+    purge_slot(a, (int)s, true, reg0, reg, hb, fr, died_start, qstat != kQsOut, died, evicted);
+    if (died && a.dmask) atomicOr(&a.dmask[s >> 6], 1ull << (s & 63));
+    if (evicted) count_evicted(a, (int)(s >> 8), 1u);
+}
+
 __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
+    const int nba = (int)gridDim.x - a.nbw;  // apply blocks; the rest purge untouched slots
+    if ((int)blockIdx.x >= nba) {
+        const int blk = (int)blockIdx.x - nba;
+        const int s = blk * kBS + (int)threadIdx.x;
+        bool died = false, evicted = false;
+        if (s < a.W) {
+            // the link stamp says whether the slot got messages (its owner purges it); the
+            // committed record loaded with it (no dependent round)
+            const bool t = (uint32_t)(a.ev_head[s] >> 32) == a.link;
+            const int reg0 = a.reg[s];
+            const double hb0 = a.hb[s];
+            const int2 fq0 = a.free_in[s];
+            if (!t) purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, died, evicted);
+        }
+        const uint64_t dm = __ballot(died);
+        const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
+        if (lane_id() == 0) {
+            if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
+            if (ne) count_evicted(a, blk, ne);
+        }
+        return;
+    }
     const int e = blockIdx.x * kBS + threadIdx.x;
     if (e >= a.E) return;
     // slot, link and payload of this message in one load round
@@ -822,9 +875,11 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     const int32_t logv0 = log_peek(a, seq0);
     SlotRun r;
     r.init(a, s);
+    const int reg0 = r.reg;
     if (hidx == e) {  // the slot's only message (most slots)
         r.step<true>(a, s, e, kind0, val0, ts0, seq0, logv0);
         r.finish(a, s, s);
+        if (a.nbw) r.purge(a, s, reg0);
         return;
     }
     // walk head -> ... -> e (link order), each message's payload loaded with its link
@@ -897,6 +952,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
         }
     }
     r.finish(a, s, s);
+    if (a.nbw) r.purge(a, s, reg0);
 }
 
 
@@ -2678,7 +2734,7 @@ void launch_ev_link(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_link, dim3(grid + a.cm_blocks), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
     hipExtLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st.s, st.e0, st.e1, 0, err, seed);
@@ -2697,7 +2753,7 @@ void launch_slots(const TickArgs &a, Stream st) {
 }
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
-    const int nbw = (a.shard == 2 || !a.slots_in_scan) ? 0 : a.nbw;
+    const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : a.nbw;
     const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;
     FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
 }

@@ -531,3 +531,18 @@ def test_event_sort_fused_histograms(radix, monkeypatch, W, E, wide):
     monkeypatch.setenv("FAASBAL_RS_FUSE", "1")
     monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
     _sort_tick(W, E, 0.3, W + E + 1, purge_mode=2)
+
+@pytest.fixture
+def purge_in_scan(monkeypatch):
+    """FAASBAL_PURGE_APPLY=0: message ticks purge the slots in k_scan's W role (as
+    before the purge moved into k_ev_apply_ll's launch)."""
+    monkeypatch.setenv("FAASBAL_PURGE_APPLY", "0")
+
+
+@pytest.mark.parametrize("seed", range(3))
+def test_random_multitick_purge_in_scan(purge_in_scan, seed):
+    test_random_multitick_vs_oracle(seed)
+
+
+def test_churn_stream_purge_in_scan(purge_in_scan):
+    test_churn_stream_vs_oracle()
