@@ -144,6 +144,11 @@ struct fb_ctx {
     double *evt[2] = {nullptr, nullptr};
     int64_t *evq[2] = {nullptr, nullptr};
     hipStream_t cp_s = nullptr;                         // H2D copies of staged events
+    // k_logscan beside k_scan: both read only what k_ev_apply_ll's launch wrote (the
+    // died bitmap, the post-message records), k_plan2 waits for both
+    hipStream_t side_s = nullptr;
+    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
+    int fork = 0;                                       // FAASBAL_FORK=1: the side stream (measured slower)
     hipEvent_t stage_ev[2] = {nullptr, nullptr};        // copies of half h done (on cp_s)
     hipEvent_t use_ev[2] = {nullptr, nullptr};          // the tick reading device half h done
     bool stage_rec[2] = {false, false}, use_rec[2] = {false, false};
@@ -752,11 +757,23 @@ int enqueue_tick(fb_ctx *c) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
     }
+    // the died bitmap is complete before k_scan when the purge ran in the apply launch:
+    // the log scan then runs beside the queue scan on a second stream
+    const bool fork = a.f_sep && a.slots_in_apply && c->fork;
+    if (fork) {
+        HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
+        HIPCHK(c, hipStreamWaitEvent(c->side_s, c->fork_ev, 0));
+        Timer t(c, "logscan");
+        launch_logscan(a, ls_grid, Stream(c->side_s, t.a, t.b));
+        HIPCHK(c, hipEventRecord(c->join_ev, c->side_s));
+    }
     {
         Timer t(c, "scan");
         launch_scan(a, t.st());
     }
-    if (a.f_sep) {
+    if (fork) {
+        HIPCHK(c, hipStreamWaitEvent(c->stream, c->join_ev, 0));
+    } else if (a.f_sep) {
         Timer t(c, "logscan");
         launch_logscan(a, ls_grid, t.st());
     }
@@ -932,6 +949,11 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
             hipEventCreateWithFlags(&c->use_ev[h], hipEventDisableTiming) != hipSuccess)
             rc = FB_EHIP;
     if (!rc && hipStreamCreateWithFlags(&c->cp_s, hipStreamNonBlocking) != hipSuccess) rc = FB_EHIP;
+    if (!rc && (hipStreamCreateWithFlags(&c->side_s, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess))
+        rc = FB_EHIP;
+    if (!rc && getenv("FAASBAL_FORK")) c->fork = atoi(getenv("FAASBAL_FORK"));
     if (!rc) {
         int nt = getenv("FAASBAL_STAGE_THREADS") ? atoi(getenv("FAASBAL_STAGE_THREADS")) : 4;
         nt = std::max(1, std::min(nt, 16));
@@ -999,6 +1021,12 @@ int fb_destroy(fb_ctx *c) {
         if (c->use_ev[h]) hipEventDestroy(c->use_ev[h]);
     }
     if (c->cp_s) hipStreamDestroy(c->cp_s);
+    if (c->side_s) {
+        hipStreamSynchronize(c->side_s);
+        hipStreamDestroy(c->side_s);
+    }
+    if (c->fork_ev) hipEventDestroy(c->fork_ev);
+    if (c->join_ev) hipEventDestroy(c->join_ev);
     for (auto &t : c->tl) {
         hipEventDestroy(t.a);
         hipEventDestroy(t.b);

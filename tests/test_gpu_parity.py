@@ -546,3 +546,10 @@ def test_random_multitick_purge_in_scan(purge_in_scan, seed):
 
 def test_churn_stream_purge_in_scan(purge_in_scan):
     test_churn_stream_vs_oracle()
+
+
+def test_churn_stream_side_stream(monkeypatch):
+    """FAASBAL_FORK=1: k_logscan beside k_scan on a second stream (joined before k_plan2)."""
+    monkeypatch.setenv("FAASBAL_FORK", "1")
+    monkeypatch.setenv("FAASBAL_LOGSCAN", "1")
+    test_churn_stream_vs_oracle()
