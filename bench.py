@@ -323,7 +323,18 @@ def main():
         import torch.distributed as dist
         dev = local % max(1, torch.cuda.device_count())
         torch.cuda.set_device(dev)
-        dist.init_process_group(args.backend, device_id=torch.device("cuda", dev) if args.backend == "nccl" else None)
+        # the communication libraries print connection banners on stdout (gloo: "Rank 0 is
+        # connected to ..."); keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group(args.backend, device_id=torch.device("cuda", dev) if args.backend == "nccl" else None)
+            dist.barrier()
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
         if dist.get_world_size() != args.gpus:
             raise SystemExit("torch.distributed reports %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
 
