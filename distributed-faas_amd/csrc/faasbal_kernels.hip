@@ -331,6 +331,28 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
     return tot;
 }
 
+// The compiler loads a by-value argument block lazily: a field's scalar load is
+// placed before its first use, so a kernel whose hot path needs fields spread over
+// the ~1 KB block pays one scalar-cache miss round per newly touched 64-byte line,
+// in dependent rounds.  Touching one dword of every line up front (a value the
+// kernel then depends on) puts the whole block into the scalar cache in one round;
+// the later field loads hit it.  (FAASBAL_KA_PREFETCH=0: off, A/B knob.)
+#ifndef FAASBAL_KA_PREFETCH
+#define FAASBAL_KA_PREFETCH 1
+#endif
+template <class A>
+__device__ __forceinline__ void prefetch_args(const A &a) {
+    if constexpr (FAASBAL_KA_PREFETCH) {
+        constexpr int nl = (int)((sizeof(A) + 63) / 64);
+        const uint32_t *w = reinterpret_cast<const uint32_t *>(&a);
+        uint32_t x = 0;
+#pragma unroll
+        for (int i = 0; i < nl; ++i) x ^= w[i * 16];
+        // never true (no grid has 2^31 - 1 blocks): only makes the loads necessary here
+        if (blockIdx.x == 0x7fffffffu && x == 0x9e3779b9u) __builtin_trap();
+    }
+}
+
 // ---------------------------------------------------------------- radix sort
 // Stable LSD radix sort of (key = slot, val = event index), `db`-bit digits
 // (db <= log2 NB).  NB = 256 for 8-bit passes; 1024 / 2048 let a 20-bit slot
@@ -708,6 +730,7 @@ struct SlotRun {
 };
 
 __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
+    prefetch_args(a);
     const int j = blockIdx.x * kBS + threadIdx.x;
     if (j >= a.E) return;
     // this position's key, its neighbours and its event index in one load round
@@ -769,7 +792,10 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
     }
 }
 
-__global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) { commit_body(a, blockIdx.x); }
+__global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
+    prefetch_args(a);
+    commit_body(a, blockIdx.x);
+}
 
 // ------------------------------------------------------------ event grouping without a sort
 // One GPU, heartbeat loop: the messages of a slot are grouped by a linked list
@@ -783,6 +809,7 @@ __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) { commit_body(a, b
 // clears: this tick's front / back lists and the touched bitmap.
 constexpr int kLinkMax = 16;
 __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
+    prefetch_args(a);
     const int lb = (int)gridDim.x - a.cm_blocks;  // link blocks; the rest commit the previous tick
     if ((int)blockIdx.x >= lb) {
         commit_body(a.cm, (int)blockIdx.x - lb);
@@ -838,6 +865,7 @@ __device__ __forceinline__ void SlotRun::purge(const EvArgs &a, uint32_t s, int 
 }
 
 __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
+    prefetch_args(a);
     const int nba = (int)gridDim.x - a.nbw;  // apply blocks; the rest purge untouched slots
     if ((int)blockIdx.x >= nba) {
         const int blk = (int)blockIdx.x - nba;
@@ -1112,6 +1140,7 @@ __device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int
 // whole block once at entry instead of one scalar fetch (and wait) per field at
 // its first use.
 constexpr int kModeIdle = 0, kModeEvents = 1, kModeDeque = 2;
+
 template <int MODE>
 __device__ __forceinline__ TickArgs specialise(TickArgs a) {
     if (MODE == kModeIdle) a.E = 0;
@@ -1159,6 +1188,7 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
 
 template <int MODE>
 __global__ __launch_bounds__(kBS) void k_slots(TickArgs a_) {
+    prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
     __shared__ uint32_t l4[kWaves];
     STAMP(a, 0, 0);
@@ -1183,6 +1213,7 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
 template <int MODE>
 __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     STAMP_TOP(a_, a_.nbw);
+    prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
     extern __shared__ __attribute__((aligned(16))) unsigned long long dyn[];
     __shared__ uint32_t l4[kWaves];
@@ -1523,6 +1554,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
 // groups of 8 consecutive entries, 8 int4 loads in flight), with k_scan's
 // per-tile ofl / fcnt layout so k_emit's orphan compaction is unchanged.
 __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
+    prefetch_args(a);
     extern __shared__ __attribute__((aligned(16))) unsigned long long bm[];
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows
     STAMP(a, SO, 0);
@@ -1595,6 +1627,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
 // wg 0: orphan block offsets + O; wg 1: evicted block offsets; wg 2: max c and
 // capacity; wg 3+r: exclusive scan of round r's counts across queue blocks.
 __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
+    prefetch_args(a);
     __shared__ unsigned long long l4[kWaves];
     __shared__ int32_t m4[kWaves];
     const int bid = blockIdx.x;
@@ -1676,6 +1709,7 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
 constexpr int kGrpLd = 4;     // group / block row loads per thread per batch (k_plan2, k_emit2)
 constexpr int kP2Rows = kBS;  // rows per pass of a group's scan (one per thread)
 __global__ __launch_bounds__(kBS) void k_plan2(TickArgs a) {
+    prefetch_args(a);
     __shared__ unsigned long long l4[kWaves];
     __shared__ uint32_t gpre[kBS], gtot[kBS];
     __shared__ uint32_t gp_r[kRFused];           // prefix of the earlier groups, round r
@@ -1850,6 +1884,7 @@ struct EmitLds {
 
 template <int MODE>
 __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
+    prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
     __shared__ EmitLds E_;
     __shared__ uint32_t red[kWaves][4];
@@ -2097,6 +2132,7 @@ __device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
 template <int MODE, bool PLAN, int NCH>
 __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     STAMP_TOP(a_, a_.nbw + a_.nbf + a_.nbq + (a_.slots_in_scan ? a_.nbw : 0));
+    prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
     __shared__ uint32_t gpre[kBS], gtot[kBS];  // per-thread partials of (round, part)
     __shared__ uint32_t red[kWaves][4];
@@ -2497,6 +2533,7 @@ constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // log position), one register per 64 rounds, read with readlane in the round
 // loop; block prefixes from k_plan, segment counts from the phase-2 k_scan.
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
+    prefetch_args(a);
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
     if (bid < a.nbq) {
