@@ -302,5 +302,7 @@ void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);
 void launch_emit_shard(const TickArgs &a, Stream st);
 void launch_commit(const CommitArgs &a, int grid, Stream st);
+// dst[i] = src[i], i < n (dst may be host memory mapped for the device: stores cross PCIe)
+void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st);
 
 }  // namespace fb

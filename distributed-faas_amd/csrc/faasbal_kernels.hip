@@ -2731,6 +2731,38 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
 }
 
 
+// ------------------------------------------------------------ readback
+// Words to (host-mapped) memory: lane j of a pass moves words 4j .. 4j + 3 -- four
+// 4-byte loads (any source alignment), one 16-byte store (dst is 16-byte aligned in
+// the callers' pinned buffers; else word stores) -- so a wave store is one 1 KB burst
+// across PCIe; two passes per thread in flight.
+__global__ __launch_bounds__(kBS) void k_copy_words(uint32_t *__restrict__ dst, const uint32_t *__restrict__ src,
+                                                   int64_t n) {
+    const bool al = (reinterpret_cast<uintptr_t>(dst) & 15) == 0;
+    const int64_t stride = (int64_t)gridDim.x * kBS * 8;
+    for (int64_t q0 = ((int64_t)blockIdx.x * kBS * 2 + threadIdx.x) * 4; q0 < n; q0 += stride) {
+        uint32_t v[2][4];
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const int64_t i = q0 + (int64_t)p * kBS * 4 + k;
+                v[p][k] = src[i < n ? i : n - 1];
+            }
+#pragma unroll
+        for (int p = 0; p < 2; ++p) {
+            const int64_t i = q0 + (int64_t)p * kBS * 4;
+            if (al && i + 3 < n) {
+                *reinterpret_cast<uint4 *>(dst + i) = make_uint4(v[p][0], v[p][1], v[p][2], v[p][3]);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+                    if (i + k < n) dst[i + k] = v[p][k];
+            }
+        }
+    }
+}
+
 }  // namespace fb
 
 // ------------------------------------------------------------ launchers
@@ -2772,6 +2804,10 @@ void launch_ev_link(const EvArgs &a, Stream st) {
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+}
+void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st) {
+    const int grid = (int)std::min<int64_t>(std::max<int64_t>(1, (n + 8 * kBS - 1) / (8 * kBS)), 2048);
+    hipExtLaunchKernelGGL(k_copy_words, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, dst, src, n);
 }
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
     hipExtLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st.s, st.e0, st.e1, 0, err, seed);
