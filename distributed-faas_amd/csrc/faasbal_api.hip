@@ -135,7 +135,10 @@ struct fb_ctx {
     int ev_ll = 1;                          // FAASBAL_EV_LL=0: always the radix sort (A/B knob)
     bool l_resort = false;                  // this tick reruns through the sort (a slot had > kLinkMax messages)
     bool l_used_ll = false;                 // the last enqueue grouped by linked lists
-    int purge_apply = 1;                    // FAASBAL_PURGE_APPLY=0: the slot purge stays in k_scan (A/B knob)
+    int purge_apply = 1;
+    // A/B knobs read once at creation (not per launch): FAASBAL_SCAN_FFIRST,
+    // FAASBAL_POST_EAGER, FAASBAL_NO_ARENA32
+    int scan_ffirst = 0, post_eager = 0, no_arena32 = 0;                    // FAASBAL_PURGE_APPLY=0: the slot purge stays in k_scan (A/B knob)
     void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
     // device event arrays, double-buffered like the pinned halves: fb_tick_stage copies
     // half h on its own stream (overlapping a running tick), the launch waits for it
@@ -656,8 +659,8 @@ int enqueue_tick(fb_ctx *c) {
     a.post = c->post;
     a.post_rf = c->post_rf;
     // past the L2-resident sizes the purge is bandwidth-bound: skip untouched post records
-    a.ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
-    a.post_lazy = (W > kLdsBitmapSlots && getenv_int("FAASBAL_POST_EAGER") == 0) ? 1 : 0;
+    a.ffirst = c->scan_ffirst;
+    a.post_lazy = (W > kLdsBitmapSlots && !c->post_eager) ? 1 : 0;
     a.front_list = front;
     a.back_list = back;
     a.st = c->st;
@@ -681,7 +684,7 @@ int enqueue_tick(fb_ctx *c) {
     a.repl = (gplan && c->repl) ? 1 : 0;  // k_plan2 writes a copy per group
     a.trash = c->trash;
     a.arena = (char *)c->arena;
-    a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !getenv_int("FAASBAL_NO_ARENA32")) ? 1 : 0;
+    a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !c->no_arena32) ? 1 : 0;
     a.log_slot = c->log_slot;
     a.free_out = c->free_[nxt];
     a.queue_out = c->queue[nxt];
@@ -939,6 +942,11 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_EV_LL")) c->ev_ll = atoi(getenv("FAASBAL_EV_LL"));
     if (!rc && getenv("FAASBAL_REPL")) c->repl = atoi(getenv("FAASBAL_REPL"));
     if (!rc && getenv("FAASBAL_PURGE_APPLY")) c->purge_apply = atoi(getenv("FAASBAL_PURGE_APPLY"));
+    if (!rc) {
+        c->scan_ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
+        c->post_eager = getenv_int("FAASBAL_POST_EAGER");
+        c->no_arena32 = getenv_int("FAASBAL_NO_ARENA32");
+    }
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;
