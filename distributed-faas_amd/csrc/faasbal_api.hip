@@ -295,6 +295,15 @@ int arena_commit(fb_ctx *c, ArenaPlan &ap) {
     hipError_t e = hipMalloc(&c->arena, total);
     if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(arena %zu B) failed: %s", total, hipGetErrorString(e));
     c->arena_bytes = total;
+    // Every byte written once: some kernels read words no tick has written yet (a
+    // round table's rows past the fill level, tail padding), and reads of never-written
+    // device memory measured 25 -> 37 us on the streaming emit in some processes
+    // (the pages' first writer, not this code, decided).  FAASBAL_ARENA_ZERO=0: off.
+    if (!getenv("FAASBAL_ARENA_ZERO") || atoi(getenv("FAASBAL_ARENA_ZERO"))) {
+        e = hipMemset(c->arena, 0, total);
+        if (e == hipSuccess) e = hipDeviceSynchronize();
+        if (e != hipSuccess) return fail(c, FB_EHIP, "hipMemset(arena) failed: %s", hipGetErrorString(e));
+    }
     char *p = (char *)c->arena;
     i = 0;
     for (auto &r : ap.req) {
@@ -353,6 +362,8 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
         c->qpre = nullptr;
         int rc;
         if ((rc = dalloc(c, &c->qcnt, cap)) || (rc = dalloc(c, &c->qpre, cap))) return rc;
+        HIPCHK(c, hipMemset(c->qcnt, 0, cap * sizeof(uint32_t)));
+        HIPCHK(c, hipMemset(c->qpre, 0, cap * sizeof(int64_t)));
         c->table_cap = cap;
         c->table_owned = true;
     }
