@@ -295,10 +295,10 @@ int arena_commit(fb_ctx *c, ArenaPlan &ap) {
     hipError_t e = hipMalloc(&c->arena, total);
     if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(arena %zu B) failed: %s", total, hipGetErrorString(e));
     c->arena_bytes = total;
-    // Every byte written once: some kernels read words no tick has written yet (a
-    // round table's rows past the fill level, tail padding), and reads of never-written
-    // device memory measured 25 -> 37 us on the streaming emit in some processes
-    // (the pages' first writer, not this code, decided).  FAASBAL_ARENA_ZERO=0: off.
+    // Every byte written once: some kernels load words no tick has written yet (a
+    // round table's rows past the fill level, tail padding) and discard them; zeroing
+    // makes those loads deterministic (FAASBAL_ARENA_ZERO=0: off).  It did not change
+    // the streaming emit's two timing modes (profiles/NOTES_r02.md).
     if (!getenv("FAASBAL_ARENA_ZERO") || atoi(getenv("FAASBAL_ARENA_ZERO"))) {
         e = hipMemset(c->arena, 0, total);
         if (e == hipSuccess) e = hipDeviceSynchronize();
