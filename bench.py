@@ -289,6 +289,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--workers", type=int, default=65536)
     ap.add_argument("--tasks", type=int, default=1_000_000)
+    ap.add_argument("--loads", default="zipf", choices=("zipf", "uniform"),
+                    help="uniform: BASELINE configs[1]'s state (capacity 256, busy ~U[0,128); "
+                         "use with --workers 1000 --tasks 100000)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-host-observed", action="store_true", help="skip the launch+wait+readback+commit timing")
     ap.add_argument("--cpu-budget", type=float, default=10.0)
@@ -349,7 +352,12 @@ def main():
     if deque and world > 1:
         raise SystemExit("--mode deque runs on one GPU (the start() loop has no sharded form)")
     # deque: same loads without deaths; 2 % of the queued workers hold a second deque entry
-    st = synth.zipf_deque_state(W=W, seed=0, dup_frac=0.02) if deque else synth.zipf_state(W=W, seed=0)
+    if deque:
+        st = synth.zipf_deque_state(W=W, seed=0, dup_frac=0.02)
+    elif args.loads == "uniform":
+        st = synth.uniform_state(W=W, seed=0)
+    else:
+        st = synth.zipf_state(W=W, seed=0)
     F = len(st["log"])
     Q = len(st["queue"])
     if world == 1:
@@ -465,10 +473,12 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "int32",
-        "data": "synthetic (faasbal.synth.zipf_state, seed=0)",
+        "data": "synthetic (faasbal.synth.%s, seed=0)" % ("uniform_state" if args.loads == "uniform" else "zipf_state"),
         "config": {"workload": ("configs[2] loads, start() loop (no heartbeats): one tick, %d pending tasks x %d "
                                 "workers, Zipf(1.5) loads cap 32, deque of %d entries (2%% repeated ids)"
                                 % (T, W, Q)) if deque else
+                               ("configs[1]-style: one tick, %d pending tasks x %d workers, uniform loads (capacity "
+                                "256, busy ~U[0,128)), %d orphans redistributed" % (T, W, O)) if args.loads == "uniform" else
                                ("configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
                                 "5%% dead -> %d orphans redistributed" % (T, W, O)) if world == 1 else
                                ("configs[2] per GPU, weak: one global tick of %d tasks x %d workers sharded by "
