@@ -454,7 +454,7 @@ def _sort_tick(W, E, hot_frac, seed, purge_mode=1, hot_n=5, expect_reruns=None):
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
     _cmp_state(g, o, 0)
-    if expect_reruns is not None:
+    if expect_reruns is not None and os.environ.get("FAASBAL_EV_LL", "1") != "0":  # reruns: linked-list path only
         assert (a["result"]["reruns"] > 0) == expect_reruns, a["result"]["reruns"]
 
 
@@ -510,7 +510,8 @@ def test_event_link_limit(n_hot):
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
     _cmp_state(g, o, 0)
-    assert (a["result"]["reruns"] > 0) == (n_hot > 16)
+    if os.environ.get("FAASBAL_EV_LL", "1") != "0":
+        assert (a["result"]["reruns"] > 0) == (n_hot > 16)
 
 
 @pytest.mark.parametrize("W,E,wide", [(1 << 20, 300_000, "1"), ((1 << 17) + 5, 1_200_000, "1"),
