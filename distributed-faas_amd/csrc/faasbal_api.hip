@@ -136,6 +136,7 @@ struct fb_ctx {
     bool l_resort = false;                  // this tick reruns through the sort (a slot had > kLinkMax messages)
     bool l_used_ll = false;                 // the last enqueue grouped by linked lists
     int purge_apply = 1;
+    int cq_direct = 1;                      // FAASBAL_CQ_DIRECT=0: idle ticks copy c / hb through k_scan (A/B knob)
     // A/B knobs read once at creation (not per launch): FAASBAL_SCAN_FFIRST,
     // FAASBAL_POST_EAGER, FAASBAL_NO_ARENA32
     int scan_ffirst = 0, post_eager = 0, no_arena32 = 0;                    // FAASBAL_PURGE_APPLY=0: the slot purge stays in k_scan (A/B knob)
@@ -663,6 +664,7 @@ int enqueue_tick(fb_ctx *c) {
     a.free_in = c->free_[cur];
     a.queue_in = c->queue[cur];
     a.qaos = (!c->shard && c->qaos) ? 1 : 0;
+    a.cq_direct = (c->cq_direct && E == 0 && a.qaos && a.segw && !c->deque) ? 1 : 0;
     a.qfree_in = c->qfree[cur];
     a.qhb_in = c->qhb[cur];
     a.touched = c->touched;
@@ -953,6 +955,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_EV_LL")) c->ev_ll = atoi(getenv("FAASBAL_EV_LL"));
     if (!rc && getenv("FAASBAL_REPL")) c->repl = atoi(getenv("FAASBAL_REPL"));
     if (!rc && getenv("FAASBAL_PURGE_APPLY")) c->purge_apply = atoi(getenv("FAASBAL_PURGE_APPLY"));
+    if (!rc && getenv("FAASBAL_CQ_DIRECT")) c->cq_direct = atoi(getenv("FAASBAL_CQ_DIRECT"));
     if (!rc) {
         c->scan_ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
         c->post_eager = getenv_int("FAASBAL_POST_EAGER");

@@ -202,7 +202,9 @@ struct TickArgs {
     const PostRec *post;
     const uint8_t *post_rf;
     int ffirst;     // k_scan: log blocks before queue blocks in the grid (A/B knob FAASBAL_SCAN_FFIRST)
-    int slots_in_apply;  // the slot purge ran in k_ev_apply_ll's launch: k_scan has no W blocks
+    int slots_in_apply;
+    int cq_direct;  // idle one-GPU tick on k_emit2: the emit recomputes each position's raw free count
+                    // and heartbeat from the committed per-position arrays; k_scan stores neither  // the slot purge ran in k_ev_apply_ll's launch: k_scan has no W blocks
     int post_lazy;  // 1: the slot purge loads post records only for touched slots (large tables)
     const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates

@@ -1417,8 +1417,10 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 raw = INT32_MIN;
         }
         if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
-        a.c_arr[pos] = raw;
-        if (!a.shard) a.c_hb[pos] = hbq;
+        if (!a.cq_direct) {
+            a.c_arr[pos] = raw;
+            if (!a.shard) a.c_hb[pos] = hbq;
+        }
         if (a.shard == 1) a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
     }
     STAMP(a, SO, 1);
@@ -2154,8 +2156,19 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int R = a.R;       // 32, 64 or 128
         // ---- every load in flight at once (clamped indices, no branches)
         const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
-        const int32_t raw0 = a.c_arr[pq];
-        const double hb0 = a.c_hb[pq];
+        int32_t raw0;
+        double hb0;
+        if (a.cq_direct) {
+            // idle tick: the committed position's free count and heartbeat, k_scan's liveness
+            // test repeated (the same bytes k_scan would have copied into c_arr / c_hb)
+            const double hq = a.qhb_in[pq];
+            const int32_t fq = a.qfree_in[pq];
+            hb0 = hq;
+            raw0 = ((a.now - hq) > a.tte) ? INT32_MIN : fq;
+        } else {
+            raw0 = a.c_arr[pq];
+            hb0 = a.c_hb[pq];
+        }
         const int s0 = a.E == 0 ? a.queue_in[pq] : lq_slot(a, pq);
         // counts of c > r in the earlier segments of this block: lane i, round 64 k + i
         // (all three earlier segments loaded unconditionally, clamped, then masked:
