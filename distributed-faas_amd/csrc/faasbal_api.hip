@@ -1675,7 +1675,9 @@ int fb_host_alloc(fb_ctx *c, int64_t bytes, void **ptr) {
 }
 
 int fb_host_free(fb_ctx *c, void *ptr) {
-    if (!c) return FB_EINVAL;
+    // pinned host memory belongs to the process, not to the context: ctx may be NULL
+    // (a buffer that outlives its context is freed when its last user lets it go)
+    if (!c) return (!ptr || hipHostFree(ptr) == hipSuccess) ? FB_OK : FB_EHIP;
     if (ptr) HIPCHK(c, hipHostFree(ptr));
     return FB_OK;
 }

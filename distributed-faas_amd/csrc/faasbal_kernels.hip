@@ -93,16 +93,13 @@ __device__ __forceinline__ void wt_store(T *p, T v) {
 #endif
 }
 
-// Fused ticks: orphan / eviction totals through atomics into the group rows (1), or
-// read back by every emit queue block from the per-block counts (0).
-#ifndef FAASBAL_EXP
-#define FAASBAL_EXP 0  // timing experiments only (results invalid when set)
-#endif
 // k_emit2 after k_plan(2) counts the per-segment round counts of its block in LDS (1)
 // or reads the ones k_scan stored (0: 2 x 4.7 MB per streaming tick)
 #ifndef FAASBAL_SEG_LDS
 #define FAASBAL_SEG_LDS 1
 #endif
+// Fused ticks: orphan / eviction totals through atomics into the group rows (1), or
+// read back by every emit queue block from the per-block counts (0).
 #ifndef FAASBAL_GRP_OW
 #define FAASBAL_GRP_OW 1
 #endif
@@ -2219,13 +2216,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         if constexpr (PLAN) {
             STAMPW(a, SO, 5);
             // this block's prefix and the total of every round, scanned by k_plan
-#if FAASBAL_EXP == 1
-            if ((int)threadIdx.x < R) {
-                pre_c[threadIdx.x] = (uint32_t)b * 256u;
-                tot_f[threadIdx.x] = 1000000u;
-            }
-            O = 0; nev = 0; cap = 1ll << 40; maxc = R;
-#else
             const int64_t *Ar = a.repl ? a.A_rep + (size_t)(b >> a.gshift) * kRFused : a.A;
             const DevTotals *Pr = a.repl ? a.P_rep + (b >> a.gshift) : a.P;
             if ((int)threadIdx.x < R) {
@@ -2236,7 +2226,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             nev = Pr->n_evicted;
             cap = Pr->cap_total;
             maxc = Pr->maxc;
-#endif
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
 #pragma unroll

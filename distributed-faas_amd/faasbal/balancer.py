@@ -9,6 +9,7 @@ block (:393-419), plus redistribution of the dead workers' in-flight tasks.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 
 import numpy as np
 
@@ -73,22 +74,20 @@ class GpuBalancer:
 
     def close(self):
         if getattr(self, "h", None) and self.h.value:
-            for p in getattr(self, "_pinned", ()):
-                self.lib.fb_host_free(self.h, p)
-            self._pinned = []
             self.lib.fb_destroy(self.h)
             self.h = C.c_void_p()
 
     def pinned(self, n, dtype=np.int32):
-        """A numpy array in pinned host memory (freed with the context): output copies
-        into it (``assignments(out=...)``) are single DMA transfers."""
+        """A numpy array in pinned host memory: output copies into it
+        (``assignments(out=...)``) are single transfers.  The memory is freed when the
+        last array viewing it is collected -- not with the context, so an array that
+        outlives ``close()`` never points at freed memory."""
         dtype = np.dtype(dtype)
         p = C.c_void_p()
         self._chk(self.lib.fb_host_alloc(self.h, int(n) * dtype.itemsize, C.byref(p)))
-        if not hasattr(self, "_pinned"):
-            self._pinned = []
-        self._pinned.append(p)
         buf = (C.c_char * max(int(n) * dtype.itemsize, 1)).from_address(p.value)
+        # buf is the base of every view of the array; fb_host_free(NULL, p) needs no context
+        weakref.finalize(buf, self.lib.fb_host_free, None, C.c_void_p(p.value))
         return np.frombuffer(buf, dtype=dtype, count=int(n))
 
     def pin_events(self, ev_kind, ev_slot, ev_val, ev_ts, ev_seq=None):

@@ -307,10 +307,19 @@ class GpuPushDispatcher:
             out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
                                      n_pending=len(self.pending))
         except FaasbalError as e:
-            # in-flight log full: the launch committed nothing, so compact and rerun once
-            if e.code != FB_ENOSPC or self.head == len(self.inflight):
+            # in-flight log full: the tick was not committed.  Compaction renumbers every
+            # in-flight sequence, so the results' sequence numbers are looked up again
+            # before the rerun; when nothing can be reclaimed the compaction still
+            # reinstalls the device log from the host's view, then the error propagates.
+            if e.code != FB_ENOSPC:
                 raise
+            reclaimable = self.head > len(self.inflight)
             self.compact_log()
+            if not reclaimable:
+                raise
+            for i, (wid, m, t) in enumerate(msgs):
+                if kind[i] == EV_RESULT:
+                    seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
             out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
                                      n_pending=len(self.pending))
         res = out["result"]

@@ -234,8 +234,10 @@ class ShardGroup:
         pass
 
 
-def serve_op(bal, op, kw, allreduce=None):
-    """One group operation on this rank's balancer (every rank runs the same op)."""
+def serve_op(bal, op, kw, allreduce=None, commit=True):
+    """One group operation on this rank's balancer (every rank runs the same op).
+    ``commit=False`` leaves a tick / purge waited but uncommitted (DistShardGroup
+    commits only once every rank has succeeded)."""
     if op == "load":
         bal.load(kw["st"])
         return None
@@ -243,11 +245,30 @@ def serve_op(bal, op, kw, allreduce=None):
         return bal.read_state(with_log=kw["with_log"])
     if op == "tick":
         out = bal.tick(kw["now"], kw["tte"], kw["ev_kind"], kw["ev_slot"], kw["ev_val"], kw["ev_ts"], kw["ev_seq"],
-                       kw["n_pending"], allreduce=allreduce)
+                       kw["n_pending"], allreduce=allreduce, commit=commit)
         return out
     if op == "purge":
-        return bal.purge(kw["now"], kw["tte"], allreduce=allreduce)
+        return bal.purge(kw["now"], kw["tte"], allreduce=allreduce, commit=commit)
     raise ValueError("unknown group operation %r" % op)
+
+
+def _serve_guarded(bal, op, kw):
+    """serve_op on this rank, its failure returned instead of raised: every rank must
+    still reach the group's gather (a rank that skipped it would leave the others
+    blocked in the collective).  A tick / purge is not committed here."""
+    try:
+        return (True, serve_op(bal, op, kw, commit=False))
+    except Exception as e:  # noqa: BLE001 -- reported to rank 0, which raises it
+        return (False, (getattr(e, "code", None), "%s: %s" % (type(e).__name__, e)))
+
+
+def _settle(bal, op, outs):
+    """After the gather, on every rank: commit a tick / purge only when it succeeded
+    on every rank (so the shards never diverge); returns the first failure or None."""
+    bad = next((o[1] for o in outs if not o[0]), None)
+    if bad is None and op in ("tick", "purge"):
+        bal.commit()
+    return bad
 
 
 class DistShardGroup(ShardGroup):
@@ -266,10 +287,15 @@ class DistShardGroup(ShardGroup):
 
     def _each(self, op, **kw):
         self.dist.broadcast_object_list([(op, kw)], src=0)
-        mine = serve_op(self.bal, op, kw)
         outs = [None] * self.dist.get_world_size()
-        self.dist.all_gather_object(outs, mine)
-        return outs
+        self.dist.all_gather_object(outs, _serve_guarded(self.bal, op, kw))
+        bad = _settle(self.bal, op, outs)
+        if bad is not None:
+            code, msg = bad
+            if code is None:
+                raise RuntimeError("shard operation %r failed on a rank: %s" % (op, msg))
+            raise FaasbalError(code, "shard operation %r failed on a rank: %s" % (op, msg))
+        return [o[1] for o in outs]
 
     def close(self):
         self.dist.broadcast_object_list([("stop", {})], src=0)
@@ -284,8 +310,9 @@ def serve_shard(balancer):
         op, kw = box[0]
         if op == "stop":
             return
-        mine = serve_op(balancer, op, kw)
-        dist.all_gather_object([None] * dist.get_world_size(), mine)
+        outs = [None] * dist.get_world_size()
+        dist.all_gather_object(outs, _serve_guarded(balancer, op, kw))
+        _settle(balancer, op, outs)  # rank 0 raises a failure; this rank keeps serving
 
 
 class LocalShardGroup(ShardGroup):

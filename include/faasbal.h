@@ -153,7 +153,7 @@ int fb_get_outputs(fb_ctx *ctx, int32_t *assign, int64_t *orphans, int32_t *evic
 /* Pinned host memory: fb_get_* copies into it are single DMA transfers on the
  * context stream (the drop-in's readback of a tick's assignments). */
 int fb_host_alloc(fb_ctx *ctx, int64_t bytes, void **ptr);
-int fb_host_free(fb_ctx *ctx, void *ptr);
+int fb_host_free(fb_ctx *ctx, void *ptr); /* ctx may be NULL (the memory outlives contexts) */
 
 /* launch + wait + copies + commit.  Output arrays may be NULL. */
 int fb_tick(fb_ctx *ctx, double now, double tte, int32_t n_events, const uint8_t *kind,

@@ -35,23 +35,28 @@ class ModelRankBalancer:
         (allreduce or dist.all_reduce)(xt)  # SUM of uint8, one contributor per byte
         return xt.numpy()
 
-    def _run(self, now, tte, k, s, v, t, q, T, allreduce, redist):
+    def _run(self, now, tte, k, s, v, t, q, T, allreduce, redist, commit):
         head = int(self.rs["head"])
         x, ctx = sm.phase1(self.rs, self.world, self.rank, now, tte, k, s, v, t, q, T)
-        out, self.rs = sm.phase2(self.rs, ctx, self._exchange(x, allreduce), redist=redist)
+        out, self._next = sm.phase2(self.rs, ctx, self._exchange(x, allreduce), redist=redist)
         n = int(out["n_assigned"])
         out["result"] = dict(n_assigned=n, log_head=head + n, n_local=len(out["task"]),
                              n_orphans_local=len(out["orphans"]), n_evicted=len(out["evicted"]))
+        if commit:
+            self.commit()
         return out
 
+    def commit(self):
+        self.rs = self._next
+
     def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
-             allreduce=None):
+             allreduce=None, commit=True):
         k = np.asarray(ev_kind, np.int64)
         seq = np.full(len(k), -1, np.int64) if ev_seq is None else np.asarray(ev_seq, np.int64)
         return self._run(now, tte, k, np.asarray(ev_slot, np.int64), np.asarray(ev_val, np.int64),
-                         np.asarray(ev_ts, np.float64), seq, int(n_pending), allreduce, True)
+                         np.asarray(ev_ts, np.float64), seq, int(n_pending), allreduce, True, commit)
 
-    def purge(self, now, tte, allreduce=None):
+    def purge(self, now, tte, allreduce=None, commit=True):
         e = np.zeros(0, np.int64)
-        out = self._run(now, tte, e, e, e, np.zeros(0), e, 0, allreduce, False)
+        out = self._run(now, tte, e, e, e, np.zeros(0), e, 0, allreduce, False, commit)
         return dict(result=out["result"], evicted=out["evicted"], orphans=out["orphans"])

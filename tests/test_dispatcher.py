@@ -326,6 +326,53 @@ def test_backlog_beyond_log_compacts_rarely(dispatcher_cls):
     assert comp[0] == 0 and 0 < comp[1] <= 40 // 3, comp
 
 
+def test_enospc_rerun_renumbers_result_sequences(dispatcher_cls):
+    """A tick that carries results and whose dispatches overflow the in-flight log
+    (the pre-check does not compact: too little garbage) fails with FB_ENOSPC; the
+    dispatcher compacts -- renumbering every in-flight sequence -- and reruns the
+    tick with the results' sequence numbers looked up again.  Afterwards the
+    finished tasks must not be redistributed when their workers die: every sent
+    message equals a run whose log never fills (dispatcher.py ENOSPC)."""
+    runs, comp = [], []
+    for cap in (1 << 16, 64):
+        env = FakeEnv()
+        d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=8, max_events=128, max_inflight=cap,
+                           redis_client=env, subscriber=env, socket=env, poller=env, clock=env.clock)
+        env.tasks.extend("e%d" % j for j in range(65))
+        sent, prev = [], []
+        for t in range(6):
+            env.now = 1000.0 + t
+            if t == 0:  # two workers with one process each: 2 dispatches per tick
+                for w in range(2):
+                    env.inbound.append((wid(w), codec.serialize(
+                        {"type": "register", "data": {"num_processes": 1}}).encode(), env.now))
+            if t == 2:  # a large worker: this tick dispatches 61 tasks (head 4 + 61 > 64)
+                env.inbound.append((wid(2), codec.serialize(
+                    {"type": "register", "data": {"num_processes": 59}}).encode(), env.now))
+            for (dst, m) in prev:
+                # every result comes back through tick 2; at tick 3 only worker 2's,
+                # then every worker falls silent
+                if m["type"] == "task" and (t <= 2 or (t == 3 and dst == wid(2))):
+                    env.inbound.append((dst, codec.serialize({"type": "result", "data": {
+                        "task_id": m["data"]["task_id"], "status": "COMPLETED", "result": 1}}).encode(), env.now))
+            if t == 5:
+                env.now = 1000.0 + 20  # every heartbeat expired: the unfinished tasks are orphans
+                env.inbound.append((wid(3), codec.serialize(
+                    {"type": "register", "data": {"num_processes": 10}}).encode(), env.now))
+            env.sent.clear()
+            d.tick()
+            prev = list(env.sent)
+            sent.append(prev)
+        runs.append(sent)
+        comp.append(d.compactions)
+    assert comp[0] == 0 and comp[1] >= 2, comp
+    assert runs[0] == runs[1]
+    # the last tick redistributes exactly the two unfinished tasks of workers 0 and 1
+    redistributed = [m["data"]["task_id"] for _, m in runs[1][5] if m["type"] == "task"]
+    unfinished = [m["data"]["task_id"] for dst, m in runs[1][2] if m["type"] == "task" and dst != wid(2)]
+    assert sorted(redistributed) == sorted(unfinished) and len(unfinished) == 2
+
+
 def test_purge_workers_evicts_without_dispatching(dispatcher_cls):
     """purge_workers() (task_dispatcher.py:241-249) deletes the expired records and
     sends nothing; the dead worker's in-flight tasks go to the front of the pending

@@ -128,3 +128,77 @@ def test_sharded_dispatcher_rccl_world2_replays_reference():
     if torch.cuda.device_count() < 2:
         pytest.skip("needs two GPUs (one process per GPU over RCCL)")
     _spawn(2, "nccl", SUBSET)
+
+
+def _fail_rank_main(rank, world, port, errq):
+    """DistShardGroup when a tick fails on one rank only: the failure
+    reaches rank 0 as the FaasbalError, no rank commits that tick, and the group keeps
+    serving (no rank left blocked in a collective)."""
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.join(os.path.dirname(HERE), "distributed-faas_amd"))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    from faasbal import synth
+    from faasbal._lib import FB_ENOSPC, FaasbalError
+    from faasbal.sharded import DistShardGroup, serve_shard
+    from shard_model_balancer import ModelRankBalancer
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+
+    class Flaky(ModelRankBalancer):
+        """Rank 1's balancer fails its second tick after the exchange (as an in-flight
+        log shard that is full would: FB_ENOSPC from fb_tick_wait)."""
+        n = 0
+
+        def tick(self, *a, **k):
+            out = super().tick(*a, **k)
+            Flaky.n += 1
+            if rank == 1 and Flaky.n == 2:
+                raise FaasbalError(FB_ENOSPC, "log shard full (injected)")
+            return out
+
+    try:
+        st = synth.zipf_state(W=64, seed=3)
+        bal = Flaky(rank, world, 64)
+        if rank != 0:
+            serve_shard(bal)
+            return
+        g = DistShardGroup(bal, 64)
+        g.load(st)
+        g.tick(1000.0, 10.0, n_pending=40)
+        before = g.read_state()
+        try:
+            g.tick(1000.5, 10.0, n_pending=40)
+            raise AssertionError("the failing rank's error did not reach rank 0")
+        except FaasbalError as e:
+            assert e.code == FB_ENOSPC, e
+        after = g.read_state()  # the group still serves; nothing was committed
+        for key in ("reg", "free", "queue", "log"):
+            assert np.array_equal(before[key], after[key]), key
+        assert after["head"] == before["head"]
+        g.tick(1000.5, 10.0, n_pending=40)  # and ticks again
+        g.close()
+    except Exception as e:
+        errq.put("rank %d: %r" % (rank, e))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_shard_group_survives_a_failing_rank():
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    errq = ctx.Queue()
+    port = _port()
+    procs = [ctx.Process(target=_fail_rank_main, args=(r, 2, port, errq)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+    errs = []
+    while not errq.empty():
+        errs.append(errq.get())
+    assert not errs, errs
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
