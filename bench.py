@@ -125,14 +125,16 @@ def cpu_baseline_deque(st, T, budget_s=10.0):
                        % (len(out["assign"]), os.cpu_count()))
 
 
-def bench_stream(args):
-    """BASELINE.json configs[4] on one GPU: 1M workers, every tick 64K new tasks,
-    64K results of in-flight tasks, 1K re-registrations, 10K heartbeats; the
-    clock advances 10 ms per tick so silent workers expire (churn) and their
-    in-flight tasks are redistributed.  Ticks are committed (state evolves);
-    the timed region holds K whole ticks: host staging of the events (tick
-    i+1's overlapping tick i on the device), the launch, the wait for the
-    results and the commit."""
+def bench_stream(args, dist=None, world=1, rank=0, dev=0):
+    """BASELINE.json configs[4]: 1M workers, every tick 64K new tasks, 64K results
+    of in-flight tasks, 1K re-registrations, 10K heartbeats; the clock advances
+    10 ms per tick so silent workers expire (churn) and their in-flight tasks are
+    redistributed.  Ticks are committed (state evolves); the timed region holds K
+    whole ticks.  One GPU: host staging of the events (tick i+1's overlapping
+    tick i on the device), the launch, the wait for the results and the commit.
+    N GPUs (configs[4] as stated, "8 MI355X"): the 1M-worker table sharded by
+    worker-id range, every rank receives the tick's whole message batch, phase 1
+    -> the exchange all-reduce (RCCL) -> phase 2 -> wait -> commit on every rank."""
     from faasbal import GpuBalancer, synth
     W = args.workers if args.workers != 65536 else 1 << 20
     T = 65536
@@ -141,36 +143,64 @@ def bench_stream(args):
     ticks = synth.stream_ticks(st, n_ticks=Wu + 2 * K, seed=2, tasks_per_tick=T, results_per_tick=T,
                                hb_frac=args.hb_frac)
     E = max(len(t["ev_kind"]) for t in ticks)
-    g = GpuBalancer(W, len(st["log"]) + (Wu + 2 * K + 2) * 2 * T, max_events=E, device=0)
-    g.load(st)
-    if not args.pageable_events:
-        # the producer writes each tick's messages straight into pinned host memory (as the
-        # dispatcher's parse loop can): staging then validates in place, no staging copy
-        for tk in ticks:
-            (tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"]) = g.pin_events(
-                tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
+    cap = len(st["log"]) + (Wu + 2 * K + 2) * 2 * T
     carried = [0]
     stats = dict(assigned=0, orphans=0, evicted=0, events=0)
+    if world == 1:
+        g = GpuBalancer(W, cap, max_events=E, device=0)
+        g.load(st)
+        if not args.pageable_events:
+            # the producer writes each tick's messages straight into pinned host memory (as the
+            # dispatcher's parse loop can): staging then validates in place, no staging copy
+            for tk in ticks:
+                (tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"]) = g.pin_events(
+                    tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
 
-    def stage(tk):
-        g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
+        def stage(tk):
+            g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
 
-    def run(i):
-        # launch tick i on its staged messages, stage tick i+1's on the host while
-        # the device runs tick i (double-buffered pinned staging), then wait + commit
-        tk = ticks[i]
-        n = carried[0] + tk["n_new"]
-        g.launch_staged(10.0, n)
-        if i + 1 < len(ticks):
-            stage(ticks[i + 1])
-        r = g.wait()
-        g.commit()
-        carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
-        return r
+        def run(i):
+            # launch tick i on its staged messages, stage tick i+1's on the host while
+            # the device runs tick i (double-buffered pinned staging), then wait + commit
+            tk = ticks[i]
+            n = carried[0] + tk["n_new"]
+            g.launch_staged(10.0, n)
+            if i + 1 < len(ticks):
+                stage(ticks[i + 1])
+            r = g.wait()
+            g.commit()
+            carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
+            return r
 
-    stage(ticks[0])
+        stage(ticks[0])
+    else:
+        import torch
+        from faasbal.sharded import ShardedBalancer
+        g = ShardedBalancer(rank, world, W, cap, max_events=E, device=dev)
+        g.load(st)
+
+        def run(i):
+            tk = ticks[i]
+            n = carried[0] + tk["n_new"]
+            g.launch(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+            with torch.cuda.stream(g.stream):
+                dist.all_reduce(g.exchange(), async_op=True).wait()  # phase 2 ordered after it on g.stream
+            g.cont()
+            r = g.wait()
+            g.commit()
+            carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
+            return r
+
+    def barrier():
+        if dist is not None:
+            t = torch.zeros(1, device="cuda")
+            dist.all_reduce(t)
+            torch.cuda.synchronize()
+
     for i in range(Wu):
         run(i)
+    g.sync()
+    barrier()
     g.sync()
     t0 = time.perf_counter()
     for i in range(Wu, Wu + K):
@@ -178,10 +208,16 @@ def bench_stream(args):
         r = run(i)
         stats["assigned"] += int(r["n_assigned"])
         stats["orphans"] += int(r["n_orphans"])
-        stats["evicted"] += int(r["n_evicted"])
+        stats["evicted"] += int(r["n_evicted"])  # sharded: this rank's evictions (summed below)
         stats["events"] += len(tk["ev_kind"])
     g.sync()
+    barrier()
     dt = time.perf_counter() - t0
+    if dist is not None:
+        t = torch.tensor([dt, float(stats["evicted"])], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:])
+        dt, stats["evicted"] = float(t[0].item()), int(t[1].item())
     g.timing_enable(True)
     for i in range(Wu + K, len(ticks)):
         run(i)
@@ -190,28 +226,35 @@ def bench_stream(args):
     kern = {k: ms / max(n, 1) * 1e3 for k, (ms, n) in kt.items()}  # us per launch
     per_tick = {k: ms / K * 1e3 for k, (ms, n) in kt.items()}      # us per tick
     line = {
-        "metric": "streaming task assignments/sec, configs[4] per GPU (64K tasks + churn per tick, 1M workers)",
+        "metric": "streaming task assignments/sec, configs[4] (64K tasks + churn per tick, 1M workers)",
         "value": stats["assigned"] / dt,
         "unit": "assignments/s",
-        "n_gpus": 1,
+        "n_gpus": world,
         "steps": K,
         "warmup": Wu,
         "ms_per_step": dt * 1e3 / K,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (faasbal.synth.zipf_state(W, seed=0, dead_frac=0) + stream_ticks(seed=2))",
-        "config": {"workload": "configs[4] per GPU: %d workers, %d new tasks + %d results + %d joins + %d heartbeats "
-                               "per tick, 10 ms per tick, committed ticks" % (W, T, T, max(1, W // 1000),
-                                                                                max(1, int(args.hb_frac * W))),
+        "config": {"workload": "configs[4]: %d workers%s, %d new tasks + %d results + %d joins + %d heartbeats "
+                               "per tick, 10 ms per tick, committed ticks"
+                               % (W, "" if world == 1 else " sharded by worker-id range over %d GPUs" % world, T, T,
+                                  max(1, W // 1000), max(1, int(args.hb_frac * W))),
                    "workers": W, "events_per_tick": stats["events"] / K, "assigned_per_tick": stats["assigned"] / K,
-                   "events_in": "pageable (staged by copy)" if args.pageable_events else "pinned (zero-copy staging)",
-                   "orphans_per_tick": stats["orphans"] / K, "evicted_per_tick": stats["evicted"] / K},
+                   "events_in": "pageable (staged by copy)" if args.pageable_events or world > 1
+                                else "pinned (zero-copy staging)",
+                   "orphans_per_tick": stats["orphans"] / K, "evicted_per_tick": stats["evicted"] / K,
+                   "parallelism": "dp1" if world == 1 else "worker-table shards x%d" % world},
         "tick": {"device_us_per_tick": sum(per_tick.values()), "kernels_us_per_tick": per_tick,
                  "kernels_us_per_launch": kern},
     }
-    print(json.dumps(line), flush=True)
+    if dist is not None:
+        line["config"]["world_size_reported"] = dist.get_world_size()
+        line["config"]["backend"] = dist.get_backend()
+    if rank == 0:
+        print(json.dumps(line), flush=True)
 
 
 # The reference loop itself (task_dispatcher.py:324-419, CPython, one core), measured
@@ -298,8 +341,10 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--mode", default="heartbeat", choices=("heartbeat", "deque"),
                     help="deque: the loop without heartbeats (PushDispatcher.start), one GPU")
-    ap.add_argument("--workload", default="tick", choices=("tick", "stream"),
-                    help="stream: configs[4] per GPU -- committed ticks with churn and 64K results each (one GPU)")
+    ap.add_argument("--workload", default="tick", choices=("tick", "cfg3", "stream"),
+                    help="tick: configs[2] (N GPUs: weak scaling, N x 64K workers, N x 1M tasks); cfg3: configs[3], "
+                         "16M tasks x 1M workers (N GPUs: the same global table sharded, strong scaling); stream: "
+                         "configs[4], committed ticks with churn and 64K results each against 1M workers")
     ap.add_argument("--pageable-events", action="store_true",
                     help="stream: messages in pageable numpy arrays (staging copies them into pinned memory)")
     ap.add_argument("--hb-frac", type=float, default=0.01,
@@ -309,9 +354,7 @@ def main():
         raise SystemExit("--gpus must be >= 1")
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(self_launch(args))
-    if args.workload == "stream":
-        if args.gpus > 1:
-            raise SystemExit("--workload stream runs on one GPU")
+    if args.workload == "stream" and args.gpus == 1:
         return bench_stream(args)
 
     rank = int(os.environ.get("RANK", "0"))
@@ -340,6 +383,11 @@ def main():
             os.close(saved)
         if dist.get_world_size() != args.gpus:
             raise SystemExit("torch.distributed reports %d ranks, --gpus %d" % (dist.get_world_size(), args.gpus))
+    if args.workload == "stream":
+        bench_stream(args, dist, world, rank, dev)
+        if dist is not None:
+            dist.destroy_process_group()
+        return
 
     from faasbal import GpuBalancer, synth
 
@@ -347,7 +395,12 @@ def main():
     # table; N > 1 shards ONE global table of N x 64K workers / N x 1M tasks by
     # worker-id range and runs the two-phase tick with the RCCL exchange
     # all-reduce every step.
-    W, T = args.workers * world, args.tasks * world
+    if args.workload == "cfg3":
+        # configs[3]: one global table of 1M workers and 16M pending tasks, whatever N
+        W = args.workers if args.workers != 65536 else 1 << 20
+        T = args.tasks if args.tasks != 1_000_000 else 16_000_000
+    else:
+        W, T = args.workers * world, args.tasks * world
     deque = args.mode == "deque"
     if deque and world > 1:
         raise SystemExit("--mode deque runs on one GPU (the start() loop has no sharded form)")
@@ -470,11 +523,17 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if args.workload == "cfg3" else "weak",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (faasbal.synth.%s, seed=0)" % ("uniform_state" if args.loads == "uniform" else "zipf_state"),
-        "config": {"workload": ("configs[2] loads, start() loop (no heartbeats): one tick, %d pending tasks x %d "
+        "config": {"workload": ("configs[3]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, 5%% "
+                                "dead -> %d orphans redistributed, %s" % (
+                                    T, W, O, "one GPU" if world == 1 else
+                                    "worker table sharded by worker-id range over %d GPUs, exchange all-reduce of %d B "
+                                    "per tick (%s)" % (world, kt_x_bytes, "RCCL" if args.backend == "nccl"
+                                                       else args.backend))) if args.workload == "cfg3" else
+                               ("configs[2] loads, start() loop (no heartbeats): one tick, %d pending tasks x %d "
                                 "workers, Zipf(1.5) loads cap 32, deque of %d entries (2%% repeated ids)"
                                 % (T, W, Q)) if deque else
                                ("configs[1]-style: one tick, %d pending tasks x %d workers, uniform loads (capacity "
@@ -503,6 +562,8 @@ def main():
     if world > 1:
         line["config"]["world_size_reported"] = dist.get_world_size()
         line["config"]["backend"] = dist.get_backend()
+    if args.workload == "cfg3":
+        line["metric"] = "task assignments/sec, 16M tasks x 1M workers, 1/2/4/8 GPU"
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline_deque(st, T, args.cpu_budget) if deque else \
             cpu_baseline(st, T, args.cpu_budget)

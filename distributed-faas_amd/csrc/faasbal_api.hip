@@ -104,6 +104,18 @@ struct fb_ctx {
     double *hb = nullptr;        // last_heartbeat per slot (NaN: no record)
     uint32_t *epoch = nullptr;   // first log sequence of the slot's current registration
     int32_t *log_slot = nullptr;
+    // one-GPU heartbeat contexts: in-flight entries per slot (by commit parity), the
+    // post-message counts, the entry each event's result completes (cleared by the
+    // commit: the log is read-only during a tick), the launch stamp of the last launch
+    // whose result completed an entry, and k_emit2's log-workgroup hand-off granules
+    uint32_t *infl[2] = {nullptr, nullptr};
+    uint32_t *post_infl = nullptr;
+    int32_t *ev_clr = nullptr;
+    uint32_t *ctag = nullptr;
+    unsigned long long *fagg = nullptr, *fticket = nullptr;
+    unsigned long long fticket_n = 0;  // tickets handed out so far (the next launch's base)
+    uint32_t lstamp = 0;               // per enqueued launch, reruns included (never 0)
+    int f_emit = 1;                    // FAASBAL_F_EMIT=0: fused ticks keep k_scan's log blocks (A/B knob)
     int32_t *trash = nullptr;  // kTrashRows x kBS words written by inactive lanes (never read)
     int64_t Qn = 0, head = 0;
     uint32_t tick = 1;
@@ -493,7 +505,29 @@ int enqueue_tick(fb_ctx *c) {
         c->gdirty[c->gpar ^ 1] = 0;
         c->gdirty[c->gpar] = a.ngrp * a.gstride;
     }
+    if (++c->lstamp == 0) c->lstamp = 1;  // every launch (reruns included) stamps its own
+    const bool defer = c->infl[0] != nullptr;  // one-GPU heartbeat context
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
+    // fused one-GPU ticks: O from the slot purge's in-flight counts, the orphans flagged
+    // and compacted by k_emit2's log workgroups (k_scan without log blocks)
+    const int nbfe = (int)cdiv(nbf, 4);
+    const size_t bm16 = (size_t)(((W + 63) / 64 + 1) / 2) * 16;
+    a.f_emit = (defer && a.fused && c->f_emit && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
+                bm16 <= (size_t)c->max_lds) ? 1 : 0;
+    if (a.f_emit) {
+        a.nbfe = nbfe;
+        a.fagg = c->fagg;
+        a.fticket = c->fticket;
+        a.fticket0 = c->fticket_n;
+        c->fticket_n += (unsigned long long)nbfe;
+    }
+    if (defer) {
+        a.infl_in = c->infl[cur];
+        a.infl_out = c->infl[nxt];
+        a.post_infl = c->post_infl;
+        a.ctag = c->ctag;
+        a.lstamp = c->lstamp;
+    }
     // the log scan gathers one 16-byte record per in-flight entry; past 128K slots
     // (2 MB of records) those gathers miss L2, so k_slots first writes the
     // died bitmap (W/8 bytes, L2-resident) and the scan tests bits instead
@@ -539,6 +573,14 @@ int enqueue_tick(fb_ctx *c) {
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         ea.link = c->link;
         ea.hout = c->hout_dev;
+        ea.defer_clr = 1;  // the linked-list path exists on one-GPU heartbeat contexts only
+        ea.ev_clr = c->ev_clr;
+        ea.ctag = c->ctag;
+        ea.lstamp = c->lstamp;
+        ea.infl_in = c->infl[cur];
+        ea.post_infl = c->post_infl;
+        ea.infl_out = c->infl[nxt];
+        ea.orph_grp = (a.f_emit && c->purge_apply) ? 1 : 0;
         if (c->cm_pending) {  // the previous tick's commit rides in this launch
             ea.cm = c->cm;
             ea.cm_blocks = c->cm_grid;
@@ -550,7 +592,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.now = c->l_now;
         ea.st = c->st;
         ea.free_out = c->free_[nxt];
-        ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep)) ? c->dmask : nullptr;
+        ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep || a.f_emit)) ? c->dmask : nullptr;
         ea.wcnt = c->wcnt;
         ea.grp = a.grp_on ? a.grp : nullptr;
         ea.ngrp = a.ngrp;
@@ -646,6 +688,14 @@ int enqueue_tick(fb_ctx *c) {
         a.tbits = c->tbits;
         a.front_list = front;
         a.back_list = back;
+        if (defer) {
+            a.defer_clr = 1;
+            a.ev_clr = c->ev_clr;
+            a.ctag = c->ctag;
+            a.lstamp = c->lstamp;
+            a.infl_in = c->infl[cur];
+            a.post_infl = c->post_infl;
+        }
         Timer t(c, "ev_apply");
         launch_ev_apply(a, t.st());
     }
@@ -929,6 +979,15 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->post_nf, W);
         ap.add(&c->c_tok, Qlog);
     }
+    if (!shard && !c->deque) {
+        ap.add(&c->infl[0], W);
+        ap.add(&c->infl[1], W);
+        ap.add(&c->post_infl, W);
+        ap.add(&c->ev_clr, E);
+        ap.add(&c->ctag, F);
+        ap.add(&c->fagg, kFEmitMaxBlocks);
+        ap.add(&c->fticket, 1);
+    }
     if (shard) {
         ap.add(&c->lseq, F);
         ap.add(&c->ocnt, tab);
@@ -956,6 +1015,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_REPL")) c->repl = atoi(getenv("FAASBAL_REPL"));
     if (!rc && getenv("FAASBAL_PURGE_APPLY")) c->purge_apply = atoi(getenv("FAASBAL_PURGE_APPLY"));
     if (!rc && getenv("FAASBAL_CQ_DIRECT")) c->cq_direct = atoi(getenv("FAASBAL_CQ_DIRECT"));
+    if (!rc && getenv("FAASBAL_F_EMIT")) c->f_emit = atoi(getenv("FAASBAL_F_EMIT"));
     if (!rc) {
         c->scan_ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
         c->post_eager = getenv_int("FAASBAL_POST_EAGER");
@@ -1135,6 +1195,14 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
             for (int64_t i = 0; i < log_len; ++i)
                 if (lg[i] >= 0 && (!reg[lg[i]] || (uint64_t)i < (uint64_t)epv[lg[i]])) lg[i] = -1;
         HIPCHK(c, hipMemcpy(c->log_slot, lg.data(), (size_t)log_len * 4, hipMemcpyHostToDevice));
+        if (c->infl[0]) {
+            std::vector<uint32_t> cnt(W ? W : 1, 0);
+            for (int64_t i = 0; i < log_len; ++i)
+                if (lg[i] >= 0) ++cnt[lg[i]];
+            if (W) HIPCHK(c, hipMemcpy(c->infl[0], cnt.data(), W * 4, hipMemcpyHostToDevice));
+        }
+    } else if (c->infl[0] && W) {
+        HIPCHK(c, hipMemset(c->infl[0], 0, W * 4));
     }
     c->W = n_workers;
     c->Qn = queue_len;
@@ -1243,6 +1311,16 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
     c->maxc_hint = maxc;
     c->launched = c->waited = false;
     c->phase = 0;
+    return FB_OK;
+}
+
+int fb_read_inflight(fb_ctx *c, uint32_t *inflight) {
+    if (!c || !inflight) return FB_EINVAL;
+    if (int rc_ = flush_commit(c)) return rc_;
+    if (!c->infl[0]) return fail(c, FB_ESTATE, "in-flight counts exist on one-GPU heartbeat contexts only");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (c->W) HIPCHK(c, hipMemcpy(inflight, c->infl[c->cur], (size_t)c->W * 4, hipMemcpyDeviceToHost));
     return FB_OK;
 }
 
@@ -1496,6 +1574,8 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             if (rc) return rc;
             continue;
         }
+        if (c->hout->fault)
+            return fail(c, FB_EHIP, "k_emit2: a log workgroup's orphan-count hand-off timed out");
         if (c->hout->status == 0) break;
         if (c->hout->status == 2)
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
@@ -1538,7 +1618,7 @@ int fb_tick_commit(fb_ctx *c) {
     if (!c->waited) return fail(c, FB_ESTATE, "fb_tick_commit without a waited tick");
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t n_orph = c->last.n_orphans_local;
-    if (c->W > 0 || n_orph > 0) {
+    if (c->W > 0 || n_orph > 0 || (c->ev_clr && c->l_E > 0)) {
         CommitArgs a{};
         a.W = c->W;
         a.nbw = (int)cdiv(c->W, kBS);
@@ -1557,14 +1637,18 @@ int fb_tick_commit(fb_ctx *c) {
         a.lseq = c->lseq;
         a.head_local = c->l_head_local;
         a.shard = c->shard;
+        a.nbo = (int)cdiv(n_orph, kBS);
+        a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
+        a.ev_clr = c->ev_clr;
+        const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS);
         if (c->ev_head && c->ev_ll && !c->commit_now) {
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
-            c->cm_grid = a.nbw + (int)cdiv(n_orph, kBS);
+            c->cm_grid = grid;
             c->cm_pending = true;
         } else {
             Timer t(c, "commit");
-            launch_commit(a, a.nbw + (int)cdiv(n_orph, kBS), t.st());
+            launch_commit(a, grid, t.st());
             HIPCHK(c, hipGetLastError());
         }
     }

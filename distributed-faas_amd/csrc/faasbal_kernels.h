@@ -43,6 +43,14 @@ constexpr uint8_t kStEvicted = 4;    // record deleted during the tick and not r
 // post flags (post_rf >> 1): bit0 died_start, bits 1-2 queue status after the tick's messages
 constexpr int kPfDiedStart = 1;
 constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
+// post_rf bit 4 (one-GPU heartbeat contexts): a result of this tick completed one of the
+// slot's in-flight entries (ctag[q] == the launch stamp names which); the log itself is
+// cleared only by the commit, so an orphan test of that slot's entries checks ctag
+constexpr uint8_t kRfCleared = 16;
+// k_emit2's log tiles (one-GPU fused ticks): at most this many compaction workgroups
+// (4 tiles of kFTile entries each), so every workgroup's look-back over the earlier
+// ones' orphan counts is one load per thread
+constexpr int kFEmitMaxBlocks = 256;
 
 // Committed per-slot heartbeat: last_heartbeat, NaN when the slot holds no record
 // (so the log scan's one 8-byte gather per in-flight entry decides liveness
@@ -74,6 +82,8 @@ struct HostOut {
     int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
                         // (deque contexts: new_qlen > token capacity is checked by the host)
     int32_t resort;     // k_ev_apply_ll: a slot got too many messages, rerun through the sort
+    int32_t fault;      // k_emit2 log workgroups: an orphan-count hand-off never arrived (zeroed by k_scan)
+    int32_t pad_;
     int64_t n_local;   // sharded: tasks appended to this rank's log shard
     int64_t O_local;    // sharded: this rank's orphans
 };
@@ -89,6 +99,9 @@ struct CommitArgs {
     int W;
     int slot_base;
     int nbw;            // slot blocks; blocks [nbw, nbw + ceil(n_orph / 256)) clear orphaned log entries
+    int nbo;            // ... then blocks [nbw + nbo, + ceil(n_clr / 256)) clear the entries the
+    int n_clr;          // committed tick's results completed: log_slot[ev_clr[e]] = -1, e < n_clr
+    const int32_t *ev_clr;
     uint32_t tick;
     const uint8_t *st;
     const uint32_t *touched;
@@ -110,6 +123,18 @@ struct EvArgs {
     int E;
     int deque;          // 1: PushDispatcher.start semantics (no liveness, deque with repeated ids)
     const int32_t *tokcnt_in;          // deque: committed tokens per slot
+    // one-GPU heartbeat contexts: the log is read-only during a tick (so a relaunch of the
+    // tick sees the same log); a result that completes entry q records q in ev_clr[e] (the
+    // commit clears it) and stamps ctag[q] = lstamp; post_infl[s] = the slot's in-flight
+    // entries after its messages (infl_in minus the distinct entries its results completed)
+    int defer_clr;
+    int32_t *ev_clr;
+    uint32_t *ctag;
+    uint32_t lstamp;
+    const uint32_t *infl_in;
+    uint32_t *post_infl;
+    uint32_t *infl_out;   // the slot purge's next in-flight count (apply launch)
+    int orph_grp;         // the slot purge adds the orphans of dead registrations to column R + 1
     int32_t *front_rank, *back_rank;   // deque: rank of a new token among its slot's tokens
     int32_t *post_tok, *post_nf;       // deque: tokens per slot after the messages; new front tokens
     int shard;          // 0: one GPU; else this rank owns global slots [slot_base, slot_base + W)
@@ -182,6 +207,24 @@ struct TickArgs {
     uint32_t *grp_zero;  // the other parity's rows: k_emit2 zeroes zero_words of them for the next launch
     int zero_words;
     int f_sep;        // 1: log role in its own launch (k_logscan, died bitmap in LDS); k_scan W-role writes the bitmap
+    // one-GPU heartbeat contexts: in-flight entries per slot (infl_in committed, infl_out
+    // next: the purge writes the post-message count, 0 for a dead registration; k_emit*
+    // adds the tasks it gives the slot), post_infl / ctag / lstamp as in EvArgs
+    const uint32_t *infl_in;
+    uint32_t *infl_out;
+    const uint32_t *post_infl;
+    const uint32_t *ctag;
+    uint32_t lstamp;
+    // f_emit (fused one-GPU ticks): the orphan count comes from the slot purge (sum of the
+    // dead registrations' in-flight counts into column R + 1), k_scan has no log blocks, and
+    // k_emit2's compaction workgroups flag and compact the orphans themselves: log tiles
+    // tested against the died bitmap in LDS, offsets from the earlier workgroups' counts
+    // ({lstamp, count} granules in fagg), workgroup order from a ticket counter
+    int f_emit;
+    int nbfe;                      // k_emit2 log workgroups (4 tiles of kFTile entries each)
+    unsigned long long *fagg;      // [kFEmitMaxBlocks] {lstamp, orphans} per log workgroup
+    unsigned long long *fticket;   // monotonic ticket counter (this launch's tickets start at fticket0)
+    unsigned long long fticket0;
     int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;
     double now, tte;

@@ -660,22 +660,29 @@ struct SlotRun {
     int32_t fr;
     double hb;
     uint32_t epoch;
+    uint32_t infl0;  // defer_clr: committed in-flight entries of the slot
+    uint32_t ncl;    // defer_clr: distinct entries this tick's results completed
     __device__ __forceinline__ void init(const EvArgs &a, uint32_t s) {
         reg = a.reg[s];
         const int2 fq = a.free_in[s];
         fr = fq.x;
         hb = a.hb[s];
         epoch = a.epoch[s];
+        infl0 = a.defer_clr ? a.infl_in[s] : 0u;
+        ncl = 0;
         inq = fq.y;
         qstat = inq ? kQsKeep : kQsOut;
         qidx = -1;
         cur_is_start = reg;
         died_start = 0;
     }
-    // PF: logv = log_slot[seq] loaded by the caller (one GPU only)
+    // PF: logv = log_slot[seq] loaded by the caller (one GPU, heartbeat loop: defer_clr),
+    // dup: an earlier message of this slot in this tick completed the same entry.
+    // Returns whether this message completed an in-flight entry.
     template <bool PF = false>
-    __device__ __forceinline__ void step(const EvArgs &a, uint32_t gs, int i, int kind, int32_t val, double ts,
-                                         int64_t seq, int32_t logv = 0) {
+    __device__ __forceinline__ bool step(const EvArgs &a, uint32_t gs, int i, int kind, int32_t val, double ts,
+                                         int64_t seq, int32_t logv = 0, bool dup = false) {
+        bool cleared = false;
         // purge at ts before the message is polled (:390 of the previous iteration)
         if (reg && (ts - hb) > a.tte) {
             reg = 0;
@@ -703,8 +710,17 @@ struct SlotRun {
             hb = ts;
             const int64_t q = seq;
             if (q >= 0 && q < a.head_in) {
-                if (PF) {  // one GPU, the entry's slot loaded ahead (clearing it twice is harmless)
-                    if (logv == (int32_t)gs) a.log_slot[q] = -1;
+                if (PF) {
+                    // one GPU: the entry's slot loaded ahead; the log stays as committed
+                    // (the commit clears the entry), ctag names the entry for this launch
+                    if (logv == (int32_t)gs && !dup) {
+                        cleared = true;
+                        a.ctag[q] = a.lstamp;
+                    }
+                } else if (a.defer_clr) {
+                    // sorted path, one GPU: a slot may carry any number of results; the
+                    // first to stamp ctag[q] in this launch counts the entry
+                    if (a.log_slot[q] == (int32_t)gs) cleared = atomicExch(&a.ctag[q], a.lstamp) != a.lstamp;
                 } else {
                     const int64_t li = a.shard ? lseq_find(a.lseq, a.head_local, q) : q;
                     if (li >= 0 && a.log_slot[li] == (int32_t)gs) a.log_slot[li] = -1;
@@ -713,12 +729,16 @@ struct SlotRun {
             if (fr == 1 && !inq) { inq = 1; qstat = kQsBack; qidx = i; }
         }
         a.ev_status[i] = status;
+        if (a.defer_clr) a.ev_clr[i] = cleared ? (int32_t)seq : -1;
+        ncl += cleared ? 1u : 0u;
+        return cleared;
     }
     // the purge at the tick's clock of this touched slot (k_ev_apply_ll's launch)
     __device__ __forceinline__ void purge(const EvArgs &a, uint32_t s, int reg0);
     __device__ __forceinline__ void finish(const EvArgs &a, uint32_t s, uint32_t gs) {
         a.post[s] = PostRec{hb, fr, epoch};
-        a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1));
+        a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1) | (ncl ? kRfCleared : 0));
+        if (a.defer_clr) a.post_infl[s] = infl0 - ncl;
         if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));  // the bitmap is the stamp
         else a.touched[s] = a.tick;
         if (qstat == kQsFront) a.front_list[a.E - 1 - qidx] = (int32_t)gs + 1;
@@ -763,6 +783,15 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 
 // ------------------------------------------------------------ commit
 __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
+    if (blk >= a.nbw + a.nbo) {
+        // entries the committed tick's results completed (one-GPU heartbeat contexts keep
+        // the log read-only during the tick): they leave the in-flight log now
+        const int64_t e = (int64_t)(blk - a.nbw - a.nbo) * kBS + threadIdx.x;
+        if (e >= a.n_clr) return;
+        const int32_t q = a.ev_clr[e];
+        if (q >= 0) a.log_slot[q] = -1;
+        return;
+    }
     if (blk >= a.nbw) {
         // the committed tick redistributed these entries: their tasks now run under new
         // sequence numbers, so the old entries leave the in-flight log
@@ -840,25 +869,38 @@ __device__ __forceinline__ int32_t log_peek(const EvArgs &a, int64_t seq) {
 // (task_dispatcher.py:209-212 for liveness): status byte, next {free, queued}, the
 // died-at-start bit and the eviction count.  Untouched slots (t = false) from the
 // committed record, touched ones from the owner thread's post-message registers.
-__device__ __forceinline__ void purge_slot(const EvArgs &a, int s, bool t, int reg0, int reg, double hb, int32_t fr,
-                                           int died_flag, bool queued_if_alive, bool &died, bool &evicted) {
+// infl: the slot's in-flight entries after its messages; returns the orphans it leaves
+// (the entries of a registration that died), and writes the next in-flight count.
+__device__ __forceinline__ uint32_t purge_slot(const EvArgs &a, int s, bool t, int reg0, int reg, double hb,
+                                               int32_t fr, int died_flag, bool queued_if_alive, uint32_t infl,
+                                               bool &died, bool &evicted) {
     const bool dead = reg && ((a.now - hb) > a.tte);
     const bool alive = reg && !dead;
     died = reg0 && (dead || died_flag);
     evicted = (reg0 || t) && !alive;
     a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
     a.free_out[s] = make_int2(alive ? fr : INT32_MIN, (alive && queued_if_alive) ? 1 : 0);
+    // a new registration after a death starts with no in-flight entries
+    if (a.infl_out) a.infl_out[s] = (alive && !died) ? infl : 0u;
+    return died ? infl : 0u;
 }
 __device__ __forceinline__ void count_evicted(const EvArgs &a, int tile, uint32_t n) {
     atomicAdd(&a.wcnt[tile], n);
     if (FAASBAL_GRP_OW && a.grp) atomicAdd(&a.grp[(tile % a.ngrp) * a.gstride + a.R + 2], n);
 }
+// orphans of dead registrations into column R + 1 of a group row (f_emit ticks: k_emit2
+// sums every row for O before the fill level; no log scan precedes it)
+__device__ __forceinline__ void count_orphans(const EvArgs &a, int tile, uint32_t n) {
+    if (a.orph_grp && n) atomicAdd(&a.grp[(tile % a.ngrp) * a.gstride + a.R + 1], n);
+}
 
 __device__ __forceinline__ void SlotRun::purge(const EvArgs &a, uint32_t s, int reg0) {
     bool died, evicted;
-    purge_slot(a, (int)s, true, reg0, reg, hb, fr, died_start, qstat != kQsOut, died, evicted);
+    const uint32_t no = purge_slot(a, (int)s, true, reg0, reg, hb, fr, died_start, qstat != kQsOut, infl0 - ncl,
+                                   died, evicted);
     if (died && a.dmask) atomicOr(&a.dmask[s >> 6], 1ull << (s & 63));
     if (evicted) count_evicted(a, (int)(s >> 8), 1u);
+    count_orphans(a, (int)(s >> 8), no);
 }
 
 __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
@@ -868,6 +910,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
         const int blk = (int)blockIdx.x - nba;
         const int s = blk * kBS + (int)threadIdx.x;
         bool died = false, evicted = false;
+        uint32_t no = 0;
         if (s < a.W) {
             // the link stamp says whether the slot got messages (its owner purges it); the
             // committed record loaded with it (no dependent round)
@@ -875,13 +918,16 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
             const int reg0 = a.reg[s];
             const double hb0 = a.hb[s];
             const int2 fq0 = a.free_in[s];
-            if (!t) purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, died, evicted);
+            const uint32_t in0 = a.infl_in ? a.infl_in[s] : 0u;
+            if (!t) no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, in0, died, evicted);
         }
         const uint64_t dm = __ballot(died);
         const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
+        const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
         if (lane_id() == 0) {
             if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
             if (ne) count_evicted(a, blk, ne);
+            count_orphans(a, blk, nw);
         }
         return;
     }
@@ -960,12 +1006,19 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
                 for (int i = 0; i < kLinkMax; ++i)
                     if ((i ^ j) > i) cx(i, i ^ j, (i & k) == 0);
     }
-    // every result's log entry in one load round, then the messages in order
+    // every result's log entry in one load round, then the messages in order; dp[k]: an
+    // earlier message of the slot completed message k's entry (a repeated result)
     int32_t lv[kLinkMax];
+    bool dp[kLinkMax];
 #pragma unroll
-    for (int k = 0; k < kLinkMax; ++k) lv[k] = k < n ? log_peek(a, sq[k]) : -1;
+    for (int k = 0; k < kLinkMax; ++k) {
+        lv[k] = k < n ? log_peek(a, sq[k]) : -1;
+        dp[k] = false;
+    }
     for (int m = 0; m < n; ++m) {
-        r.step<true>(a, s, idx[0], kd[0], vl[0], tt[0], sq[0], lv[0]);
+        const bool cl = r.step<true>(a, s, idx[0], kd[0], vl[0], tt[0], sq[0], lv[0], dp[0]);
+#pragma unroll
+        for (int k = 1; k < kLinkMax; ++k) dp[k] = dp[k] || (cl && sq[k] == sq[0]);
 #pragma unroll
         for (int k = 0; k + 1 < kLinkMax; ++k) {
             idx[k] = idx[k + 1];
@@ -974,6 +1027,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
             tt[k] = tt[k + 1];
             sq[k] = sq[k + 1];
             lv[k] = lv[k + 1];
+            dp[k] = dp[k + 1];
         }
     }
     r.finish(a, s, s);
@@ -1152,8 +1206,12 @@ __device__ __forceinline__ TickArgs specialise(TickArgs a) {
 __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t *l4) {
     const int s = blk * kBS + threadIdx.x;
     bool died_start = false, evicted = false;
+    uint32_t no = 0;  // orphans: in-flight entries of this slot's dead registration
     if (s < a.W) {
         const Cur c = cur_slot(a, s);
+        // in-flight entries after the messages (loaded with the record, selected after)
+        const uint32_t i0 = a.infl_out ? a.infl_in[s] : 0u;
+        const uint32_t ip = (a.infl_out && a.E > 0) ? a.post_infl[s] : 0u;
         const bool dead = is_dead(a, c);
         const bool alive = c.reg && !dead;
         died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
@@ -1163,14 +1221,25 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         // front / back insertion) -- k_emit2 then rewrites only the slots it serves
         const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
         a.free_out[s] = make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
+        if (a.infl_out) {
+            const uint32_t pin = c.t ? ip : i0;
+            a.infl_out[s] = (alive && !died_start) ? pin : 0u;  // a new registration starts empty
+            no = died_start ? pin : 0u;
+        }
         if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
             a.tokcnt_out[s] = 0;
             a.xw_out[s] = 0;
         }
     }
     const uint64_t dm = __ballot(died_start);
-    if ((!a.slots_in_scan || a.f_sep) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) {
+    if ((!a.slots_in_scan || a.f_sep || a.f_emit) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) {
         a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
+    }
+    if (a.f_emit) {
+        // O for the fill level: the dead registrations' in-flight counts (k_emit2's log
+        // tiles find the same entries, for the compaction)
+        const uint32_t nw = wave_sum_u32(no);
+        if (lane_id() == 0 && nw) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 1], nw);
     }
     const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
     if (lane_id() == 0) l4[wave_id()] = ev;
@@ -1191,6 +1260,24 @@ __global__ __launch_bounds__(kBS) void k_slots(TickArgs a_) {
     STAMP(a, 0, 0);
     slots_body(a, blockIdx.x, l4);
     STAMP(a, 0, 15);
+}
+
+// One-GPU message ticks: in-flight entry q of slot s was completed by one of this
+// tick's results (the log keeps it until the commit).  Only asked for entries whose
+// slot died this tick, so the gathers behind the touched test are rare.
+template <class A>
+__device__ __forceinline__ bool completed_now(const A &a, int s, int64_t q) {
+    return got_msg(a, s) && (a.post_rf[s] & kRfCleared) && a.ctag[q] == a.lstamp;
+}
+// drop the completed entries from a tile row's orphan flags (bit j: entry base + j)
+template <class A>
+__device__ __forceinline__ uint32_t drop_completed(const A &a, uint32_t flags, const int32_t *v, int64_t base) {
+    if (a.E == 0 || !a.ctag) return flags;
+    for (uint32_t m = flags; m; m &= m - 1) {
+        const int j = __builtin_ctz(m);
+        if (completed_now(a, v[j], base + j)) flags &= ~(1u << j);
+    }
+    return flags;
 }
 
 // The registration of slot s alive at tick start died during this tick (read
@@ -1217,7 +1304,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     __shared__ int32_t m4[kWaves];
     __shared__ unsigned long long s4[kWaves];
     __shared__ uint32_t wc[kWaves][kBS];
-    const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
+    const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
     // a.ffirst: log blocks first in hardware order (logical ids unchanged)
     int bid = blockIdx.x;
     if (a.ffirst) bid = bid < nbf ? bid + a.nbq : (bid < nbf + a.nbq ? bid - nbf : bid);
@@ -1292,7 +1379,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             died |= (v[j] >= 0 && ((wd >> (sj & 63)) & 1ull)) ? (1u << j) : 0u;
         }
         }
-        const uint32_t flags = died;
+        const uint32_t flags = drop_completed(a, died, v, base);
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
         const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
         if (lane_id() == 0) l4[wave_id()] = wv;
@@ -1316,6 +1403,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     }
     // ---- Q-role: LRU positions [b*256, +256) of fronts ++ queue ++ backs
     const int b = bid;
+    if (a.f_emit && b == 0 && threadIdx.x == 0) a.hout->fault = 0;  // k_emit2's log hand-offs
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
     int c = 0, oc = 0;
     if (a.shard == 2) {
@@ -1608,6 +1696,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
                 const int sc = sj < 0 ? 0 : sj;
                 flags |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
             }
+            flags = drop_completed(a, flags, v[k], (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems);
             a.ofl[(size_t)b * kBS + k * 64 + lane] = (uint8_t)flags;
             cnt += (uint32_t)__popc(flags);
         }
@@ -2070,6 +2159,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
             }
             // the worker's next {free, queued}: one 8-byte store
             a.free_out[s] = make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0);
+            if (a.infl_out && n_q) atomicAdd(&a.infl_out[s], (uint32_t)n_q);
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
@@ -2126,6 +2216,121 @@ __device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
     return x;
 }
 
+// Log workgroup of a fused one-GPU tick (f_emit): orphan flags and their compaction.
+// The slot purge (k_scan's W role or the apply launch) wrote the died-registration
+// bitmap and already counted O for the fill level, so nothing here is on the queue
+// role's path.  A ticket gives the workgroup its 4 log tiles in start order; its tiles'
+// entries are tested against the bitmap in LDS (coalesced 16-byte log loads, entry
+// t*2048 + 256k + 4*lane + j), its orphan count is published as an {lstamp, count}
+// granule, and its output offset is the sum of the earlier workgroups' granules -- one
+// polled load per thread (at most kFEmitMaxBlocks workgroups), waiting only on
+// workgroups that took earlier tickets and so are already running.  The poll is
+// bounded: a hand-off that never arrives flags hout->fault (the host fails the tick).
+__device__ __forceinline__ void emit_log_tiles(const TickArgs &a, unsigned long long *bm) {
+    __shared__ uint32_t tk;
+    __shared__ uint32_t wtot[kWaves], pre4[kWaves];
+    const int lane = lane_id(), w = wave_id();
+    if (threadIdx.x == 0) tk = (uint32_t)(atomicAdd(a.fticket, 1ull) - a.fticket0);
+    // the died bitmap (<= kLdsBitmapSlots bits) into LDS: <= 4 int4 per thread, all in flight
+    {
+        const int n4 = ((((a.W + 63) >> 6) + 1) >> 1);
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
+        uint4 t4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + k * kBS;
+            t4[k] = src[i < n4 ? i : n4 - 1];
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int i = threadIdx.x + k * kBS;
+            if (i < n4) reinterpret_cast<uint4 *>(bm)[i] = t4[k];
+        }
+    }
+    __syncthreads();  // the bitmap and the ticket
+    const int j = (int)tk;
+    const int64_t nlog = a.head_in;
+    const int64_t tbase = ((int64_t)4 * j + w) * kFTile;
+    const int64_t last4 = nlog > 0 ? ((nlog - 1) & ~(int64_t)3) : 0;
+    int32_t v[8][4];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const int64_t i = tbase + k * 256 + 4 * lane;
+        const int4 x = *reinterpret_cast<const int4 *>(a.log_slot + (i < last4 ? i : last4));
+        v[k][0] = i < nlog ? x.x : -1;
+        v[k][1] = i + 1 < nlog ? x.y : -1;
+        v[k][2] = i + 2 < nlog ? x.z : -1;
+        v[k][3] = i + 3 < nlog ? x.w : -1;
+    }
+    uint32_t f[8], cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        uint32_t m = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int sj = v[k][q], sc = sj < 0 ? 0 : sj;
+            m |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << q) : 0u;
+        }
+        f[k] = drop_completed(a, m, v[k], tbase + k * 256 + 4 * lane);
+        cnt += (uint32_t)__popc(f[k]);
+    }
+    const uint32_t wt = wave_sum_u32(cnt);
+    if (lane == 0) wtot[w] = wt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t bt = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+        __hip_atomic_store(a.fagg + j, ((unsigned long long)a.lstamp << 32) | bt, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // orphans of the earlier workgroups: thread i polls workgroup i's granule
+    uint32_t pv = 0;
+    if ((int)threadIdx.x < j) {
+        for (uint32_t spin = 0;; ++spin) {
+            const unsigned long long g =
+                __hip_atomic_load(a.fagg + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(g >> 32) == a.lstamp) {
+                pv = (uint32_t)g;
+                break;
+            }
+            if (spin > (1u << 22)) {
+                a.hout->fault = 1;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+    }
+    const uint32_t ps = wave_sum_u32(pv);
+    if (lane == 0) pre4[w] = ps;
+    __syncthreads();
+    int64_t off = (int64_t)pre4[0] + pre4[1] + pre4[2] + pre4[3];
+    for (int q = 0; q < w; ++q) off += wtot[q];
+    // entry order within the tile: k, then lane, then j
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        const uint32_t c = (uint32_t)__popc(f[k]);
+        const uint32_t incl = wave_incl_scan_u32(c);
+        int64_t o = off + (int64_t)(incl - c);
+        const int64_t e0 = tbase + k * 256 + 4 * lane;
+        for (uint32_t m = f[k]; m; m &= m - 1) wt_store(a.orphans + o++, (int64_t)(e0 + __builtin_ctz(m)));
+        off += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+    }
+}
+
+// XCD-aware order of the queue blocks: workgroups are dealt round-robin over the 8
+// XCDs (placement is a speed matter only), so logical block L = (i mod 8) * n/8 + i / 8
+// puts consecutive LRU segments on one XCD.  Each round's task range of block L ends
+// where block L + 1's begins, in the middle of a 128-byte line: written from one XCD's
+// L2 the two halves merge there, from two XCDs each L2 writes back a partial line.
+// A bijection on [0, n) for any n.
+#ifndef FAASBAL_XCD_MAP
+#define FAASBAL_XCD_MAP 1
+#endif
+__device__ __forceinline__ int xcd_block(int i, int n) {
+    if (!FAASBAL_XCD_MAP) return i;
+    const int x = i & 7, y = i >> 3, q = n >> 3, r = n & 7;
+    return x * q + (x < r ? x : r) + y;
+}
+
 // PLAN: large tables (round table beyond the fused limit, R <= 128) -- the same
 // emission with this block's prefixes and the totals from k_plan.
 template <int MODE, bool PLAN, int NCH>
@@ -2148,7 +2353,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const int qb0 = a.cfirst ? nbf4 + nbw4 : 0;  // first queue block
     const int cb0 = a.cfirst ? 0 : a.nbq;        // first compaction block
     if (bid >= qb0 && bid < qb0 + a.nbq) {
-        const int b = bid - qb0;
+        const int b = xcd_block(bid - qb0, a.nbq);
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
         const int R = a.R;       // 32, 64 or 128
         // ---- every load in flight at once (clamped indices, no branches)
@@ -2467,6 +2672,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // this tick -- the slot role already wrote {free, 1} for every queued one (a
             // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
             if (n_q != 0 || np < 0) wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
+            // the slot's in-flight entries: the purge wrote the count after its messages
+            if (a.infl_out && n_q) atomicAdd(&a.infl_out[s], (uint32_t)n_q);
             if (np >= 0) {
                 wt_store(a.queue_out + np, s);
                 wt_store(a.qfree_out + np, raw - (int32_t)n_q);
@@ -2480,6 +2687,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     // 256 slots), four tiles per workgroup -- a quarter of the blocks of one
     // thread per flag byte / slot, so they do not queue behind the queue role
     const bool frole = bid < cb0 + nbf4;
+    if (frole && a.f_emit) {
+        extern __shared__ __attribute__((aligned(16))) unsigned long long dynbm[];
+        emit_log_tiles(a, dynbm);
+        return;
+    }
     const int t0 = 4 * (frole ? bid - cb0 : bid - cb0 - nbf4);
     const int t = t0 + w;
     const int ntile = frole ? a.nbf : a.nbw;
@@ -2829,7 +3041,7 @@ void launch_slots(const TickArgs &a, Stream st) {
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
     const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : a.nbw;
-    const int nbf = (a.shard == 2 || a.f_sep) ? 0 : a.nbf;
+    const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;
     FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
 }
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
@@ -2847,10 +3059,12 @@ void launch_emit(const TickArgs &a, Stream st) {
 template <bool PLAN, int NCH>
 static void launch_emit2_t(const TickArgs &a, Stream st) {
     const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
+    // f_emit: the log workgroups stage the died bitmap in LDS (rounded to whole int4)
+    const size_t lds = a.f_emit ? (size_t)(((a.W + 63) / 64 + 1) / 2) * 16 : 0;
     switch (tick_mode(a)) {
-    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN, NCH>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
-    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN, NCH>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
-    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PLAN, NCH>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a); break;
+    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PLAN, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
     }
 }
 void launch_emit2(const TickArgs &a, Stream st) {

@@ -24,7 +24,8 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_selftest", "fb_debug_read", "fb_sync", "fb_set_stream", "fb_get_local_assignments",
            "fb_create_sharded", "fb_load_shard", "fb_read_shard_log", "fb_exchange_bytes", "fb_bind_exchange",
            "fb_tick_continue", "fb_create_deque", "fb_tick_stage", "fb_tick_launch_staged", "fb_host_alloc",
-           "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign", "fb_get_outputs")
+           "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign", "fb_get_outputs",
+           "fb_read_inflight")
 
 
 class TickResult(C.Structure):
@@ -119,6 +120,7 @@ def load(path=None):
         "fb_host_alloc": (C.c_int, [_P, i64, C.POINTER(_P)]),
         "fb_host_free": (C.c_int, [_P, _P]),
         "fb_purge_launch": (C.c_int, [_P, dbl, dbl]),
+        "fb_read_inflight": (C.c_int, [_P, _P]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name, None)

@@ -150,6 +150,12 @@ class GpuBalancer:
             out["log"] = log[: loglen.value]
         return out
 
+    def inflight(self):
+        """Per-slot count of in-flight log entries (committed state; one-GPU heartbeat)."""
+        out = np.zeros(max(self.n_workers, 1), np.uint32)
+        self._chk(self.lib.fb_read_inflight(self.h, _p(out)))
+        return out[: self.n_workers]
+
     # ----------------------------------------------------------------- ticks
     def launch(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0):
         if not len(ev_kind) and not len(ev_slot):

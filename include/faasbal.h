@@ -96,6 +96,11 @@ int fb_read_state(fb_ctx *ctx, uint8_t *registered, int32_t *free_processes,
                   double *last_heartbeat, uint32_t *epoch, int32_t *queue, int64_t *queue_len,
                   int32_t *log_slot, int64_t *log_len);
 
+/* One-GPU heartbeat contexts: in-flight log entries per slot of the committed state
+ * (n_workers words; build-defined bookkeeping of the redistribution, DESIGN.md §3:
+ * the count of the slot's entries that are neither completed nor redistributed). */
+int fb_read_inflight(fb_ctx *ctx, uint32_t *inflight);
+
 /* Enqueue one tick on the context's stream (no host sync).
  * Replaces, per tick: the inbound branches (task_dispatcher.py:343-387), the
  * purge (:241-249, called at :390) and the dispatch block (:393-419), plus the

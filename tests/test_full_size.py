@@ -106,7 +106,7 @@ def test_gpu_stream_1m_workers_matches_oracle():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_gpu_sharded_16m_x_1m_matches_oracle(world):
     """configs[3]: 16M pending tasks x 1M workers, the worker table sharded by
     slot range over `world` rank contexts on one GPU; the exchange buffers are
@@ -119,5 +119,34 @@ def test_gpu_sharded_16m_x_1m_matches_oracle(world):
     b = o.tick(1000.0, 10.0, [], [], [], [], [], T)
     assert len(b["assign"]) == res["n_assigned"] > 0 and len(b["orphans"]) > 0
     _cmp_sharded(bals, o, merged, b, 0)
+    for x in bals:
+        x.close()
+
+
+@pytest.mark.gpu
+def test_gpu_sharded_stream_1m_workers_world8_matches_oracle():
+    """configs[4] in its stated multi-GPU form: the 1M-worker table sharded by
+    worker-id range over 8 rank contexts (one GPU; the exchange summed on the
+    device, what the RCCL all-reduce computes), committed streaming ticks with
+    64K new tasks, 64K results, joins and heartbeats each, silent workers
+    expiring; every merged output and the reassembled state against the oracle
+    (heap purge)."""
+    from test_gpu_sharded import _cmp as _cmp_sharded, _group, _group_tick
+    W, T, world = 1 << 20, 65536, 8
+    st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=3, seed=2, tasks_per_tick=T, results_per_tick=T, dt=0.05)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    bals, o = _group(st, world, len(st["log"]) + 8 * T, max_events=E, purge_mode=2)
+    carried, n_orph = 0, 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a, res = _group_tick(bals, *args)
+        b = o.tick(*args)
+        assert len(b["assign"]) > 0
+        _cmp_sharded(bals, o, a, b, t)
+        n_orph += len(b["orphans"])
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert n_orph > 0, "silent workers must expire and their tasks be redistributed"
     for x in bals:
         x.close()

@@ -45,6 +45,10 @@ def _cmp_state(g, o, t):
     np.testing.assert_array_equal(sg["hb"][reg], so["hb"][reg], err_msg="tick %d hb" % t)
     np.testing.assert_array_equal(sg["queue"], so["queue"], err_msg="tick %d queue" % t)
     np.testing.assert_array_equal(sg["log"], so["log"], err_msg="tick %d log" % t)
+    # the per-slot in-flight counts (O of the fused tick) equal the log's live entries
+    live = so["log"][so["log"] >= 0]
+    np.testing.assert_array_equal(g.inflight(), np.bincount(live, minlength=len(so["reg"])).astype(np.uint32),
+                                  err_msg="tick %d in-flight counts" % t)
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
@@ -85,6 +89,37 @@ def test_random_multitick_vs_oracle(seed):
             mine = np.nonzero(log == tk["ev_slot"][i])[0]
             if len(mine) and tk["ev_pick"][i] % 5 != 4:
                 seq[i] = mine[tk["ev_pick"][i] % len(mine)]
+        n = carried + tk["n_new"]
+        args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp_out(a, b, t)
+        _cmp_state(g, o, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_random_results_any_entry_vs_oracle(seed):
+    """Results naming any log entry -- another worker's, a completed or redistributed
+    one, the same entry twice in a tick, before and after the sender's death and
+    re-registration -- against the oracle; in-flight counts checked every tick (the
+    log is read-only during a tick, the commit clears the completed entries)."""
+    W = [7, 64, 500, 3000][seed % 4]
+    scen = synth.random_scenario(5000 + seed, W=W, n_ticks=8, max_events=[40, 400, 3000][seed % 3],
+                                 max_new=[60, 500, 4000][(seed // 3) % 3])
+    g, o = _pair(_state(scen), len(scen["init_log"]) + 60000)
+    rng = np.random.default_rng(seed)
+    carried = 0
+    for t, tk in enumerate(scen["ticks"]):
+        head = o.export()["head"]
+        log = o.export()["log"]
+        E = len(tk["ev_kind"])
+        seq = rng.integers(-1, max(head, 1), E).astype(np.int64)
+        own = np.nonzero(tk["ev_kind"] == synth.EV_RESULT)[0]
+        # half the results name one of the sender's own entries (often the same one twice)
+        for i in own[: len(own) // 2]:
+            mine = np.nonzero(log == tk["ev_slot"][i])[0]
+            if len(mine):
+                seq[i] = mine[rng.integers(0, min(len(mine), 2))]
         n = carried + tk["n_new"]
         args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
         a, b = g.tick(*args), o.tick(*args)

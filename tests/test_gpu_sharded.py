@@ -15,7 +15,7 @@ from oracle import Oracle
 pytestmark = pytest.mark.gpu
 
 
-def _group(st, world, log_cap, max_events=4096):
+def _group(st, world, log_cap, max_events=4096, purge_mode=1):
     import torch  # noqa: F401  (loads the HIP runtime before libfaasbal)
     from faasbal.sharded import ShardedBalancer
 
@@ -23,7 +23,7 @@ def _group(st, world, log_cap, max_events=4096):
     bals = [ShardedBalancer(r, world, W, log_cap, max_events=max_events) for r in range(world)]
     for b in bals:
         b.load(st)
-    o = Oracle(W, log_cap)
+    o = Oracle(W, log_cap, purge_mode=purge_mode)
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
     return bals, o
 
