@@ -116,6 +116,11 @@ struct fb_ctx {
     unsigned long long fticket_n = 0;  // tickets handed out so far (the next launch's base)
     uint32_t lstamp = 0;               // per enqueued launch, reruns included (never 0)
     int f_emit = 1;                    // FAASBAL_F_EMIT=0: fused ticks keep k_scan's log blocks (A/B knob)
+    // compact assignments (fb_set_compact): slot and min(c, L + 1) per LRU position
+    int32_t *rb_slot = nullptr;
+    uint8_t *rb_c = nullptr;
+    int compact = 0, l_compact = 0;    // the setting, and the one the last launch ran with
+    HostPool *xpool = nullptr;         // fb_expand_compact's workers (created on first use)
     int32_t *trash = nullptr;  // kTrashRows x kBS words written by inactive lanes (never read)
     int64_t Qn = 0, head = 0;
     uint32_t tick = 1;
@@ -573,7 +578,7 @@ int enqueue_tick(fb_ctx *c) {
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         ea.link = c->link;
         ea.hout = c->hout_dev;
-        ea.defer_clr = 1;  // the linked-list path exists on one-GPU heartbeat contexts only
+        ea.defer_clr = defer ? 1 : 0;
         ea.ev_clr = c->ev_clr;
         ea.ctag = c->ctag;
         ea.lstamp = c->lstamp;
@@ -581,6 +586,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.post_infl = c->post_infl;
         ea.infl_out = c->infl[nxt];
         ea.orph_grp = (a.f_emit && c->purge_apply) ? 1 : 0;
+        if (!defer) ea.infl_in = ea.post_infl = ea.infl_out = nullptr;
         if (c->cm_pending) {  // the previous tick's commit rides in this launch
             ea.cm = c->cm;
             ea.cm_blocks = c->cm_grid;
@@ -746,6 +752,11 @@ int enqueue_tick(fb_ctx *c) {
     a.P_rep = c->P_rep;
     a.repl = (gplan && c->repl) ? 1 : 0;  // k_plan2 writes a copy per group
     a.trash = c->trash;
+    c->l_compact = c->compact && !c->shard;
+    if (c->l_compact) {
+        a.rb_slot = c->rb_slot;
+        a.rb_c = c->rb_c;
+    }
     a.arena = (char *)c->arena;
     a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !c->no_arena32) ? 1 : 0;
     a.log_slot = c->log_slot;
@@ -943,6 +954,10 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     }
     ap.add(&c->c_arr, Qlog);
     if (!shard) {
+        ap.add(&c->rb_slot, Qlog);
+        ap.add(&c->rb_c, Qlog);
+    }
+    if (!shard) {
         ap.add(&c->c_hb, Qlog);
     }
     ap.add(&c->qbmax, (size_t)cdiv(Qlog, kBS));
@@ -979,7 +994,9 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->post_nf, W);
         ap.add(&c->c_tok, Qlog);
     }
-    if (!shard && !c->deque) {
+    // in-flight counts only where the fused tick can use them (the died bitmap of the
+    // log workgroups fits in LDS); larger tables keep k_logscan and in-place clears
+    if (!shard && !c->deque && W <= (size_t)kLdsBitmapSlots) {
         ap.add(&c->infl[0], W);
         ap.add(&c->infl[1], W);
         ap.add(&c->post_infl, W);
@@ -1099,6 +1116,7 @@ int fb_destroy(fb_ctx *c) {
     if (c->hout) hipHostFree(c->hout);
     if (c->h_stage) hipHostFree(c->h_stage);
     delete c->pool;
+    delete c->xpool;
     if (c->cp_s) hipStreamSynchronize(c->cp_s);
     for (int h = 0; h < 2; ++h) {
         if (c->stage_ev[h]) hipEventDestroy(c->stage_ev[h]);
@@ -1746,6 +1764,74 @@ int fb_get_outputs(fb_ctx *c, int32_t *assign, int64_t *orphans, int32_t *evicte
         return rc;
     if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
+}
+
+int fb_set_compact(fb_ctx *c, int enable) {
+    if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "compact assignments exist on one-GPU contexts only");
+    c->compact = enable != 0;
+    return FB_OK;
+}
+
+int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, int64_t *n_pos, int64_t *orphans,
+                           int32_t *evicted) {
+    if (!c || !n_pos) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    if (!c->l_compact) return fail(c, FB_ESTATE, "the tick was launched without fb_set_compact");
+    if (c->last.fill_level + 1 > 255)
+        return fail(c, FB_ERANGE, "fill level %d: rounds beyond a byte, read fb_get_outputs", c->last.fill_level);
+    const int64_t n = c->l_Qn + 2 * (int64_t)c->l_E;
+    *n_pos = n;
+    if ((slot || cnt) && cap < n) return fail(c, FB_EINVAL, "compact buffers of %lld < %lld positions", (long long)cap,
+                                              (long long)n);
+    HIPCHK(c, hipSetDevice(c->device));
+    int rc;
+    if (slot && n && (rc = d2h(c, slot, c->rb_slot, (size_t)n * 4))) return rc;
+    if (cnt && n && (rc = d2h(c, cnt, c->rb_c, (size_t)n))) return rc;
+    if (orphans && c->last.n_orphans_local &&
+        (rc = d2h(c, orphans, c->orphans, (size_t)c->last.n_orphans_local * 8)))
+        return rc;
+    if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
+}
+
+// Host: every task's slot from the compact form of the waited tick.  Round r <= L
+// serves the positions with c > r in LRU order, task S(r) + j going to the j-th of
+// them; S(r) = sum of min(c, r).  The rounds are independent ranges of the output,
+// so they are expanded in parallel (FAASBAL_EXPAND_THREADS workers, default 8).
+int fb_expand_compact(fb_ctx *c, const int32_t *slot, const uint8_t *cnt, int64_t n_pos, int32_t *assign) {
+    if (!c || (n_pos && (!slot || !cnt)) || (!assign && c->last.n_assigned)) return FB_EINVAL;
+    if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
+    const int L = c->last.fill_level;
+    const int64_t N = c->last.n_assigned;
+    if (L + 1 > 255) return fail(c, FB_ERANGE, "fill level %d beyond the compact form", L);
+    // A(r) = #{c > r}, S(r + 1) = S(r) + A(r), r <= L
+    std::vector<int64_t> hist(L + 3, 0), S(L + 2, 0);
+    for (int64_t i = 0; i < n_pos; ++i) hist[std::min<int>(cnt[i], L + 2)]++;
+    int64_t above = 0;
+    std::vector<int64_t> A(L + 2, 0);
+    for (int r = L + 1; r >= 0; --r) {
+        above += hist[r + 1];
+        A[r] = above;
+    }
+    for (int r = 0; r <= L; ++r) S[r + 1] = S[r] + A[r];
+    if (S[L] > N || N > S[L + 1]) return fail(c, FB_EINVAL, "compact form does not match the waited tick");
+    if (!c->xpool) {
+        const char *e = getenv("FAASBAL_EXPAND_THREADS");
+        c->xpool = new HostPool(std::max(1, std::min(e ? atoi(e) : 8, 64)));
+    }
+    const int np = c->xpool->size();
+    c->xpool->run([&](int t) {
+        for (int r = t; r <= L; r += np) {
+            int32_t *o = assign + S[r];
+            const int64_t lim = std::min<int64_t>(A[r], N - S[r]);
+            int64_t k = 0;
+            for (int64_t i = 0; i < n_pos && k < lim; ++i)
+                if (cnt[i] > r) o[k++] = slot[i];
+        }
+    });
     return FB_OK;
 }
 

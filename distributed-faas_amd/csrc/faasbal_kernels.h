@@ -269,6 +269,8 @@ struct TickArgs {
     // outputs
     int32_t *log_slot;
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
+    int32_t *rb_slot;   // compact assignments (null: off): slot per LRU position, -1 none
+    uint8_t *rb_c;      // ... and min(c, L + 1) (clamped to 255)
     char *arena;        // base of the context's arena (every buffer above)
     int arena32;        // 1: the arena spans < 4 GB (32-bit byte offsets from arena)
     int2 *free_out;     // next {free_processes (INT32_MIN: no live record), queued}

@@ -711,11 +711,13 @@ struct SlotRun {
             const int64_t q = seq;
             if (q >= 0 && q < a.head_in) {
                 if (PF) {
-                    // one GPU: the entry's slot loaded ahead; the log stays as committed
-                    // (the commit clears the entry), ctag names the entry for this launch
+                    // one GPU: the entry's slot loaded ahead.  defer_clr: the log stays as
+                    // committed (the commit clears the entry), ctag names the entry for this
+                    // launch; else cleared in place (clearing it twice is harmless)
                     if (logv == (int32_t)gs && !dup) {
                         cleared = true;
-                        a.ctag[q] = a.lstamp;
+                        if (a.defer_clr) a.ctag[q] = a.lstamp;
+                        else a.log_slot[q] = -1;
                     }
                 } else if (a.defer_clr) {
                     // sorted path, one GPU: a slot may carry any number of results; the
@@ -1960,6 +1962,16 @@ __device__ __forceinline__ void deque_finish(const TickArgs &a, int64_t pos, int
     }
 }
 
+// The tick's assignments in compact form (fb_get_outputs_compact): per LRU position its
+// slot and min(c, L + 1) -- with the fill level, every task's slot in closed form
+// (task k of round r <= L is A_r[k - S(r)]) in 5 bytes per queued worker instead of 4
+// bytes per task.  c = 0: no live queued worker at this position.
+__device__ __forceinline__ void compact_out(const TickArgs &a, int64_t pos, int s, int c, int L) {
+    const int cl = c < L + 1 ? c : L + 1;
+    a.rb_slot[pos] = c > 0 ? s : -1;
+    a.rb_c[pos] = (uint8_t)(cl < 255 ? cl : 255);
+}
+
 // ------------------------------------------------------------ k_emit
 // Water-filling emission for one queue block once the fill level is known:
 // rounds [0, rfull) in full, round L partially (ranks < p), round L+1 ranks.
@@ -2054,6 +2066,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
         if (status) return;
         // ---- water-filling emission, 256 rounds per chunk, rounds 0 .. L+1
         const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
+        if (a.rb_slot && pos < a.Qlog) compact_out(a, pos, s, c, L);
         int32_t *const out = a.log_slot + a.head_in;
         int64_t rankL = -1, exL1 = 0;
         int64_t carryS = 0;  // S(rc)
@@ -2577,6 +2590,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int s = s0;
         // free <= 0 still takes one task; deque mode: c_arr holds the token's c itself
         const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
+        if (a.rb_slot && pos < a.Qlog) compact_out(a, pos, s, c, L);
         int32_t rbv[NCH], basev[NCH];
 #pragma unroll
         for (int k = 0; k < NCH; ++k) {

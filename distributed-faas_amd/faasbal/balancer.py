@@ -233,6 +233,39 @@ class GpuBalancer:
                 None if orphans is None else orphans[: r["n_orphans_local"]],
                 None if evicted is None else evicted[: r["n_evicted"]])
 
+    def set_compact(self, on=True):
+        """Ticks launched afterwards also write the compact assignment form (slot and
+        min(c, L + 1) per LRU position): ``outputs_compact`` then reads 5 bytes per
+        queued worker instead of 4 per task."""
+        self._chk(self.lib.fb_set_compact(self.h, 1 if on else 0))
+
+    def outputs_compact(self, slot, c, orphans=None, evicted=None):
+        """The waited tick's compact assignments into ``slot`` (int32) / ``c`` (uint8),
+        plus orphans and evicted slots, one synchronisation; returns the filled views
+        (slot, c, orphans, evicted).  ``expand(slot, c)`` gives the per-task slots."""
+        r = self.last
+        for a, n, dt in ((orphans, r["n_orphans_local"], np.int64), (evicted, r["n_evicted"], np.int32)):
+            if a is not None and (len(a) < n or a.dtype != dt):
+                raise ValueError("output array too small or of the wrong type")
+        if slot.dtype != np.int32 or c.dtype != np.uint8 or len(c) < len(slot):
+            raise ValueError("slot must be int32, c uint8 of at least as many entries")
+        n = C.c_int64()
+        self._chk(self.lib.fb_get_outputs_compact(self.h, _p(slot), _p(c), len(slot), C.byref(n),
+                                                  None if orphans is None else _p(orphans),
+                                                  None if evicted is None else _p(evicted)))
+        return (slot[: n.value], c[: n.value], None if orphans is None else orphans[: r["n_orphans_local"]],
+                None if evicted is None else evicted[: r["n_evicted"]])
+
+    def expand(self, slot, c, out=None):
+        """Per-task slots (``assignments()``) from the compact form (host, parallel)."""
+        n = self.last["n_assigned"]
+        if out is None:
+            out = np.zeros(max(n, 1), np.int32)
+        slot = np.ascontiguousarray(slot, np.int32)
+        c = np.ascontiguousarray(c, np.uint8)
+        self._chk(self.lib.fb_expand_compact(self.h, _p(slot), _p(c), len(slot), out.ctypes.data_as(C.c_void_p)))
+        return out[:n]
+
     def local_assignments(self, first=0, n=None):
         """(task index, slot) of the tasks given to this context's workers."""
         n = self.last["n_local"] - first if n is None else n

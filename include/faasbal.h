@@ -155,6 +155,21 @@ int fb_get_event_status(fb_ctx *ctx, int32_t n, uint8_t *dst); /* FB_EVS_* per e
  * transfers back to back. */
 int fb_get_outputs(fb_ctx *ctx, int32_t *assign, int64_t *orphans, int32_t *evicted);
 
+/* Compact assignments (one-GPU contexts).  After fb_set_compact(ctx, 1) every tick
+ * also writes, per position of its LRU order (fronts ++ queue ++ backs, n_pos of them),
+ * the slot and min(c, L + 1) of the worker there (c = effective free count, 0 = no live
+ * queued worker): with the fill level L this determines every assignment of the tick
+ * (task k of round r <= L goes to the (k - S(r))-th position with c > r), in 5 bytes per
+ * position instead of 4 per task (configs[2]: 0.3 MB instead of 4.1 MB to read back).
+ * fb_get_outputs_compact copies that form plus the orphans and evicted slots with one
+ * synchronisation (cap = entries of slot / c; *n_pos = positions written; FB_ERANGE
+ * when L + 1 > 255); fb_expand_compact turns it into fb_get_assignments' array on the
+ * host (result->n_assigned slots). */
+int fb_set_compact(fb_ctx *ctx, int enable);
+int fb_get_outputs_compact(fb_ctx *ctx, int32_t *slot, uint8_t *c, int64_t cap, int64_t *n_pos, int64_t *orphans,
+                           int32_t *evicted);
+int fb_expand_compact(fb_ctx *ctx, const int32_t *slot, const uint8_t *c, int64_t n_pos, int32_t *assign);
+
 /* Pinned host memory: fb_get_* copies into it are single DMA transfers on the
  * context stream (the drop-in's readback of a tick's assignments). */
 int fb_host_alloc(fb_ctx *ctx, int64_t bytes, void **ptr);

@@ -128,6 +128,47 @@ def test_random_results_any_entry_vs_oracle(seed):
         carried = n + len(b["orphans"]) - len(b["assign"])
 
 
+def _compact_matches(g, where):
+    """The compact form (slot, min(c, L + 1) per LRU position) read back and expanded
+    on the host equals the per-task assignments."""
+    n = g.last["n_assigned"]
+    cap = g.max_workers + 2 * g.max_events + 16
+    slot, c = g.pinned(cap, np.int32), g.pinned(cap, np.uint8)
+    slot, c, _, _ = g.outputs_compact(slot, c)
+    np.testing.assert_array_equal(g.expand(slot, c), g.assignments(), err_msg=where)
+    return n
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_compact_assignments_random_multitick(seed):
+    W = [5, 37, 300, 1000][seed % 4]
+    scen = synth.random_scenario(7000 + seed, W=W, n_ticks=5, max_events=[20, 200, 2000][seed % 3],
+                                 max_new=[50, 400, 3000][(seed // 3) % 3])
+    g, o = _pair(_state(scen), len(scen["init_log"]) + 40000)
+    g.set_compact(True)
+    carried = 0
+    for t, tk in enumerate(scen["ticks"]):
+        n = carried + tk["n_new"]
+        args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        g.launch(*args)
+        g.wait()
+        _compact_matches(g, "seed %d tick %d" % (seed, t))
+        g.commit()
+        b = o.tick(*args)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+def test_compact_assignments_config2():
+    st = synth.zipf_state(W=65536, seed=0)
+    T = 1_000_000
+    g = GpuBalancer(65536, 2 * len(st["log"]) + T + 16, max_events=1)
+    g.load(st)
+    g.set_compact(True)
+    g.launch(1000.0, 10.0, n_pending=T)
+    r = g.wait()
+    assert _compact_matches(g, "configs[2]") == r["n_assigned"] > 0
+
+
 def _one_tick_full(st, T, now=1000.0, tte=10.0):
     cap = len(st["log"]) + T + len(st["log"]) + 16
     g, o = _pair(st, cap)
