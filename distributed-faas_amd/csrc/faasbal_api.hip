@@ -221,6 +221,10 @@ struct fb_ctx {
     size_t arena_bytes = 0;
     bool table_owned = false; // qcnt/qpre grown beyond the arena's reservation
     bool A_owned = false;
+    size_t seg_cap = 0;       // entries (per row of 4) of segcnt and the sharded ocnt/opre/osegcnt
+    bool seg_owned = false;
+    int oA_cap = 0;
+    bool oA_owned = false;
     // last launch
     bool launched = false, waited = false;
     double l_now = 0, l_tte = 0;
@@ -247,6 +251,7 @@ struct fb_ctx {
     uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
     int64_t xcap = 0;
     int phase = 0;                                    // 1: phase 1 enqueued; 2: phase 2 enqueued
+    int shard_R = 0;                                  // > 0: round rows a relaunch asked for (FB_ERERUN)
     hipStream_t own_s = nullptr;                      // the context's own stream (fb_set_stream may borrow another)
 };
 
@@ -394,6 +399,36 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
         c->R_cap = R;
         c->A_owned = true;
     }
+    // per-segment round counts (4 rows per block) and, sharded, this rank's tables: the
+    // arena holds them for 128 rows; wider sharded tables get their own, grown the same way
+    if (c->shard && need > c->seg_cap) {
+        const size_t cap = std::max(need, c->seg_cap * 2);
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->seg_owned) {
+            hipFree(c->segcnt);
+            hipFree(c->osegcnt);
+            hipFree(c->ocnt);
+            hipFree(c->opre);
+        }
+        c->segcnt = c->osegcnt = c->ocnt = nullptr;
+        c->opre = nullptr;
+        int rc;
+        if ((rc = dalloc(c, &c->segcnt, 4 * cap))) return rc;
+        if (c->shard && ((rc = dalloc(c, &c->osegcnt, 4 * cap)) || (rc = dalloc(c, &c->ocnt, cap)) ||
+                         (rc = dalloc(c, &c->opre, cap))))
+            return rc;
+        c->seg_cap = cap;
+        c->seg_owned = true;
+    }
+    if (c->shard && R > c->oA_cap) {
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->oA_owned) hipFree(c->oA);
+        c->oA = nullptr;
+        int rc;
+        if ((rc = dalloc(c, &c->oA, (size_t)R))) return rc;
+        c->oA_cap = R;
+        c->oA_owned = true;
+    }
     return FB_OK;
 }
 
@@ -403,16 +438,18 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
 struct XLayout {
     size_t rec, front, back, evs, c8, total;
 };
-XLayout xlayout(int world, int64_t E, int64_t Qlog) {
+// xcw: bytes per exchanged c (1 while the round table has <= kRFused rows, else 2)
+XLayout xlayout(int world, int64_t E, int64_t Qlog, int xcw = 1) {
     XLayout x;
     x.rec = 0;
     x.front = (size_t)8 * kXRecWords * world;
     x.back = x.front + 4 * (size_t)E;
     x.evs = x.back + 4 * (size_t)E;
-    x.c8 = x.evs + (size_t)E;
-    x.total = (x.c8 + (size_t)Qlog + 15) & ~(size_t)15;
+    x.c8 = (x.evs + (size_t)E + 1) & ~(size_t)1;  // 2-byte aligned for the wide form
+    x.total = (x.c8 + (size_t)xcw * (size_t)Qlog + 15) & ~(size_t)15;
     return x;
 }
+inline int xc_width(int R) { return R > kRFused ? 2 : 1; }
 
 int choose_R(int32_t maxc) {
     int R = 32;
@@ -446,7 +483,7 @@ int enqueue_tick(fb_ctx *c) {
     int rc;
     if ((rc = ensure_table(c, R, nbq))) return rc;
     const int cur = c->cur, nxt = 1 - cur;
-    const XLayout xl = xlayout(c->world, E, Qlog);
+    const XLayout xl = xlayout(c->world, E, Qlog, xc_width(R));
     int32_t *front = c->front_list, *back = c->back_list;
     uint8_t *evs = c->ev_status;
     if (c->shard) {
@@ -777,6 +814,7 @@ int enqueue_tick(fb_ctx *c) {
         a.lseq = c->lseq;
         a.lseq_out = c->lseq;
         a.xc8 = c->xbuf + xl.c8;
+        a.xcw = xc_width(R);
         a.xrec = (unsigned long long *)(c->xbuf + xl.rec);
         a.ocnt = c->ocnt;
         a.osegcnt = c->osegcnt;
@@ -817,7 +855,7 @@ int enqueue_tick(fb_ctx *c) {
         return FB_OK;
     }
     if (a.shard == 2) {
-        if (R > kRFused) return fail(c, FB_ERANGE, "sharded tick: round table of %d rows (limit %d)", R, kRFused);
+        if (R > kShardMaxR) return fail(c, FB_ERANGE, "sharded tick: round table of %d rows (limit %d)", R, kShardMaxR);
         {
             Timer t(c, "scan2");
             launch_scan(a, t.st());
@@ -1018,6 +1056,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc) {
         c->table_cap = tab;
         c->R_cap = 128;
+        c->seg_cap = tab;
+        c->oA_cap = 128;
     }
     if (!rc && hipHostMalloc((void **)&c->hout, sizeof(HostOut), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
         rc = FB_ENOMEM;
@@ -1111,6 +1151,13 @@ int fb_destroy(fb_ctx *c) {
         hipFree(c->qpre);
     }
     if (c->A_owned) hipFree(c->A);
+    if (c->seg_owned) {
+        hipFree(c->segcnt);
+        hipFree(c->osegcnt);
+        hipFree(c->ocnt);
+        hipFree(c->opre);
+    }
+    if (c->oA_owned) hipFree(c->oA);
     if (c->dbg) hipFree(c->dbg);
     if (c->arena) hipFree(c->arena);
     if (c->hout) hipHostFree(c->hout);
@@ -1369,7 +1416,9 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
     if (!c || !bytes) return FB_EINVAL;
     const int64_t E = n_events < 0 ? c->E_cap : n_events;
     const int64_t Qn = n_events < 0 ? c->Wq_cap : (c->launched ? c->l_Qn : c->Qn);
-    *bytes = (int64_t)xlayout(c->world, E, Qn + 2 * E).total;
+    // the maximum: room for the wide form; a launched tick: its own width
+    const int xcw = n_events < 0 ? 2 : xc_width(c->launched ? c->l_R : kRFused);
+    *bytes = (int64_t)xlayout(c->world, E, Qn + 2 * E, xcw).total;
     return FB_OK;
 }
 
@@ -1536,10 +1585,10 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->tick += 1;  // per-launch stamp: a relaunch with other messages never sees this launch's marks
     if (c->tbitsb[0]) c->tbits = c->tbitsb[c->tick & 1];  // the last tick's bits stay for its deferred commit
     c->l_R = choose_R(std::max(c->maxc_hint, c->st_vmax));
-    // sharded: a round table of at most 128 rows whatever the free counts (k_emit_shard);
-    // counts beyond it are exact for every round below the table (the exchange clamps c
-    // to a byte, 255 > 128), so only a fill level reaching the table fails the tick
-    if (c->shard) c->l_R = std::min(c->l_R, kRFused);
+    // sharded: the round table starts at <= 128 rows (one byte per exchanged c: every
+    // round below the table is exact, 255 > 128); a fill level reaching the table makes
+    // fb_tick_wait ask for a relaunch, which gets a wider table (two bytes per c)
+    if (c->shard) c->l_R = std::min(c->shard_R > 0 ? c->shard_R : std::min(c->l_R, kRFused), kShardMaxR);
     c->reruns = 0;
     c->l_resort = false;
     c->launched = true;
@@ -1599,9 +1648,17 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
                         (long long)c->l_head, (long long)c->log_cap);
         // the queue holds free counts beyond the round table: widen and rerun
-        if (c->shard)
-            return fail(c, FB_ERANGE, "sharded tick: the fill level reaches the %d-round table (max free %d)",
-                        c->l_R, c->hout->maxc);
+        if (c->shard) {
+            // the exchange runs between the phases, so the caller relaunches: the same tick
+            // with a table sized by the max free count seen (clamped to the exchange width)
+            const int R = choose_R(c->hout->maxc);
+            if (c->l_R >= kShardMaxR || R <= c->l_R)
+                return fail(c, FB_ERANGE, "sharded tick: fill level beyond a %d-round table (max free %d)", c->l_R,
+                            c->hout->maxc);
+            c->shard_R = std::min(R, kShardMaxR);
+            return fail(c, FB_ERERUN, "sharded tick: the fill level reaches the %d-round table; relaunch (%d rows)",
+                        c->l_R, c->shard_R);
+        }
         const int R = choose_R(c->hout->maxc);
         if (R <= c->l_R || c->reruns > 4)
             return fail(c, FB_ERANGE, "fill level beyond the round table (maxc %d, R %d)", c->hout->maxc, c->l_R);
@@ -1671,6 +1728,9 @@ int fb_tick_commit(fb_ctx *c) {
         }
     }
     c->cur = 1 - c->cur;
+    // sharded: a tick that needed a wide table keeps it for the next one while the fill
+    // level stays beyond the narrow table (no relaunch per tick)
+    if (c->shard) c->shard_R = c->last.fill_level + 2 > kRFused ? c->l_R : 0;
     c->head = c->last.log_head;
     c->head_local += c->shard ? c->last.n_local : 0;
     c->Qn = c->last.queue_len;

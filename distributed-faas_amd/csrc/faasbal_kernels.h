@@ -26,6 +26,7 @@ constexpr int kPeel = 4;           // fused tick: block-count arrays of at most 
 constexpr int kLdsBitmapSlots = 1 << 17;  // died bitmap staged in LDS up to 128K slots (16 KB)
 constexpr int kLsBS = 1024;        // k_logscan: one 16-wave workgroup per CU
 constexpr int kGrpWords = 64 * 132;  // fused path: group rows of round totals (<= 64 groups x (128 + 4) words)
+constexpr int kShardMaxR = 4096;     // sharded round tables (k_emit_shard_wide: 64 chunks of 64 rounds)
 
 // event kinds / status (include/faasbal.h)
 constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3;
@@ -289,7 +290,8 @@ struct TickArgs {
     int64_t head_local;            // local log entries; lseq[i] = global sequence of entry i (ascending)
     const uint32_t *lseq;
     uint32_t *lseq_out;
-    uint8_t *xc8;                  // exchange: min(c, 255) per LRU position (single contributor per byte)
+    uint8_t *xc8;                  // exchange: c per LRU position (single contributor per byte), xcw bytes each:
+    int xcw;                       // 1: min(c, 255) while the round table has <= 128 rows, 2: min(c, 65535)
     unsigned long long *xrec;      // exchange: per rank kXRecLines orphan-count partials, one per 128-B line
     uint32_t *ocnt;                // [block][round] counts of this rank's positions
     uint32_t *osegcnt;             // [64-position segment][round] counts of this rank's positions

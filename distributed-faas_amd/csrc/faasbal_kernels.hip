@@ -1292,6 +1292,17 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
     return (rf & 1) && ((a.now - a.post[s].hb) > a.tte);
 }
 
+// Sharded exchange of the effective free counts: one byte per LRU position while the
+// round table has at most 128 rows (every c that matters is below the 255 clamp), two
+// bytes (clamp 65535) for wider tables.  Either way one rank writes each position.
+__device__ __forceinline__ int xc_get(const TickArgs &a, int64_t pos) {
+    return a.xcw == 2 ? (int)reinterpret_cast<const uint16_t *>(a.xc8)[pos] : (int)a.xc8[pos];
+}
+__device__ __forceinline__ void xc_put(const TickArgs &a, int64_t pos, int c) {
+    if (a.xcw == 2) reinterpret_cast<uint16_t *>(a.xc8)[pos] = (uint16_t)(c < 65535 ? c : 65535);
+    else a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
+}
+
 // ------------------------------------------------------------ k_scan
 // F-blocks flag orphaned log entries (died bitmap in LDS); Q-blocks compute the
 // effective free count c of every LRU position and the block's count of c > r
@@ -1412,7 +1423,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         // phase 2 of a sharded tick: every rank's effective free counts arrived in the exchange
         // both loads issued together (a guarded slot load would wait for the c byte first)
         const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
-        const int cq = a.xc8[pq];
+        const int cq = xc_get(a, pq);
         const int sq = lq_slot(a, pq);
         if (pos < a.Qlog) {
             c = cq;
@@ -1508,12 +1519,12 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             a.c_arr[pos] = raw;
             if (!a.shard) a.c_hb[pos] = hbq;
         }
-        if (a.shard == 1) a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
+        if (a.shard == 1) xc_put(a, pos, c);
     }
     STAMP(a, SO, 1);
     if (a.shard == 1) {
-        // phase 1 ends with the c bytes: phase 2 re-derives capacity and max c from
-        // them (exact below the 128-row round table: the byte clamp is 255).
+        // phase 1 ends with the c values: phase 2 re-derives capacity and max c from
+        // them (exact below the round table: its rows stay below the clamp).
         // Per-wave atomics on one exchange word cost ~10 ns each, serialised --
         // 14 K of them per tick at 8 ranks.
         STAMP(a, SO, 15);
@@ -1524,40 +1535,44 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     unsigned long long csum = 0;
     if (a.shard == 2) {
         // phase 2: the round counts of all positions and of this rank's, one ballot per
-        // round for both (rounds < R <= 128: two 64-round groups at most)
+        // round for both, 256 rounds (four 64-round groups) per pass
         __shared__ uint32_t owc[kWaves][kBS];
         const uint64_t own = __ballot(oc > 0);
+        for (int rc = 0; rc < a.R; rc += kBS) {
+            const int rn = (a.R - rc) < kBS ? (a.R - rc) : kBS;
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
-            const int r0 = g * 64;
-            uint32_t cnt = 0, ocnt = 0;
-            if (r0 < a.R && r0 < (int)wmx) {
-                int k = a.R - r0;
-                k = k < 64 ? k : 64;
-                k = k < (int)wmx - r0 ? k : (int)wmx - r0;
-                wave_round_counts2(c, own, r0, k, cnt, ocnt);
+            for (int g = 0; g < kBS / 64; ++g) {
+                const int r0 = rc + g * 64;
+                uint32_t cnt = 0, ocnt = 0;
+                if (r0 < rc + rn && r0 < (int)wmx) {
+                    int k = rc + rn - r0;
+                    k = k < 64 ? k : 64;
+                    k = k < (int)wmx - r0 ? k : (int)wmx - r0;
+                    wave_round_counts2(c, own, r0, k, cnt, ocnt);
+                }
+                wc[wave_id()][g * 64 + lane_id()] = cnt;
+                owc[wave_id()][g * 64 + lane_id()] = ocnt;
+                // per 64-position segment: k_emit_shard's in-block rank bases
+                if (g * 64 + lane_id() < rn) {
+                    const size_t si = (size_t)(4 * b + wave_id()) * a.R + r0 + lane_id();
+                    a.segcnt[si] = cnt;
+                    a.osegcnt[si] = ocnt;
+                }
             }
-            wc[wave_id()][g * 64 + lane_id()] = cnt;
-            owc[wave_id()][g * 64 + lane_id()] = ocnt;
-            // per 64-position segment: k_emit_shard's in-block rank bases
-            if (g * 64 + lane_id() < a.R) {
-                const size_t si = (size_t)(4 * b + wave_id()) * a.R + g * 64 + lane_id();
-                a.segcnt[si] = cnt;
-                a.osegcnt[si] = ocnt;
+            lds_barrier();
+            uint32_t t = 0;
+            if ((int)threadIdx.x < rn) {
+                const int r = threadIdx.x;
+                t = wc[0][r] + wc[1][r] + wc[2][r] + wc[3][r];
+                a.qcnt[(size_t)b * a.R + rc + r] = t;
+                a.ocnt[(size_t)b * a.R + rc + r] = owc[0][r] + owc[1][r] + owc[2][r] + owc[3][r];
             }
+            const uint32_t ts = wave_sum_u32(t);
+            if (lane_id() == 0) l4[wave_id()] = ts;
+            lds_barrier();
+            csum += (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
+            lds_barrier();
         }
-        lds_barrier();
-        uint32_t t = 0;
-        if ((int)threadIdx.x < a.R) {
-            const int r = threadIdx.x;
-            t = wc[0][r] + wc[1][r] + wc[2][r] + wc[3][r];
-            a.qcnt[(size_t)b * a.R + r] = t;
-            a.ocnt[(size_t)b * a.R + r] = owc[0][r] + owc[1][r] + owc[2][r] + owc[3][r];
-        }
-        const uint32_t ts = wave_sum_u32(t);
-        if (lane_id() == 0) l4[wave_id()] = ts;
-        lds_barrier();
-        csum = (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
     } else {
     // R <= 128: the wave's counts of c > r for every round from a histogram of
     // min(c, R) in LDS -- one LDS atomic per lane and a wave scan instead of one
@@ -2750,6 +2765,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 }
 
 // ------------------------------------------------------------ k_emit_shard
+__device__ __forceinline__ void shard_compact(const TickArgs &a, int bid);
 constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // Phase 2 of a sharded tick.  Every rank computes the global water-filling from
 // the exchanged counts (identical on all ranks), writes the whole next LRU queue,
@@ -2770,7 +2786,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
         // ---- every load in flight at once (clamped indices, no branches)
         const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
-        const int cq = a.xc8[pq];
+        const int cq = xc_get(a, pq);
         const int sq = lq_slot(a, pq);
         const int32_t rawq = a.c_arr[pq];
         int64_t Av[kRCh], oAv[kRCh], pv[kRCh], opv[kRCh];
@@ -2928,8 +2944,13 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         }
         return;
     }
-    // ---- compaction roles as in k_emit2: one wave per tile (a phase-1 k_scan block's
-    // 2048 log entries or 256 slots), four tiles per workgroup
+    shard_compact(a, bid);
+}
+
+// ---- compaction roles of k_emit_shard*, as in k_emit2: one wave per tile (a phase-1
+// k_scan block's 2048 log entries or 256 slots), four tiles per workgroup
+__device__ __forceinline__ void shard_compact(const TickArgs &a, int bid) {
+    const int lane = lane_id(), w = wave_id();
     const int nbf4 = (a.nbf + 3) >> 2;
     const bool frole = bid < a.nbq + nbf4;
     const int t = 4 * (frole ? bid - a.nbq : bid - a.nbq - nbf4) + w;
@@ -2958,6 +2979,169 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     }
 }
 
+
+// Phase 2 of a sharded tick whose round table is wider than k_emit_shard's three
+// 64-round chunks (fill levels of 128 and more: free counts in the hundreds or
+// thousands).  The same water-filling, with the rounds walked in 64-round chunks: a
+// first pass over the totals finds L, S(L) and So(L) (and keeps every chunk's starting
+// S / So in LDS), the emission pass reloads each chunk's block prefixes and segment
+// counts, and rounds L and L + 1 read their rank bases directly.
+constexpr int kWideMaxCh = 64;  // R <= 4096 rows
+__global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
+    prefetch_args(a);
+    const int bid = blockIdx.x;
+    const int lane = lane_id(), w = wave_id();
+    if (bid >= a.nbq) {
+        shard_compact(a, bid);
+        return;
+    }
+    __shared__ int64_t chS[kWideMaxCh], chSo[kWideMaxCh];
+    const int b = bid;
+    const int R = a.R;
+    const int64_t pos = (int64_t)b * kBS + threadIdx.x;
+    const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
+    const int cq = xc_get(a, pq);
+    const int sq = lq_slot(a, pq);
+    const int32_t rawq = a.c_arr[pq];
+    const int64_t O = a.P->O;
+    int64_t cap = a.P->cap_total;
+    const int maxc = a.P->maxc;
+    const int rlim = maxc < R ? maxc : R;
+    if (maxc > R) cap = INT64_MAX;
+    const int64_t N = (a.redist ? O : 0) + a.T;
+    const int64_t N_eff = N < cap ? N : cap;
+    // ---- pass 1 (every wave alike): S(r), So(r) chunk by chunk until S(r + 1) > N_eff
+    int L = 0;
+    int64_t S_L = 0, oSL = 0;
+    {
+        int64_t carry = 0, ocarry = 0;
+        bool found = false;
+        for (int k = 0; 64 * k < rlim; ++k) {
+            const int r = 64 * k + lane;
+            const uint32_t v = r < rlim ? (uint32_t)a.A[r] : 0u;
+            const uint32_t ov = r < rlim ? (uint32_t)a.oA[r] : 0u;
+            if (w == 0 && lane == 0) {
+                chS[k] = carry;
+                chSo[k] = ocarry;
+            }
+            const uint32_t incl = wave_incl_scan_u32(v), oincl = wave_incl_scan_u32(ov);
+            const int64_t S1 = carry + (int64_t)incl;
+            const int nl = __popcll(__ballot(r < rlim && S1 <= N_eff));
+            L += nl;
+            if (nl < 64) {  // S is non-decreasing: the fill level lies in this chunk
+                S_L = carry + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(incl - v), nl);
+                oSL = ocarry + (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)(oincl - ov), nl);
+                found = true;
+                break;
+            }
+            carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+            ocarry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)oincl, 63);
+        }
+        if (!found) {  // every round of the table below the fill level: S(rlim)
+            S_L = carry;
+            oSL = ocarry;
+        }
+    }
+    lds_barrier();
+    int status = 0;
+    if (maxc > R && L >= R - 1) status = 1;  // R <= 64 * kWideMaxCh (the host caps it)
+    if (a.head_local + N_eff > a.log_cap) status = 2;
+    const int64_t p = N_eff - S_L;
+    const int64_t AL = (L < maxc && L < rlim) ? a.A[L] : 0;
+    if (b == 0 && threadIdx.x == 0) {
+        a.hout->O = O;
+        a.hout->O_local = a.P->O_local;
+        a.hout->n_evicted = a.P->n_evicted;
+        a.hout->cap_total = cap;
+        a.hout->maxc = maxc;
+        a.hout->L = L;
+        a.hout->status = status;
+        a.hout->N_eff = status ? 0 : N_eff;
+        a.hout->p = p;
+        a.hout->AL = AL;
+        if (!status && AL == 0) {
+            a.hout->new_qlen = 0;
+            a.hout->n_local = oSL;
+        }
+    }
+    if (status) return;
+    const int c = pos < a.Qlog ? cq : 0;
+    const int s = sq;
+    const int ls = s >= 0 ? own_slot(a, s) : -1;
+    const bool own = c > 0 && ls >= 0;
+    const int oc = own ? c : 0;
+    // rank bases of this wave's segment in A_r (all and own) for round r
+    auto rank_base = [&](int r, int64_t &rb, int64_t &orb) {
+        const int rr = r < R ? r : R - 1;
+        rb = r < rlim ? a.qpre[(size_t)b * R + rr] : 0;
+        orb = r < rlim ? a.opre[(size_t)b * R + rr] : 0;
+        for (int q = 0; q < w; ++q) {
+            rb += r < R ? a.segcnt[(size_t)(4 * b + q) * R + rr] : 0u;
+            orb += r < R ? a.osegcnt[(size_t)(4 * b + q) * R + rr] : 0u;
+        }
+    };
+    int32_t *const lslot = a.log_slot + a.head_local;
+    uint32_t *const lseq = a.lseq_out + a.head_local;
+    const uint32_t hin = (uint32_t)a.head_in;
+    // ---- full rounds r < min(L, max own c of the wave), a 64-round chunk at a time
+    const int owmx = (int)wave_max_u32((uint32_t)oc);
+    const int rfull = L < owmx ? L : owmx;
+    for (int k = 0; 64 * k < rfull; ++k) {
+        const int r = 64 * k + lane;
+        int64_t rb, orb;
+        rank_base(r, rb, orb);
+        const uint32_t v = r < rlim ? (uint32_t)a.A[r] : 0u;
+        const uint32_t ov = r < rlim ? (uint32_t)a.oA[r] : 0u;
+        const int64_t Sr = chS[k] + (int64_t)(wave_incl_scan_u32(v) - v);
+        const int64_t Sor = chSo[k] + (int64_t)(wave_incl_scan_u32(ov) - ov);
+        const int32_t basev = (int32_t)(Sr + rb), obasev = (int32_t)(Sor + orb);
+        const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
+        for (int i = 0; i < r1; ++i) {
+            const int rr = 64 * k + i;
+            const uint64_t m = __ballot(c > rr);
+            const uint64_t om = __ballot(oc > rr);
+            const int base = __builtin_amdgcn_readlane(basev, i);
+            const int obase = __builtin_amdgcn_readlane(obasev, i);
+            if (oc > rr) {
+                const int lp = obase + popc_lt(om);
+                lslot[lp] = s;
+                lseq[lp] = hin + (uint32_t)(base + popc_lt(m));
+            }
+        }
+    }
+    // ---- round L (partial: ranks < p) and round L + 1 (ranks for the next queue)
+    int64_t rbL, orbL, rbL1, orbL1;
+    rank_base(L, rbL, orbL);
+    rank_base(L + 1, rbL1, orbL1);
+    const uint64_t mL = __ballot(c > L);
+    const uint64_t omL = __ballot(oc > L);
+    const int64_t rankL = rbL + popc_lt(mL);
+    const int64_t orankL = orbL + popc_lt(omL);
+    if (oc > L && rankL < p) {
+        const int64_t lp = oSL + orankL;
+        lslot[lp] = s;
+        lseq[lp] = hin + (uint32_t)(S_L + rankL);
+    }
+    const int64_t exL1 = rbL1 + popc_lt(__ballot(c > L + 1));
+    if (c > 0) {
+        int64_t n_q = c < L ? c : L;
+        if (c > L && rankL < p) n_q += 1;
+        if (own) a.free_out[ls].x = rawq - (int32_t)n_q;
+        int64_t np = -1;
+        if (c > L) {
+            if (rankL >= p) np = rankL - p;
+            else if (c > L + 1) np = (AL - p) + exL1;
+            if (rankL == p) {
+                a.hout->new_qlen = (AL - p) + exL1;
+                a.hout->n_local = oSL + orankL;
+            }
+        }
+        if (np >= 0) {
+            a.queue_out[np] = s;
+            if (own) a.free_out[ls].y = 1;
+        }
+    }
+}
 
 // ------------------------------------------------------------ readback
 // Words to (host-mapped) memory: lane j of a pass moves words 4j .. 4j + 3 -- four
@@ -3092,6 +3276,11 @@ void launch_emit2(const TickArgs &a, Stream st) {
     }
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {
+    if (a.R > 64 * kRCh - 64) {  // rounds 0 .. L+1 beyond the three register chunks
+        hipExtLaunchKernelGGL(k_emit_shard_wide, dim3(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4), dim3(kBS), 0, st.s,
+                              st.e0, st.e1, 0, a);
+        return;
+    }
     hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4), dim3(kBS), 0, st.s, st.e0,
                           st.e1, 0, a);
 }

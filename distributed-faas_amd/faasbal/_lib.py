@@ -13,9 +13,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "libfaasbal.so")
 
 FB_EVS_APPLIED, FB_EVS_RECONNECT, FB_EVS_UNKNOWN = 0, 1, 2
-FB_OK, FB_EINVAL, FB_ENOMEM, FB_EHIP, FB_ERANGE, FB_ENOSPC, FB_ESTATE = 0, -1, -2, -3, -4, -5, -6
+FB_OK, FB_EINVAL, FB_ENOMEM, FB_EHIP, FB_ERANGE, FB_ENOSPC, FB_ESTATE, FB_ERERUN = 0, -1, -2, -3, -4, -5, -6, -7
 ERRNAMES = {FB_EINVAL: "FB_EINVAL", FB_ENOMEM: "FB_ENOMEM", FB_EHIP: "FB_EHIP", FB_ERANGE: "FB_ERANGE",
-            FB_ENOSPC: "FB_ENOSPC", FB_ESTATE: "FB_ESTATE"}
+            FB_ENOSPC: "FB_ENOSPC", FB_ESTATE: "FB_ESTATE", FB_ERERUN: "FB_ERERUN"}
 
 # Every symbol include/faasbal.h declares (checked by tests/test_abi.py).
 EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read_state", "fb_tick_launch",

@@ -23,7 +23,9 @@ import numpy as np
 
 from . import _lib
 from .balancer import GpuBalancer, _arr, _p
-from ._lib import FaasbalError
+from ._lib import FB_ERERUN, FaasbalError
+
+MAX_RELAUNCH = 6  # FB_ERERUN: each relaunch at least doubles the round table
 
 
 def shard_range(n_workers, world, rank):
@@ -121,19 +123,33 @@ class ShardedBalancer(GpuBalancer):
         self._xbytes = n.value
         with self.torch.cuda.stream(self.stream):
             if allreduce is None:
+                # issued on self.stream; the explicit wait orders phase 2 after it on that
+                # stream (RCCL) or after its completion (gloo)
                 self.torch.distributed.all_reduce(self.exchange(), async_op=True).wait()
             else:
                 allreduce(self.exchange())
+
+    def _run_phases(self, launch, allreduce):
+        """Phase 1, the exchange, phase 2 and the wait -- again with a wider round table
+        while the tick asks for it (FB_ERERUN: the same tick, relaunched; every rank
+        gets the same answer, so the ranks' collectives stay matched)."""
+        for attempt in range(MAX_RELAUNCH + 1):
+            launch()
+            self._allreduce(allreduce)
+            self.cont()
+            try:
+                return self.wait()
+            except FaasbalError as e:
+                if e.code != FB_ERERUN or attempt == MAX_RELAUNCH:
+                    raise
 
     def purge(self, now, tte, commit=True, allreduce=None):
         """This rank's share of ``purge_workers`` (``task_dispatcher.py:241-249``):
         the exchange and phase 2 run as for a tick, nothing is dispatched; returns
         dict(result, evicted, orphans) of this rank's slots and log shard."""
         self._E = 0
-        self._chk(self.lib.fb_purge_launch(self.h, float(now), float(tte)))
-        self._allreduce(allreduce)
-        self.cont()
-        res = self.wait()
+        res = self._run_phases(lambda: self._chk(self.lib.fb_purge_launch(self.h, float(now), float(tte))),
+                               allreduce)
         out = dict(result=res, evicted=self.evicted(), orphans=self.orphans())
         if commit:
             self.commit()
@@ -142,16 +158,8 @@ class ShardedBalancer(GpuBalancer):
     def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
              commit=True, outputs=True, allreduce=None):
         """One sharded tick; ``allreduce(tensor)`` defaults to torch.distributed.all_reduce (SUM)."""
-        self.launch(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
-        with self.torch.cuda.stream(self.stream):
-            if allreduce is None:
-                # issued on self.stream; the explicit wait orders phase 2 after it on that
-                # stream (RCCL) or after its completion (gloo)
-                self.torch.distributed.all_reduce(self.exchange(), async_op=True).wait()
-            else:
-                allreduce(self.exchange())
-        self.cont()
-        res = self.wait()
+        res = self._run_phases(lambda: self.launch(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending),
+                               allreduce)
         out = dict(result=res)
         if outputs:
             task, slot = self.local_assignments()
@@ -331,7 +339,16 @@ class LocalShardGroup(ShardGroup):
         return [serve_op(b, op, kw) for b in self.bals]
 
     def _collective(self, op, kw):
-        # phase 1 on every rank, then the summed exchange, then phase 2 / outputs / commit
+        # phase 1 on every rank, then the summed exchange, then phase 2 / outputs / commit;
+        # relaunched with a wider round table while the ranks ask for it (FB_ERERUN)
+        for attempt in range(MAX_RELAUNCH + 1):
+            try:
+                return self._collective_once(op, kw)
+            except FaasbalError as e:
+                if e.code != FB_ERERUN or attempt == MAX_RELAUNCH:
+                    raise
+
+    def _collective_once(self, op, kw):
         torch = self.bals[0].torch
         for b in self.bals:
             if op == "tick":
@@ -350,10 +367,19 @@ class LocalShardGroup(ShardGroup):
         for b in self.bals:
             b.exchange().copy_(total)
         torch.cuda.synchronize()
-        outs = []
         for b in self.bals:
             b.cont()
-            res = b.wait()
+        res_all = []
+        err = None
+        for b in self.bals:  # every rank waits (a rerun request reaches them all)
+            try:
+                res_all.append(b.wait())
+            except FaasbalError as e:
+                err = err or e
+        if err is not None:
+            raise err
+        outs = []
+        for b, res in zip(self.bals, res_all):
             if op == "tick":
                 task, slot = b.local_assignments()
                 outs.append(dict(result=res, task=task, slot=slot, orphans=b.orphans(), evicted=b.evicted(),

@@ -28,6 +28,8 @@ extern "C" {
 #define FB_ERANGE (-4)  /* free counts beyond the supported round range       */
 #define FB_ENOSPC (-5)  /* in-flight log full                                 */
 #define FB_ESTATE (-6)  /* call out of order (e.g. wait without launch)       */
+#define FB_ERERUN (-7)  /* sharded: the fill level reached the round table; launch the
+                         * same tick again (a wider table), exchange, continue, wait */
 
 /* Inbound message kinds (task_dispatcher.py:347-387). */
 #define FB_EV_REGISTER 0   /* {"type":"register","data":{"num_processes":n}}   */

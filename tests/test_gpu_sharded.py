@@ -28,22 +28,36 @@ def _group(st, world, log_cap, max_events=4096, purge_mode=1):
     return bals, o
 
 
-def _group_tick(bals, *args):
+def _group_tick(bals, *args, relaunches=None):
     import torch
+    from faasbal import FaasbalError
+    from faasbal._lib import FB_ERERUN
     from faasbal.sharded import merge_outputs
 
-    for b in bals:
-        b.launch(*args)
-    torch.cuda.synchronize()
-    total = bals[0].exchange().clone()
-    for b in bals[1:]:
-        total += b.exchange()  # single contributor per byte: the uint8 sum is exact
-    for b in bals:
-        b.exchange().copy_(total)
-    torch.cuda.synchronize()
-    for b in bals:
-        b.cont()
-    res = [b.wait() for b in bals]
+    for attempt in range(7):
+        for b in bals:
+            b.launch(*args)
+        torch.cuda.synchronize()
+        total = bals[0].exchange().clone()
+        for b in bals[1:]:
+            total += b.exchange()  # single contributor per byte: the uint8 sum is exact
+        for b in bals:
+            b.exchange().copy_(total)
+        torch.cuda.synchronize()
+        for b in bals:
+            b.cont()
+        res, codes = [], set()
+        for b in bals:
+            try:
+                res.append(b.wait())
+            except FaasbalError as e:
+                codes.add(e.code)
+        if not codes:
+            break
+        assert codes == {FB_ERERUN}, codes  # a relaunch is asked of every rank or of none
+        assert not res
+        if relaunches is not None:
+            relaunches.append(attempt)
     for k in ("n_assigned", "n_orphans", "queue_len", "log_head", "fill_level"):
         assert len({r[k] for r in res}) == 1, k
     outs = []
@@ -213,3 +227,38 @@ def test_sharded_wide_free_counts(world):
         assert o.export()["free"].max() > 255 and r["max_free"] == 255  # c travels clamped to a byte
         _cmp(bals, o, a, b, t)
         carried = n + len(b["orphans"]) - len(b["assign"])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_fill_level_beyond_128(world):
+    """Fill levels of hundreds of rounds (600 workers with free counts up to 10 000,
+    200 K tasks per tick): the sharded tick asks for a relaunch (FB_ERERUN) with a wider
+    round table and two-byte exchanged counts, then matches the oracle; no FB_ERANGE."""
+    rng = np.random.default_rng(70 + world)
+    W, now = 600, 1000.0
+    reg = np.ones(W, np.uint8)
+    free = rng.integers(0, 10_001, W).astype(np.int32)
+    hb = now - rng.random(W) * 9.9
+    hb[rng.random(W) < 0.03] = now - 10.5
+    queue = rng.permutation(np.nonzero(free > 0)[0]).astype(np.int32)
+    log = rng.integers(-1, W, 20_000).astype(np.int32)
+    st = dict(reg=reg, free=free, hb=hb, epoch=np.zeros(W, np.uint32), queue=queue, log=log)
+    bals, o = _group(st, world, len(log) + 1_200_000, max_events=512)
+    carried, levels, relaunches = 0, [], []
+    for t in range(4):
+        t_now = now + 0.5 * t
+        E = 200
+        kind = rng.choice([synth.EV_REGISTER, synth.EV_HEARTBEAT, synth.EV_RESULT, synth.EV_RECONNECT], size=E,
+                          p=[0.2, 0.4, 0.3, 0.1]).astype(np.uint8)
+        slot = rng.integers(0, W, E).astype(np.int32)
+        val = rng.integers(0, 10_001, E).astype(np.int32)
+        ts = np.sort(t_now - 0.5 * rng.random(E))
+        n = carried + 200_000
+        args = (t_now, 10.0, kind, slot, val, ts, np.full(E, -1, np.int64), n)
+        a, r = _group_tick(bals, *args, relaunches=relaunches)
+        b = o.tick(*args)
+        levels.append(r["fill_level"])
+        _cmp(bals, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert max(levels) > 128, levels
+    assert relaunches, "the first wide tick must ask for a relaunch"
