@@ -112,10 +112,13 @@ struct fb_ctx {
     uint32_t *post_infl = nullptr;
     int32_t *ev_clr = nullptr;
     uint32_t *ctag = nullptr;
-    unsigned long long *fagg = nullptr, *fticket = nullptr;
-    unsigned long long fticket_n = 0;  // tickets handed out so far (the next launch's base)
     uint32_t lstamp = 0;               // per enqueued launch, reruns included (never 0)
     int f_emit = 1;                    // FAASBAL_F_EMIT=0: fused ticks keep k_scan's log blocks (A/B knob)
+    // f_emit ticks leave their orphans in per-tile segments (orphans[t*2048 + i], i < fcnt[t]);
+    // the dense list is gathered into orph_dense when something reads it
+    bool l_oseg = false, dense_ok = false;
+    int l_nbf = 0;
+    int64_t *orph_dense = nullptr;
     // compact assignments (fb_set_compact): slot and min(c, L + 1) per LRU position
     int32_t *rb_slot = nullptr;
     uint8_t *rb_c = nullptr;
@@ -550,19 +553,6 @@ int enqueue_tick(fb_ctx *c) {
     if (++c->lstamp == 0) c->lstamp = 1;  // every launch (reruns included) stamps its own
     const bool defer = c->infl[0] != nullptr;  // one-GPU heartbeat context
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
-    // fused one-GPU ticks: O from the slot purge's in-flight counts, the orphans flagged
-    // and compacted by k_emit2's log workgroups (k_scan without log blocks)
-    const int nbfe = (int)cdiv(nbf, 4);
-    const size_t bm16 = (size_t)(((W + 63) / 64 + 1) / 2) * 16;
-    a.f_emit = (defer && a.fused && c->f_emit && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
-                bm16 <= (size_t)c->max_lds) ? 1 : 0;
-    if (a.f_emit) {
-        a.nbfe = nbfe;
-        a.fagg = c->fagg;
-        a.fticket = c->fticket;
-        a.fticket0 = c->fticket_n;
-        c->fticket_n += (unsigned long long)nbfe;
-    }
     if (defer) {
         a.infl_in = c->infl[cur];
         a.infl_out = c->infl[nxt];
@@ -580,6 +570,16 @@ int enqueue_tick(fb_ctx *c) {
     a.f_sep = (head > 0 && !c->deque && (c->logscan > 0 || (c->logscan < 0 && W > kLdsBitmapSlots)) &&
                bm_bytes <= (size_t)c->max_lds && !(c->shard && c->phase == 2)) ? 1 : 0;
     if (a.f_sep) a.slots_in_scan = 1;
+    // fused one-GPU ticks: O from the slot purge's in-flight counts, the orphans flagged
+    // and compacted by k_emit2's log workgroups (k_scan without log blocks); not when the
+    // log role was asked to run as k_logscan (FAASBAL_LOGSCAN=1)
+    const int nbfe = (int)cdiv(nbf, 4);
+    const size_t bm16 = (size_t)(((W + 63) / 64 + 1) / 2) * 16;
+    a.f_emit = (defer && a.fused && !a.f_sep && c->f_emit && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
+                bm16 <= (size_t)c->max_lds) ? 1 : 0;
+    c->l_oseg = a.f_emit != 0;
+    c->l_nbf = nbf;
+    c->dense_ok = false;
     const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
     c->l_used_ll = false;
     const bool ll = E > 0 && c->ev_head && c->ev_ll && !c->l_resort;
@@ -1018,7 +1018,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->A_rep, (size_t)64 * kRFused);
     ap.add(&c->P_rep, 64);
     ap.add(&c->log_slot, F);
-    ap.add(&c->orphans, F);
+    ap.add(&c->orphans, (size_t)cdiv(F, kFTile) * kFTile);  // whole tiles: f_emit's per-tile segments
     if (c->deque) {
         for (int i = 0; i < 2; ++i) {
             ap.add(&c->tokcnt[i], W);
@@ -1040,8 +1040,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->post_infl, W);
         ap.add(&c->ev_clr, E);
         ap.add(&c->ctag, F);
-        ap.add(&c->fagg, kFEmitMaxBlocks);
-        ap.add(&c->fticket, 1);
+        ap.add(&c->orph_dense, F);
     }
     if (shard) {
         ap.add(&c->lseq, F);
@@ -1641,8 +1640,6 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             if (rc) return rc;
             continue;
         }
-        if (c->hout->fault)
-            return fail(c, FB_EHIP, "k_emit2: a log workgroup's orphan-count hand-off timed out");
         if (c->hout->status == 0) break;
         if (c->hout->status == 2)
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
@@ -1713,6 +1710,10 @@ int fb_tick_commit(fb_ctx *c) {
         a.head_local = c->l_head_local;
         a.shard = c->shard;
         a.nbo = (int)cdiv(n_orph, kBS);
+        if (c->l_oseg && n_orph > 0) {  // per-tile segments: one block per log tile
+            a.oseg = c->fcnt;
+            a.nbo = c->l_nbf;
+        }
         a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
         a.ev_clr = c->ev_clr;
         const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS);
@@ -1781,6 +1782,31 @@ static int d2h(fb_ctx *c, void *dst, const void *src, size_t bytes) {
     HIPCHK(c, hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
     return FB_OK;
 }
+// Device pointer of the waited tick's dense orphan list: an f_emit tick left per-tile
+// segments, gathered into orph_dense here (once per tick).
+static int64_t *orph_dense_dev(fb_ctx *c) {
+    if (!c->l_oseg) return c->orphans;
+    if (!c->dense_ok) {
+        launch_orph_gather(c->orph_dense, c->orphans, c->fcnt, c->l_nbf, Stream(c->stream));
+        c->dense_ok = true;
+    }
+    return c->orph_dense;
+}
+// n orphans of the waited tick into dst; the whole list of segments goes straight into
+// pinned host memory by the gather kernel
+static int orph_out(fb_ctx *c, int64_t *dst, int64_t n) {
+    if (!n) return FB_OK;
+    if (c->l_oseg && c->d2h_kernel && n == c->last.n_orphans_local) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
+            launch_orph_gather((int64_t *)at.devicePointer, c->orphans, c->fcnt, c->l_nbf, Stream(c->stream));
+            HIPCHK(c, hipGetLastError());
+            return FB_OK;
+        }
+        (void)hipGetLastError();
+    }
+    return d2h(c, dst, orph_dense_dev(c), (size_t)n * 8);
+}
 static int copy_out(fb_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!bytes) return FB_OK;
     if (int rc = d2h(c, dst, src, bytes)) return rc;
@@ -1800,7 +1826,10 @@ int fb_get_orphans(fb_ctx *c, int64_t n, int64_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (n < 0 || n > c->last.n_orphans_local) return fail(c, FB_EINVAL, "orphan count");
-    return copy_out(c, dst, c->orphans, (size_t)n * 8);
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = orph_out(c, dst, n)) return rc;
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
 }
 
 int fb_get_evicted(fb_ctx *c, int32_t n, int32_t *dst) {
@@ -1819,9 +1848,7 @@ int fb_get_outputs(fb_ctx *c, int32_t *assign, int64_t *orphans, int32_t *evicte
     int rc;
     if (assign && c->last.n_assigned && (rc = d2h(c, assign, c->log_slot + c->l_head, (size_t)c->last.n_assigned * 4)))
         return rc;
-    if (orphans && c->last.n_orphans_local &&
-        (rc = d2h(c, orphans, c->orphans, (size_t)c->last.n_orphans_local * 8)))
-        return rc;
+    if (orphans && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
     if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return FB_OK;
@@ -1847,12 +1874,39 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
                                               (long long)n);
     HIPCHK(c, hipSetDevice(c->device));
     int rc;
-    if (slot && n && (rc = d2h(c, slot, c->rb_slot, (size_t)n * 4))) return rc;
-    if (cnt && n && (rc = d2h(c, cnt, c->rb_c, (size_t)n))) return rc;
-    if (orphans && c->last.n_orphans_local &&
-        (rc = d2h(c, orphans, c->orphans, (size_t)c->last.n_orphans_local * 8)))
+    // into pinned memory: the word copies in one kernel (and the orphan segments gathered
+    // straight into their buffer), else one transfer per array
+    CopyMulti m{};
+    auto mapped = [](void *p) -> uint32_t * {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, p) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer)
+            return (uint32_t *)at.devicePointer;
+        (void)hipGetLastError();
+        return nullptr;
+    };
+    auto add = [&](void *dst, const void *src, int64_t bytes) -> bool {
+        uint32_t *d = c->d2h_kernel && (bytes & 3) == 0 ? mapped(dst) : nullptr;
+        if (!d) return false;
+        const int b0 = m.n ? m.blk0[m.n - 1] + (int)std::min<int64_t>(
+                                                       std::max<int64_t>(1, (m.words[m.n - 1] + 4 * kBS - 1) / (4 * kBS)), 512)
+                           : 0;
+        m.dst[m.n] = d;
+        m.src[m.n] = (const uint32_t *)src;
+        m.words[m.n] = bytes / 4;
+        m.blk0[m.n] = b0;
+        m.n++;
+        return true;
+    };
+    // the c bytes travel as whole words when the caller's buffer has room for the padding
+    const int64_t cw = (n + 3) & ~(int64_t)3;
+    if (slot && n && !add(slot, c->rb_slot, n * 4) && (rc = d2h(c, slot, c->rb_slot, (size_t)n * 4))) return rc;
+    if (cnt && n && !(cw <= cap && add(cnt, c->rb_c, cw)) && (rc = d2h(c, cnt, c->rb_c, (size_t)n))) return rc;
+    if (evicted && c->last.n_evicted && !add(evicted, c->evicted, (int64_t)c->last.n_evicted * 4) &&
+        (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4)))
         return rc;
-    if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) return rc;
+    launch_copy_multi(m, Stream(c->stream));
+    HIPCHK(c, hipGetLastError());
+    if (orphans && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return FB_OK;
 }
@@ -1997,7 +2051,7 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     v->registered = c->reg;
     v->queue = c->queue[c->cur];
     v->log_slot = c->log_slot;
-    v->orphans = c->orphans;
+    v->orphans = orph_dense_dev(c);
     v->evicted = c->evicted;
     v->n_workers = c->W;
     v->queue_len = c->Qn;

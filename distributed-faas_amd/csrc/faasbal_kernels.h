@@ -48,10 +48,9 @@ constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 // slot's in-flight entries (ctag[q] == the launch stamp names which); the log itself is
 // cleared only by the commit, so an orphan test of that slot's entries checks ctag
 constexpr uint8_t kRfCleared = 16;
-// k_emit2's log tiles (one-GPU fused ticks): at most this many compaction workgroups
-// (4 tiles of kFTile entries each), so every workgroup's look-back over the earlier
-// ones' orphan counts is one load per thread
-constexpr int kFEmitMaxBlocks = 256;
+// k_emit2's log tiles (one-GPU fused ticks): at most this many log workgroups (4 tiles
+// of kFTile entries each; k_orph_gather sums up to 4 x this many tile counts per block)
+constexpr int kFEmitMaxBlocks = 1024;
 
 // Committed per-slot heartbeat: last_heartbeat, NaN when the slot holds no record
 // (so the log scan's one 8-byte gather per in-flight entry decides liveness
@@ -83,8 +82,6 @@ struct HostOut {
     int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
                         // (deque contexts: new_qlen > token capacity is checked by the host)
     int32_t resort;     // k_ev_apply_ll: a slot got too many messages, rerun through the sort
-    int32_t fault;      // k_emit2 log workgroups: an orphan-count hand-off never arrived (zeroed by k_scan)
-    int32_t pad_;
     int64_t n_local;   // sharded: tasks appended to this rank's log shard
     int64_t O_local;    // sharded: this rank's orphans
 };
@@ -100,6 +97,8 @@ struct CommitArgs {
     int W;
     int slot_base;
     int nbw;            // slot blocks; blocks [nbw, nbw + ceil(n_orph / 256)) clear orphaned log entries
+    const uint32_t *oseg;  // non-null: orphans in per-tile segments (orphans[t*2048 + i], i < oseg[t]),
+                           // blocks [nbw, nbw + nbo) one per tile
     int nbo;            // ... then blocks [nbw + nbo, + ceil(n_clr / 256)) clear the entries the
     int n_clr;          // committed tick's results completed: log_slot[ev_clr[e]] = -1, e < n_clr
     const int32_t *ev_clr;
@@ -218,14 +217,9 @@ struct TickArgs {
     uint32_t lstamp;
     // f_emit (fused one-GPU ticks): the orphan count comes from the slot purge (sum of the
     // dead registrations' in-flight counts into column R + 1), k_scan has no log blocks, and
-    // k_emit2's compaction workgroups flag and compact the orphans themselves: log tiles
-    // tested against the died bitmap in LDS, offsets from the earlier workgroups' counts
-    // ({lstamp, count} granules in fagg), workgroup order from a ticket counter
+    // k_emit2's log workgroups flag the orphans against the died bitmap in LDS and write
+    // them into per-tile segments (orphans[t*2048 + i], i < fcnt[t])
     int f_emit;
-    int nbfe;                      // k_emit2 log workgroups (4 tiles of kFTile entries each)
-    unsigned long long *fagg;      // [kFEmitMaxBlocks] {lstamp, orphans} per log workgroup
-    unsigned long long *fticket;   // monotonic ticket counter (this launch's tickets start at fticket0)
-    unsigned long long fticket0;
     int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;
     double now, tte;
@@ -353,5 +347,17 @@ void launch_emit_shard(const TickArgs &a, Stream st);
 void launch_commit(const CommitArgs &a, int grid, Stream st);
 // dst[i] = src[i], i < n (dst may be host memory mapped for the device: stores cross PCIe)
 void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st);
+// up to 4 word copies in one launch; copy i uses blocks [blk0[i], blk0[i + 1]) (the last:
+// up to the grid's end), the caller sizes blk0
+struct CopyMulti {
+    uint32_t *dst[4];
+    const uint32_t *src[4];
+    int64_t words[4];
+    int blk0[4];
+    int n;
+};
+void launch_copy_multi(const CopyMulti &m, Stream st);
+// the dense orphan list from per-tile segments (dst may be host-mapped memory)
+void launch_orph_gather(int64_t *dst, const int64_t *src, const uint32_t *cnt, int ntile, Stream st);
 
 }  // namespace fb

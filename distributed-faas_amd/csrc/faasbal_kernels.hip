@@ -794,6 +794,13 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
         if (q >= 0) a.log_slot[q] = -1;
         return;
     }
+    if (blk >= a.nbw && a.oseg) {
+        // orphans in per-tile segments (fused one-GPU tick): one block per tile
+        const int t = blk - a.nbw;
+        const uint32_t n = a.oseg[t];
+        for (uint32_t i = threadIdx.x; i < n; i += kBS) a.log_slot[a.orphans[(int64_t)t * kFTile + i]] = -1;
+        return;
+    }
     if (blk >= a.nbw) {
         // the committed tick redistributed these entries: their tasks now run under new
         // sequence numbers, so the old entries leave the in-flight log
@@ -1416,7 +1423,6 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     }
     // ---- Q-role: LRU positions [b*256, +256) of fronts ++ queue ++ backs
     const int b = bid;
-    if (a.f_emit && b == 0 && threadIdx.x == 0) a.hout->fault = 0;  // k_emit2's log hand-offs
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
     int c = 0, oc = 0;
     if (a.shard == 2) {
@@ -2247,18 +2253,14 @@ __device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
 // Log workgroup of a fused one-GPU tick (f_emit): orphan flags and their compaction.
 // The slot purge (k_scan's W role or the apply launch) wrote the died-registration
 // bitmap and already counted O for the fill level, so nothing here is on the queue
-// role's path.  A ticket gives the workgroup its 4 log tiles in start order; its tiles'
-// entries are tested against the bitmap in LDS (coalesced 16-byte log loads, entry
-// t*2048 + 256k + 4*lane + j), its orphan count is published as an {lstamp, count}
-// granule, and its output offset is the sum of the earlier workgroups' granules -- one
-// polled load per thread (at most kFEmitMaxBlocks workgroups), waiting only on
-// workgroups that took earlier tickets and so are already running.  The poll is
-// bounded: a hand-off that never arrives flags hout->fault (the host fails the tick).
-__device__ __forceinline__ void emit_log_tiles(const TickArgs &a, unsigned long long *bm) {
-    __shared__ uint32_t tk;
-    __shared__ uint32_t wtot[kWaves], pre4[kWaves];
+// role's path.  Each wave takes one 2048-entry log tile: coalesced 16-byte log loads
+// (entry t*2048 + 256k + 4*lane + j), the died bits from the bitmap in LDS, and the
+// tile's orphans written in ascending order into the tile's own segment of the orphan
+// buffer (orphans[t*2048 + i], i < ofcnt[t]).  No workgroup waits for another: the
+// dense list -- the segments in tile order -- is gathered when it is read
+// (fb_get_orphans and friends, k_orph_gather) and the commit walks the segments.
+__device__ __forceinline__ void emit_log_tiles(const TickArgs &a, int j, unsigned long long *bm) {
     const int lane = lane_id(), w = wave_id();
-    if (threadIdx.x == 0) tk = (uint32_t)(atomicAdd(a.fticket, 1ull) - a.fticket0);
     // the died bitmap (<= kLdsBitmapSlots bits) into LDS: <= 4 int4 per thread, all in flight
     {
         const int n4 = ((((a.W + 63) >> 6) + 1) >> 1);
@@ -2275,10 +2277,9 @@ __device__ __forceinline__ void emit_log_tiles(const TickArgs &a, unsigned long 
             if (i < n4) reinterpret_cast<uint4 *>(bm)[i] = t4[k];
         }
     }
-    __syncthreads();  // the bitmap and the ticket
-    const int j = (int)tk;
+    const int t = 4 * j + w;
     const int64_t nlog = a.head_in;
-    const int64_t tbase = ((int64_t)4 * j + w) * kFTile;
+    const int64_t tbase = (int64_t)t * kFTile;
     const int64_t last4 = nlog > 0 ? ((nlog - 1) & ~(int64_t)3) : 0;
     int32_t v[8][4];
 #pragma unroll
@@ -2290,7 +2291,9 @@ __device__ __forceinline__ void emit_log_tiles(const TickArgs &a, unsigned long 
         v[k][2] = i + 2 < nlog ? x.z : -1;
         v[k][3] = i + 3 < nlog ? x.w : -1;
     }
-    uint32_t f[8], cnt = 0;
+    lds_barrier();  // the bitmap
+    if (t >= a.nbf) return;
+    int64_t o = tbase;  // this tile's segment
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         uint32_t m = 0;
@@ -2299,49 +2302,16 @@ __device__ __forceinline__ void emit_log_tiles(const TickArgs &a, unsigned long 
             const int sj = v[k][q], sc = sj < 0 ? 0 : sj;
             m |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << q) : 0u;
         }
-        f[k] = drop_completed(a, m, v[k], tbase + k * 256 + 4 * lane);
-        cnt += (uint32_t)__popc(f[k]);
-    }
-    const uint32_t wt = wave_sum_u32(cnt);
-    if (lane == 0) wtot[w] = wt;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t bt = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-        __hip_atomic_store(a.fagg + j, ((unsigned long long)a.lstamp << 32) | bt, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // orphans of the earlier workgroups: thread i polls workgroup i's granule
-    uint32_t pv = 0;
-    if ((int)threadIdx.x < j) {
-        for (uint32_t spin = 0;; ++spin) {
-            const unsigned long long g =
-                __hip_atomic_load(a.fagg + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(g >> 32) == a.lstamp) {
-                pv = (uint32_t)g;
-                break;
-            }
-            if (spin > (1u << 22)) {
-                a.hout->fault = 1;
-                break;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-    }
-    const uint32_t ps = wave_sum_u32(pv);
-    if (lane == 0) pre4[w] = ps;
-    __syncthreads();
-    int64_t off = (int64_t)pre4[0] + pre4[1] + pre4[2] + pre4[3];
-    for (int q = 0; q < w; ++q) off += wtot[q];
-    // entry order within the tile: k, then lane, then j
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const uint32_t c = (uint32_t)__popc(f[k]);
-        const uint32_t incl = wave_incl_scan_u32(c);
-        int64_t o = off + (int64_t)(incl - c);
         const int64_t e0 = tbase + k * 256 + 4 * lane;
-        for (uint32_t m = f[k]; m; m &= m - 1) wt_store(a.orphans + o++, (int64_t)(e0 + __builtin_ctz(m)));
-        off += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        m = drop_completed(a, m, v[k], e0);
+        // entry order within the tile: k, then lane, then j
+        const uint32_t c = (uint32_t)__popc(m);
+        const uint32_t incl = wave_incl_scan_u32(c);
+        int64_t oo = o + (int64_t)(incl - c);
+        for (uint32_t mm = m; mm; mm &= mm - 1) wt_store(a.orphans + oo++, (int64_t)(e0 + __builtin_ctz(mm)));
+        o += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
     }
+    if (lane == 0) a.fcnt[t] = (uint32_t)(o - tbase);
 }
 
 // XCD-aware order of the queue blocks: workgroups are dealt round-robin over the 8
@@ -2718,7 +2688,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const bool frole = bid < cb0 + nbf4;
     if (frole && a.f_emit) {
         extern __shared__ __attribute__((aligned(16))) unsigned long long dynbm[];
-        emit_log_tiles(a, dynbm);
+        emit_log_tiles(a, bid - cb0, dynbm);
         return;
     }
     const int t0 = 4 * (frole ? bid - cb0 : bid - cb0 - nbf4);
@@ -3143,7 +3113,50 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
     }
 }
 
+// ------------------------------------------------------------ orphan segments
+// A fused one-GPU tick leaves its orphans in per-tile segments (emit_log_tiles): the
+// dense list is the segments in tile order.  One workgroup per tile: its offset is the
+// sum of the earlier tiles' counts (<= 4 loads per thread), then the copy.  dst may be
+// host memory mapped for the device (the readback into pinned memory).
+__global__ __launch_bounds__(kBS) void k_orph_gather(int64_t *__restrict__ dst, const int64_t *__restrict__ src,
+                                                    const uint32_t *__restrict__ cnt, int ntile) {
+    __shared__ uint32_t l4[kWaves];
+    const int t = blockIdx.x;
+    uint32_t pre = 0;
+    for (int i = threadIdx.x; i < t; i += kBS) pre += cnt[i];
+    pre = wave_sum_u32(pre);
+    if (lane_id() == 0) l4[wave_id()] = pre;
+    __syncthreads();
+    const int64_t off = (int64_t)l4[0] + l4[1] + l4[2] + l4[3];
+    const uint32_t n = cnt[t];
+    for (uint32_t i = threadIdx.x; i < n; i += kBS) dst[off + i] = src[(int64_t)t * kFTile + i];
+}
+
 // ------------------------------------------------------------ readback
+// Several word copies in one launch (a tick's outputs into pinned host memory with one
+// kernel instead of one per array): copy i takes the blocks [b_i, b_{i+1}) of the grid.
+__global__ __launch_bounds__(kBS) void k_copy_multi(CopyMulti m) {
+    int i = 0;
+    while (i + 1 < m.n && (int)blockIdx.x >= m.blk0[i + 1]) ++i;
+    uint32_t *__restrict__ dst = m.dst[i];
+    const uint32_t *__restrict__ src = m.src[i];
+    const int64_t n = m.words[i];
+    const int64_t nb = (int64_t)(i + 1 < m.n ? m.blk0[i + 1] : (int)gridDim.x) - m.blk0[i];
+    const int64_t stride = nb * kBS * 4;
+    for (int64_t q0 = ((int64_t)(blockIdx.x - m.blk0[i]) * kBS + threadIdx.x) * 4; q0 < n; q0 += stride) {
+        uint32_t v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) v[k] = src[q0 + k < n ? q0 + k : n - 1];
+        if (((reinterpret_cast<uintptr_t>(dst) & 15) == 0) && q0 + 3 < n) {
+            *reinterpret_cast<uint4 *>(dst + q0) = make_uint4(v[0], v[1], v[2], v[3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (q0 + k < n) dst[q0 + k] = v[k];
+        }
+    }
+}
+
 // Words to (host-mapped) memory: lane j of a pass moves words 4j .. 4j + 3 -- four
 // 4-byte loads (any source alignment), one 16-byte store (dst is 16-byte aligned in
 // the callers' pinned buffers; else word stores) -- so a wave store is one 1 KB burst
@@ -3216,6 +3229,15 @@ void launch_ev_link(const EvArgs &a, Stream st) {
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+}
+void launch_copy_multi(const CopyMulti &m, Stream st) {
+    if (m.n <= 0) return;
+    const int last = m.n - 1;
+    const int grid = m.blk0[last] + (int)std::min<int64_t>(std::max<int64_t>(1, (m.words[last] + 4 * kBS - 1) / (4 * kBS)), 512);
+    hipExtLaunchKernelGGL(k_copy_multi, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, m);
+}
+void launch_orph_gather(int64_t *dst, const int64_t *src, const uint32_t *cnt, int ntile, Stream st) {
+    if (ntile > 0) hipExtLaunchKernelGGL(k_orph_gather, dim3(ntile), dim3(kBS), 0, st.s, st.e0, st.e1, 0, dst, src, cnt, ntile);
 }
 void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st) {
     const int grid = (int)std::min<int64_t>(std::max<int64_t>(1, (n + 8 * kBS - 1) / (8 * kBS)), 2048);

@@ -46,9 +46,11 @@ def _cmp_state(g, o, t):
     np.testing.assert_array_equal(sg["queue"], so["queue"], err_msg="tick %d queue" % t)
     np.testing.assert_array_equal(sg["log"], so["log"], err_msg="tick %d log" % t)
     # the per-slot in-flight counts (O of the fused tick) equal the log's live entries
-    live = so["log"][so["log"] >= 0]
-    np.testing.assert_array_equal(g.inflight(), np.bincount(live, minlength=len(so["reg"])).astype(np.uint32),
-                                  err_msg="tick %d in-flight counts" % t)
+    # (kept by contexts whose died bitmap fits the fused tick's LDS: <= 128K slots)
+    if g.max_workers <= 1 << 17:
+        live = so["log"][so["log"] >= 0]
+        np.testing.assert_array_equal(g.inflight(), np.bincount(live, minlength=len(so["reg"])).astype(np.uint32),
+                                      err_msg="tick %d in-flight counts" % t)
 
 
 @pytest.mark.parametrize("path", GOLDEN, ids=[os.path.basename(p)[:-4] for p in GOLDEN])
