@@ -108,7 +108,8 @@ struct fb_ctx {
     // post-message counts, the entry each event's result completes (cleared by the
     // commit: the log is read-only during a tick), the launch stamp of the last launch
     // whose result completed an entry, and k_emit2's log-workgroup hand-off granules
-    uint32_t *infl[2] = {nullptr, nullptr};
+    int32_t *bud = nullptr;       // in flight + free processes of a registered slot (committed)
+    int32_t *bud_next = nullptr;  // touched slots: the budget after the tick (the commit installs it)
     uint32_t *post_infl = nullptr;
     int32_t *ev_clr = nullptr;
     uint32_t *ctag = nullptr;
@@ -551,11 +552,11 @@ int enqueue_tick(fb_ctx *c) {
         c->gdirty[c->gpar] = a.ngrp * a.gstride;
     }
     if (++c->lstamp == 0) c->lstamp = 1;  // every launch (reruns included) stamps its own
-    const bool defer = c->infl[0] != nullptr;  // one-GPU heartbeat context
+    const bool defer = c->bud != nullptr;  // one-GPU heartbeat context
     a.lds_bitmap = W <= kLdsBitmapSlots ? 1 : 0;
     if (defer) {
-        a.infl_in = c->infl[cur];
-        a.infl_out = c->infl[nxt];
+        a.bud = c->bud;
+        a.bud_next = c->bud_next;
         a.post_infl = c->post_infl;
         a.ctag = c->ctag;
         a.lstamp = c->lstamp;
@@ -619,11 +620,10 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_clr = c->ev_clr;
         ea.ctag = c->ctag;
         ea.lstamp = c->lstamp;
-        ea.infl_in = c->infl[cur];
+        ea.bud = c->bud;
         ea.post_infl = c->post_infl;
-        ea.infl_out = c->infl[nxt];
+        ea.bud_next = c->bud_next;
         ea.orph_grp = (a.f_emit && c->purge_apply) ? 1 : 0;
-        if (!defer) ea.infl_in = ea.post_infl = ea.infl_out = nullptr;
         if (c->cm_pending) {  // the previous tick's commit rides in this launch
             ea.cm = c->cm;
             ea.cm_blocks = c->cm_grid;
@@ -736,7 +736,7 @@ int enqueue_tick(fb_ctx *c) {
             a.ev_clr = c->ev_clr;
             a.ctag = c->ctag;
             a.lstamp = c->lstamp;
-            a.infl_in = c->infl[cur];
+            a.bud = c->bud;
             a.post_infl = c->post_infl;
         }
         Timer t(c, "ev_apply");
@@ -1035,8 +1035,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     // in-flight counts only where the fused tick can use them (the died bitmap of the
     // log workgroups fits in LDS); larger tables keep k_logscan and in-place clears
     if (!shard && !c->deque && W <= (size_t)kLdsBitmapSlots) {
-        ap.add(&c->infl[0], W);
-        ap.add(&c->infl[1], W);
+        ap.add(&c->bud, W);
+        ap.add(&c->bud_next, W);
         ap.add(&c->post_infl, W);
         ap.add(&c->ev_clr, E);
         ap.add(&c->ctag, F);
@@ -1259,14 +1259,17 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
             for (int64_t i = 0; i < log_len; ++i)
                 if (lg[i] >= 0 && (!reg[lg[i]] || (uint64_t)i < (uint64_t)epv[lg[i]])) lg[i] = -1;
         HIPCHK(c, hipMemcpy(c->log_slot, lg.data(), (size_t)log_len * 4, hipMemcpyHostToDevice));
-        if (c->infl[0]) {
-            std::vector<uint32_t> cnt(W ? W : 1, 0);
+        if (c->bud) {
+            std::vector<int32_t> bud(W ? W : 1, 0);
             for (int64_t i = 0; i < log_len; ++i)
-                if (lg[i] >= 0) ++cnt[lg[i]];
-            if (W) HIPCHK(c, hipMemcpy(c->infl[0], cnt.data(), W * 4, hipMemcpyHostToDevice));
+                if (lg[i] >= 0) ++bud[lg[i]];
+            for (size_t s = 0; s < W; ++s) bud[s] = reg[s] ? (int32_t)((uint32_t)bud[s] + (uint32_t)free_processes[s]) : 0;
+            if (W) HIPCHK(c, hipMemcpy(c->bud, bud.data(), W * 4, hipMemcpyHostToDevice));
         }
-    } else if (c->infl[0] && W) {
-        HIPCHK(c, hipMemset(c->infl[0], 0, W * 4));
+    } else if (c->bud && W) {
+        std::vector<int32_t> bud(W);
+        for (size_t s = 0; s < W; ++s) bud[s] = reg[s] ? free_processes[s] : 0;
+        HIPCHK(c, hipMemcpy(c->bud, bud.data(), W * 4, hipMemcpyHostToDevice));
     }
     c->W = n_workers;
     c->Qn = queue_len;
@@ -1381,10 +1384,18 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
 int fb_read_inflight(fb_ctx *c, uint32_t *inflight) {
     if (!c || !inflight) return FB_EINVAL;
     if (int rc_ = flush_commit(c)) return rc_;
-    if (!c->infl[0]) return fail(c, FB_ESTATE, "in-flight counts exist on one-GPU heartbeat contexts only");
+    if (!c->bud) return fail(c, FB_ESTATE, "in-flight counts exist on one-GPU heartbeat contexts only");
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
-    if (c->W) HIPCHK(c, hipMemcpy(inflight, c->infl[c->cur], (size_t)c->W * 4, hipMemcpyDeviceToHost));
+    const size_t W = (size_t)c->W;
+    if (!W) return FB_OK;
+    std::vector<int32_t> bud(W);
+    std::vector<int2> fq(W);
+    std::vector<uint8_t> reg(W);
+    HIPCHK(c, hipMemcpy(bud.data(), c->bud, W * 4, hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(fq.data(), c->free_[c->cur], W * sizeof(int2), hipMemcpyDeviceToHost));
+    HIPCHK(c, hipMemcpy(reg.data(), c->reg, W, hipMemcpyDeviceToHost));
+    for (size_t s = 0; s < W; ++s) inflight[s] = reg[s] ? (uint32_t)bud[s] - (uint32_t)fq[s].x : 0u;
     return FB_OK;
 }
 
@@ -1716,6 +1727,8 @@ int fb_tick_commit(fb_ctx *c) {
         }
         a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
         a.ev_clr = c->ev_clr;
+        a.bud = c->bud;
+        a.bud_next = c->bud_next;
         const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS);
         if (c->ev_head && c->ev_ll && !c->commit_now) {
             // deferred: the next launch's k_ev_link runs it (or flush_commit)

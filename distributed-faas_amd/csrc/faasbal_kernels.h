@@ -97,6 +97,8 @@ struct CommitArgs {
     int W;
     int slot_base;
     int nbw;            // slot blocks; blocks [nbw, nbw + ceil(n_orph / 256)) clear orphaned log entries
+    int32_t *bud;              // one-GPU heartbeat: touched slots get bud_next[s] (budget after the tick)
+    const int32_t *bud_next;
     const uint32_t *oseg;  // non-null: orphans in per-tile segments (orphans[t*2048 + i], i < oseg[t]),
                            // blocks [nbw, nbw + nbo) one per tile
     int nbo;            // ... then blocks [nbw + nbo, + ceil(n_clr / 256)) clear the entries the
@@ -125,15 +127,19 @@ struct EvArgs {
     const int32_t *tokcnt_in;          // deque: committed tokens per slot
     // one-GPU heartbeat contexts: the log is read-only during a tick (so a relaunch of the
     // tick sees the same log); a result that completes entry q records q in ev_clr[e] (the
-    // commit clears it) and stamps ctag[q] = lstamp; post_infl[s] = the slot's in-flight
-    // entries after its messages (infl_in minus the distinct entries its results completed)
+    // commit clears it) and stamps ctag[q] = lstamp.  bud[s] = in-flight entries + free
+    // processes of a registered slot (committed): a dispatch moves one unit from free to
+    // in flight, so only messages and deaths change it.  post_infl[s] = the slot's in-flight
+    // entries after its messages (bud - free minus the distinct entries its results
+    // completed); the purge of a touched slot writes its next budget into bud_next[s],
+    // which the commit installs
     int defer_clr;
     int32_t *ev_clr;
     uint32_t *ctag;
     uint32_t lstamp;
-    const uint32_t *infl_in;
+    const int32_t *bud;
     uint32_t *post_infl;
-    uint32_t *infl_out;   // the slot purge's next in-flight count (apply launch)
+    int32_t *bud_next;
     int orph_grp;         // the slot purge adds the orphans of dead registrations to column R + 1
     int32_t *front_rank, *back_rank;   // deque: rank of a new token among its slot's tokens
     int32_t *post_tok, *post_nf;       // deque: tokens per slot after the messages; new front tokens
@@ -207,11 +213,9 @@ struct TickArgs {
     uint32_t *grp_zero;  // the other parity's rows: k_emit2 zeroes zero_words of them for the next launch
     int zero_words;
     int f_sep;        // 1: log role in its own launch (k_logscan, died bitmap in LDS); k_scan W-role writes the bitmap
-    // one-GPU heartbeat contexts: in-flight entries per slot (infl_in committed, infl_out
-    // next: the purge writes the post-message count, 0 for a dead registration; k_emit*
-    // adds the tasks it gives the slot), post_infl / ctag / lstamp as in EvArgs
-    const uint32_t *infl_in;
-    uint32_t *infl_out;
+    // one-GPU heartbeat contexts: bud / post_infl / bud_next / ctag / lstamp as in EvArgs
+    const int32_t *bud;
+    int32_t *bud_next;
     const uint32_t *post_infl;
     const uint32_t *ctag;
     uint32_t lstamp;

@@ -660,7 +660,7 @@ struct SlotRun {
     int32_t fr;
     double hb;
     uint32_t epoch;
-    uint32_t infl0;  // defer_clr: committed in-flight entries of the slot
+    uint32_t infl0;  // defer_clr: in-flight entries of the slot at tick start (bud - free)
     uint32_t ncl;    // defer_clr: distinct entries this tick's results completed
     __device__ __forceinline__ void init(const EvArgs &a, uint32_t s) {
         reg = a.reg[s];
@@ -668,7 +668,8 @@ struct SlotRun {
         fr = fq.x;
         hb = a.hb[s];
         epoch = a.epoch[s];
-        infl0 = a.defer_clr ? a.infl_in[s] : 0u;
+        // a slot without a record has no in-flight entries (its budget is stale)
+        infl0 = (a.defer_clr && reg) ? (uint32_t)(a.bud[s] - fq.x) : 0u;
         ncl = 0;
         inq = fq.y;
         qstat = inq ? kQsKeep : kQsOut;
@@ -821,6 +822,7 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
         a.reg[s] = alive ? 1 : 0;
         a.hb[s] = alive ? pr.hb : __builtin_nan("");
         a.epoch[s] = pr.epoch;
+        if (a.bud) a.bud[s] = a.bud_next[s];
     } else if (stt & kStEvicted) {
         a.reg[s] = 0;
         a.hb[s] = __builtin_nan("");
@@ -882,15 +884,14 @@ __device__ __forceinline__ int32_t log_peek(const EvArgs &a, int64_t seq) {
 // (the entries of a registration that died), and writes the next in-flight count.
 __device__ __forceinline__ uint32_t purge_slot(const EvArgs &a, int s, bool t, int reg0, int reg, double hb,
                                                int32_t fr, int died_flag, bool queued_if_alive, uint32_t infl,
-                                               bool &died, bool &evicted) {
+                                               bool &died, bool &evicted, bool &alive_out) {
     const bool dead = reg && ((a.now - hb) > a.tte);
     const bool alive = reg && !dead;
     died = reg0 && (dead || died_flag);
     evicted = (reg0 || t) && !alive;
     a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
     a.free_out[s] = make_int2(alive ? fr : INT32_MIN, (alive && queued_if_alive) ? 1 : 0);
-    // a new registration after a death starts with no in-flight entries
-    if (a.infl_out) a.infl_out[s] = (alive && !died) ? infl : 0u;
+    alive_out = alive;
     return died ? infl : 0u;
 }
 __device__ __forceinline__ void count_evicted(const EvArgs &a, int tile, uint32_t n) {
@@ -904,9 +905,12 @@ __device__ __forceinline__ void count_orphans(const EvArgs &a, int tile, uint32_
 }
 
 __device__ __forceinline__ void SlotRun::purge(const EvArgs &a, uint32_t s, int reg0) {
-    bool died, evicted;
+    bool died, evicted, alive;
     const uint32_t no = purge_slot(a, (int)s, true, reg0, reg, hb, fr, died_start, qstat != kQsOut, infl0 - ncl,
-                                   died, evicted);
+                                   died, evicted, alive);
+    // the budget the commit installs: a new registration after a death starts with no
+    // in-flight entries (a dead slot's budget is never read)
+    if (a.bud_next) a.bud_next[s] = (int32_t)((alive && !died) ? infl0 - ncl : 0u) + fr;
     if (died && a.dmask) atomicOr(&a.dmask[s >> 6], 1ull << (s & 63));
     if (evicted) count_evicted(a, (int)(s >> 8), 1u);
     count_orphans(a, (int)(s >> 8), no);
@@ -927,8 +931,10 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
             const int reg0 = a.reg[s];
             const double hb0 = a.hb[s];
             const int2 fq0 = a.free_in[s];
-            const uint32_t in0 = a.infl_in ? a.infl_in[s] : 0u;
-            if (!t) no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, in0, died, evicted);
+            const int32_t b0 = a.bud ? a.bud[s] : 0;
+            const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(b0 - fq0.x) : 0u;
+            bool alive;
+            if (!t) no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, in0, died, evicted, alive);
         }
         const uint64_t dm = __ballot(died);
         const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
@@ -1219,8 +1225,8 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
     if (s < a.W) {
         const Cur c = cur_slot(a, s);
         // in-flight entries after the messages (loaded with the record, selected after)
-        const uint32_t i0 = a.infl_out ? a.infl_in[s] : 0u;
-        const uint32_t ip = (a.infl_out && a.E > 0) ? a.post_infl[s] : 0u;
+        const int32_t b0 = a.bud ? a.bud[s] : 0;
+        const uint32_t ip = (a.bud && a.E > 0) ? a.post_infl[s] : 0u;
         const bool dead = is_dead(a, c);
         const bool alive = c.reg && !dead;
         died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
@@ -1230,10 +1236,13 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         // front / back insertion) -- k_emit2 then rewrites only the slots it serves
         const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
         a.free_out[s] = make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
-        if (a.infl_out) {
-            const uint32_t pin = c.t ? ip : i0;
-            a.infl_out[s] = (alive && !died_start) ? pin : 0u;  // a new registration starts empty
+        if (a.bud) {
+            // untouched: the committed free count is c.fr; a slot without a record has none
+            const uint32_t pin = c.t ? ip : (c.reg0 ? (uint32_t)(b0 - c.fr) : 0u);
             no = died_start ? pin : 0u;
+            // a touched slot's budget after the tick (a new registration starts empty);
+            // an untouched one keeps its budget: dispatches move free into in flight
+            if (c.t) a.bud_next[s] = (int32_t)((alive && !died_start) ? pin : 0u) + c.fr;
         }
         if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
             a.tokcnt_out[s] = 0;
@@ -2193,7 +2202,6 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
             }
             // the worker's next {free, queued}: one 8-byte store
             a.free_out[s] = make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0);
-            if (a.infl_out && n_q) atomicAdd(&a.infl_out[s], (uint32_t)n_q);
             if (np >= 0) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
@@ -2671,8 +2679,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // this tick -- the slot role already wrote {free, 1} for every queued one (a
             // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
             if (n_q != 0 || np < 0) wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
-            // the slot's in-flight entries: the purge wrote the count after its messages
-            if (a.infl_out && n_q) atomicAdd(&a.infl_out[s], (uint32_t)n_q);
+
             if (np >= 0) {
                 wt_store(a.queue_out + np, s);
                 wt_store(a.qfree_out + np, raw - (int32_t)n_q);
