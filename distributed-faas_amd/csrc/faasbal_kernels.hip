@@ -2261,14 +2261,29 @@ __device__ __forceinline__ T chunk_pick(const T (&v)[NCH], int k) {
 // Log workgroup of a fused one-GPU tick (f_emit): orphan flags and their compaction.
 // The slot purge (k_scan's W role or the apply launch) wrote the died-registration
 // bitmap and already counted O for the fill level, so nothing here is on the queue
-// role's path.  Each wave takes one 2048-entry log tile: coalesced 16-byte log loads
-// (entry t*2048 + 256k + 4*lane + j), the died bits from the bitmap in LDS, and the
-// tile's orphans written in ascending order into the tile's own segment of the orphan
-// buffer (orphans[t*2048 + i], i < ofcnt[t]).  No workgroup waits for another: the
-// dense list -- the segments in tile order -- is gathered when it is read
-// (fb_get_orphans and friends, k_orph_gather) and the commit walks the segments.
-__device__ __forceinline__ void emit_log_tiles(const TickArgs &a, int j, unsigned long long *bm) {
-    const int lane = lane_id(), w = wave_id();
+// role's path.  One workgroup per 2048-entry log tile (many small workgroups spread the
+// log reads over the CUs beside the queue blocks): two coalesced 16-byte log loads per
+// thread (entry t*2048 + 1024k + 4*tid + j) issued with the bitmap's copy into LDS, the
+// died bits from LDS, and the tile's orphans written in ascending order into the
+// tile's own segment of the orphan buffer (orphans[t*2048 + i], i < fcnt[t]).  No
+// workgroup waits for another: the dense list -- the segments in tile order -- is
+// gathered when it is read (k_orph_gather) and the commit walks the segments.
+__device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned long long *bm) {
+    __shared__ uint32_t l4[kWaves];
+    const int tid = threadIdx.x;
+    const int64_t nlog = a.head_in;
+    const int64_t tbase = (int64_t)t * kFTile;
+    const int64_t last4 = nlog > 0 ? ((nlog - 1) & ~(int64_t)3) : 0;
+    int32_t v[2][4];
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+        const int64_t i = tbase + k * 1024 + 4 * tid;
+        const int4 x = *reinterpret_cast<const int4 *>(a.log_slot + (i < last4 ? i : last4));
+        v[k][0] = i < nlog ? x.x : -1;
+        v[k][1] = i + 1 < nlog ? x.y : -1;
+        v[k][2] = i + 2 < nlog ? x.z : -1;
+        v[k][3] = i + 3 < nlog ? x.w : -1;
+    }
     // the died bitmap (<= kLdsBitmapSlots bits) into LDS: <= 4 int4 per thread, all in flight
     {
         const int n4 = ((((a.W + 63) >> 6) + 1) >> 1);
@@ -2276,50 +2291,34 @@ __device__ __forceinline__ void emit_log_tiles(const TickArgs &a, int j, unsigne
         uint4 t4[4];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + k * kBS;
+            const int i = tid + k * kBS;
             t4[k] = src[i < n4 ? i : n4 - 1];
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int i = threadIdx.x + k * kBS;
+            const int i = tid + k * kBS;
             if (i < n4) reinterpret_cast<uint4 *>(bm)[i] = t4[k];
         }
     }
-    const int t = 4 * j + w;
-    const int64_t nlog = a.head_in;
-    const int64_t tbase = (int64_t)t * kFTile;
-    const int64_t last4 = nlog > 0 ? ((nlog - 1) & ~(int64_t)3) : 0;
-    int32_t v[8][4];
+    lds_barrier();
+    int64_t o = tbase;  // this tile's segment; entry order within the tile: k, then tid, then j
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-        const int64_t i = tbase + k * 256 + 4 * lane;
-        const int4 x = *reinterpret_cast<const int4 *>(a.log_slot + (i < last4 ? i : last4));
-        v[k][0] = i < nlog ? x.x : -1;
-        v[k][1] = i + 1 < nlog ? x.y : -1;
-        v[k][2] = i + 2 < nlog ? x.z : -1;
-        v[k][3] = i + 3 < nlog ? x.w : -1;
-    }
-    lds_barrier();  // the bitmap
-    if (t >= a.nbf) return;
-    int64_t o = tbase;  // this tile's segment
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k < 2; ++k) {
         uint32_t m = 0;
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
             const int sj = v[k][q], sc = sj < 0 ? 0 : sj;
             m |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << q) : 0u;
         }
-        const int64_t e0 = tbase + k * 256 + 4 * lane;
+        const int64_t e0 = tbase + k * 1024 + 4 * tid;
         m = drop_completed(a, m, v[k], e0);
-        // entry order within the tile: k, then lane, then j
-        const uint32_t c = (uint32_t)__popc(m);
-        const uint32_t incl = wave_incl_scan_u32(c);
-        int64_t oo = o + (int64_t)(incl - c);
+        uint32_t tot;
+        const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(m), l4, tot);
+        int64_t oo = o + ex;
         for (uint32_t mm = m; mm; mm &= mm - 1) wt_store(a.orphans + oo++, (int64_t)(e0 + __builtin_ctz(mm)));
-        o += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        o += tot;
     }
-    if (lane == 0) a.fcnt[t] = (uint32_t)(o - tbase);
+    if (tid == 0) a.fcnt[t] = (uint32_t)(o - tbase);
 }
 
 // XCD-aware order of the queue blocks: workgroups are dealt round-robin over the 8
@@ -2355,7 +2354,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     // the other parity's group rows, for the next launch's k_scan atomics
     for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
     // grid: queue blocks then compaction blocks, or (a.cfirst) compaction first
-    const int nbf4 = (a.nbf + 3) >> 2, nbw4 = (a.nbw + 3) >> 2;
+    // log workgroups: 4 tiles each (f_emit: one tile each), then the slot tiles 4 per workgroup
+    const int nbf4 = a.f_emit ? a.nbf : (a.nbf + 3) >> 2, nbw4 = (a.nbw + 3) >> 2;
     const int qb0 = a.cfirst ? nbf4 + nbw4 : 0;  // first queue block
     const int cb0 = a.cfirst ? 0 : a.nbq;        // first compaction block
     if (bid >= qb0 && bid < qb0 + a.nbq) {
@@ -2692,12 +2692,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     // ---- compaction roles: one wave per tile (a k_scan block's 2048 log entries or
     // 256 slots), four tiles per workgroup -- a quarter of the blocks of one
     // thread per flag byte / slot, so they do not queue behind the queue role
-    const bool frole = bid < cb0 + nbf4;
-    if (frole && a.f_emit) {
+    if (a.f_emit && bid >= cb0 && bid < cb0 + a.nbf) {  // f_emit: one log workgroup per tile
         extern __shared__ __attribute__((aligned(16))) unsigned long long dynbm[];
-        emit_log_tiles(a, bid - cb0, dynbm);
+        emit_log_tile(a, bid - cb0, dynbm);
         return;
     }
+    const bool frole = !a.f_emit && bid < cb0 + nbf4;
     const int t0 = 4 * (frole ? bid - cb0 : bid - cb0 - nbf4);
     const int t = t0 + w;
     const int ntile = frole ? a.nbf : a.nbw;
@@ -3285,7 +3285,7 @@ void launch_emit(const TickArgs &a, Stream st) {
 }
 template <bool PLAN, int NCH>
 static void launch_emit2_t(const TickArgs &a, Stream st) {
-    const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
+    const dim3 g(a.nbq + (a.f_emit ? a.nbf : (a.nbf + 3) / 4) + (a.nbw + 3) / 4);
     // f_emit: the log workgroups stage the died bitmap in LDS (rounded to whole int4)
     const size_t lds = a.f_emit ? (size_t)(((a.W + 63) / 64 + 1) / 2) * 16 : 0;
     switch (tick_mode(a)) {
