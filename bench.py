@@ -31,14 +31,17 @@ def tick_bytes(W, Q, F, O, N, E=0):
     return 16 * W + 8 * W + 4 * (N - O) + 4 * F + 8 * O + 17 * E
 
 
-def emit_bytes(W, Q, F, O, N, Qn_out, n_evicted):
+def emit_bytes(W, Q, F, O, N, Qn_out, n_evicted, log_in_emit=False):
     """Algorithmic bytes of one k_emit launch.  Queue role, per LRU
     position: its c, heartbeat and slot (4+8+4 B read), next free count and
     queued flag of its worker (4+1 B written); per task its slot (4 B); per
     next-queue entry slot, free count and heartbeat (4+4+8 B).  Log role: the
-    orphan flags (1 bit per in-flight entry) and the orphan ids (8 B each).
-    Slot role: the slot status byte and the evicted ids (4 B each)."""
-    return 4 * N + 21 * Q + 16 * Qn_out + F // 8 + 8 * O + W + 4 * n_evicted
+    orphan flags (1 bit per in-flight entry) and the orphan ids (8 B each) --
+    or, when the emit flags the orphans itself (fused one-GPU ticks), every
+    in-flight entry's slot (4 B) and the died bitmap (W/8 B) once.  Slot role:
+    the slot status byte and the evicted ids (4 B each)."""
+    log = 4 * F + W // 8 if log_in_emit else F // 8
+    return 4 * N + 21 * Q + 16 * Qn_out + log + 8 * O + W + 4 * n_evicted
 
 
 def scan_bytes(W, Q, F, logscan=False):
@@ -516,18 +519,23 @@ def main():
         kt_x_bytes = xb.numel()
 
     kern = {k: (ms / n, n) for k, (ms, n) in kt.items()}
+    # fused one-GPU heartbeat ticks (scan + emit only, W <= 128K slots): the emit's log
+    # workgroups read the in-flight log and flag the orphans, k_scan has no log role
+    log_in_emit = (world == 1 and not deque and set(kern) == {"scan", "emit"} and W <= 1 << 17
+                   and os.environ.get("FAASBAL_F_EMIT", "1") != "0")
     dom = max((k for k in kern if k != "exchange_allreduce"), key=lambda k: kern[k][0])
     dom_ms = kern[dom][0]
     tick_dev_ms = sum(v[0] for k, v in kern.items() if k != "exchange_allreduce")
     if dom == "emit" and deque:
         dom_bytes = emit_deque_bytes(Q, n_assigned, int(res["queue_len"]))
     elif dom == "emit" and world == 1:
-        dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]), int(res["n_evicted"]))
+        dom_bytes = emit_bytes(W, Q, F, O, n_assigned, int(res["queue_len"]), int(res["n_evicted"]),
+                               log_in_emit=log_in_emit)
     elif dom == "emit":
         dom_bytes = emit_shard_bytes(Q, Q // world, F // world, int(res["n_orphans_local"]), int(res["n_local"]),
                                      int(res["queue_len"]))
     elif dom == "scan" and world == 1:
-        dom_bytes = scan_bytes(W, Q, F, logscan="logscan" in kern)
+        dom_bytes = scan_bytes(W, Q, F, logscan="logscan" in kern or log_in_emit)
     elif dom == "logscan":
         dom_bytes = logscan_bytes(W, F)
     else:

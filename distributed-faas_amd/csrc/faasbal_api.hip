@@ -127,6 +127,27 @@ struct fb_ctx {
     HostPool *xpool = nullptr;         // fb_expand_compact's workers (created on first use)
     int32_t *trash = nullptr;  // kTrashRows x kBS words written by inactive lanes (never read)
     int64_t Qn = 0, head = 0;
+    // window ticks (one-GPU heartbeat contexts): the committed queue is
+    // [qoff, qoff + Qn) of queue[qcur] / qfree[qcur] / qhb[qcur] (qcap entries each; qfree
+    // kTomb marks a position whose slot left), pos_of[qcur][s] the position of a queued slot
+    int qcur = 0;
+    int64_t qoff = 0, qcap = 0, Qtrue = 0;  // Qtrue: the LRU queue's length (tombstones excluded)
+    bool win_cap = false;      // the context can run window ticks (buffers allocated)
+    int win = -1;              // fb_set_window / FAASBAL_WINDOW: -1 auto (large tables), 0 off, 1 on
+    bool l_win = false;        // the last launch is a window tick
+    int l_nchW = 0;            // ... and the window chunks it scans
+    int64_t l_qoff = 0;
+    int32_t *pos_of[2] = {nullptr, nullptr};
+    int2 *wnpos = nullptr;
+    int4 *wagg = nullptr;
+    uint32_t *lpart = nullptr, *wpart = nullptr;
+    int64_t win_slack = 8192;  // window positions scanned beyond the tasks' estimate (grows on a miss)
+    int64_t last_O = 0;
+    int last_L = -1;
+    int64_t win_ticks = 0, win_fallbacks = 0;
+    bool evict_ok = false;     // the waited window tick's dense evicted list is built
+    bool win_owned = false;    // window buffers allocated by fb_set_window (one allocation)
+    void *win_mem = nullptr;
     uint32_t tick = 1;
     // per-tick sparse post-message records
     uint32_t *touched = nullptr;
@@ -461,6 +482,112 @@ int choose_R(int32_t maxc) {
     return R;
 }
 
+// The committed window [qoff, qoff + Qn) without its tombstones: slots, free counts and
+// (h non-null) heartbeats on the host.  The stream must be idle.
+int win_read(fb_ctx *c, std::vector<int32_t> &q, std::vector<int32_t> &f, std::vector<double> *h, int64_t &n) {
+    const size_t Qn = (size_t)c->Qn;
+    std::vector<int32_t> q0(Qn), f0(Qn);
+    std::vector<double> h0(h ? Qn : 0);
+    if (Qn) {
+        HIPCHK(c, hipMemcpy(q0.data(), c->queue[c->qcur] + c->qoff, Qn * 4, hipMemcpyDeviceToHost));
+        HIPCHK(c, hipMemcpy(f0.data(), c->qfree[c->qcur] + c->qoff, Qn * 4, hipMemcpyDeviceToHost));
+        if (h) HIPCHK(c, hipMemcpy(h0.data(), c->qhb[c->qcur] + c->qoff, Qn * 8, hipMemcpyDeviceToHost));
+    }
+    q.clear();
+    f.clear();
+    if (h) h->clear();
+    for (size_t i = 0; i < Qn; ++i)
+        if (f0[i] != kTomb) {
+            q.push_back(q0[i]);
+            f.push_back(f0[i]);
+            if (h) h->push_back(h0[i]);
+        }
+    n = (int64_t)q.size();
+    if (n != c->Qtrue) return fail(c, FB_EHIP, "window holds %lld live entries, the queue %lld", (long long)n, (long long)c->Qtrue);
+    return FB_OK;
+}
+
+// Rewrite the committed window densely from position 0 of the other buffers (the state a
+// general tick leaves): for readers of the device view.
+int win_normalize(fb_ctx *c) {
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    std::vector<int32_t> q, f;
+    std::vector<double> h;
+    int64_t n = 0;
+    if (int rc = win_read(c, q, f, &h, n)) return rc;
+    const int o = c->qcur ^ 1;
+    if (n) {
+        HIPCHK(c, hipMemcpy(c->queue[o], q.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->qfree[o], f.data(), (size_t)n * 4, hipMemcpyHostToDevice));
+        HIPCHK(c, hipMemcpy(c->qhb[o], h.data(), (size_t)n * 8, hipMemcpyHostToDevice));
+    }
+    if (c->W) {
+        std::vector<int32_t> pos((size_t)c->W, 0);
+        for (int64_t i = 0; i < n; ++i) pos[q[i]] = (int32_t)i;
+        HIPCHK(c, hipMemcpy(c->pos_of[o], pos.data(), (size_t)c->W * 4, hipMemcpyHostToDevice));
+    }
+    c->qcur = o;
+    c->qoff = 0;
+    c->Qn = n;
+    return FB_OK;
+}
+
+// Window buffers for a context created without them (fb_set_window): one allocation,
+// the committed queue copied over.
+int win_alloc(fb_ctx *c) {
+    if (c->win_cap) return FB_OK;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    const size_t W = (size_t)c->W_cap, E = (size_t)c->E_cap, Wq = (size_t)c->Wq_cap;
+    const size_t qcap = 2 * Wq + 2 * E + 4096;
+    auto r256 = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    const size_t bytes = 2 * (r256(qcap * 4) * 2 + r256(qcap * 8) + r256(W * 4)) + r256(W * 8) + r256(kWinMaxCh * 16) +
+                         r256(1024 * 4) + r256(64 * 32 * 4);
+    void *m = nullptr;
+    hipError_t e = hipMalloc(&m, bytes);
+    if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(window buffers %zu B) failed: %s", bytes, hipGetErrorString(e));
+    HIPCHK(c, hipMemset(m, 0, bytes));
+    char *p = (char *)m;
+    auto take = [&](size_t b) { char *r = p; p += r256(b); return r; };
+    int32_t *nq[2], *nf[2];
+    double *nh[2];
+    for (int i = 0; i < 2; ++i) {
+        nq[i] = (int32_t *)take(qcap * 4);
+        nf[i] = (int32_t *)take(qcap * 4);
+        nh[i] = (double *)take(qcap * 8);
+        c->pos_of[i] = (int32_t *)take(W * 4);
+    }
+    c->wnpos = (int2 *)take(W * 8);
+    c->wagg = (int4 *)take(kWinMaxCh * 16);
+    c->lpart = (uint32_t *)take(1024 * 4);
+    c->wpart = (uint32_t *)take(64 * 32 * 4);
+    const int k = c->qcur;
+    if (c->Qn) {
+        HIPCHK(c, hipMemcpy(nq[0], c->queue[k], (size_t)c->Qn * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipMemcpy(nf[0], c->qfree[k], (size_t)c->Qn * 4, hipMemcpyDeviceToDevice));
+        HIPCHK(c, hipMemcpy(nh[0], c->qhb[k], (size_t)c->Qn * 8, hipMemcpyDeviceToDevice));
+    }
+    for (int i = 0; i < 2; ++i) {
+        c->queue[i] = nq[i];
+        c->qfree[i] = nf[i];
+        c->qhb[i] = nh[i];
+    }
+    c->qcur = 0;
+    c->qoff = 0;
+    c->qcap = (int64_t)qcap;
+    c->win_mem = m;
+    c->win_owned = true;
+    c->win_cap = true;
+    if (c->W && c->Qn) {
+        std::vector<int32_t> q((size_t)c->Qn), pos((size_t)c->W, 0);
+        HIPCHK(c, hipMemcpy(q.data(), c->queue[0], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
+        for (int64_t i = 0; i < c->Qn; ++i) pos[q[i]] = (int32_t)i;
+        HIPCHK(c, hipMemcpy(c->pos_of[0], pos.data(), (size_t)c->W * 4, hipMemcpyHostToDevice));
+    }
+    return FB_OK;
+}
+
 // The deferred commit of the last tick as its own launch (when no k_ev_link takes it).
 int flush_commit(fb_ctx *c) {
     if (!c->cm_pending) return FB_OK;
@@ -470,6 +597,32 @@ int flush_commit(fb_ctx *c) {
     launch_commit(c->cm, c->cm_grid, t.st());
     HIPCHK(c, hipGetLastError());
     return FB_OK;
+}
+
+// Whether the tick about to launch runs as a window tick, and how much of
+// the window it scans: the tasks (T plus about the last tick's orphans), the positions
+// between them that are no longer live, a slack that grows whenever a window tick missed
+// its first unserved element.  Only level-0 ticks qualify (the last tick was one), with
+// messages (the purge rides in k_ev_apply_ll's launch), on the linked-list path.
+bool win_plan(fb_ctx *c) {
+    const int mode = c->win;
+    if (!c->win_cap || mode == 0 || c->l_E <= 0 || !c->ev_head || !c->ev_ll || !c->purge_apply || c->compact ||
+        c->l_purge_only || c->deque || c->shard)
+        return false;
+    if (mode < 0 && c->last_L != 0) return false;  // auto: after a level-0 tick
+    if (mode > 0 && c->last_L > 0) return false;
+    const int64_t want = (c->l_T + 2 * c->last_O + 256) * 5 / 4 + c->win_slack;
+    const int64_t scan = std::min<int64_t>(c->Qn, want);
+    if (mode < 0 && scan * 2 > c->Qn) return false;  // auto: only when most of the queue stays put
+    const int nchW = (int)cdiv(scan, kWinCh);
+    if ((size_t)((c->W + 63) / 64 + 2) * 8 > (size_t)c->max_lds) return false;  // k_logscan's bitmap in LDS
+    const int nchB = (int)cdiv(c->l_E, kWinCh);
+    if (2 * nchB + nchW > kWinMaxCh) return false;
+    // room for the appends (backs, served workers with c > 1) behind the window
+    // (an underestimate only costs a rerun: k_emit_win flags a store past the buffer)
+    if (c->qoff + c->Qn + (int64_t)c->l_E + c->l_T + c->last_O + 1024 > c->qcap) return false;
+    c->l_nchW = nchW;
+    return true;
 }
 
 // Enqueue every kernel of the tick described by c->l_* (events already on device).
@@ -530,7 +683,7 @@ int enqueue_tick(fb_ctx *c) {
     a.cfirst = c->emit_cfirst;
     // large tables for k_emit2: group rows too, scanned by k_plan2 (FAASBAL_GPLAN=0: k_plan)
     const bool gplan = !a.fused && a.segw && !c->shard && c->gplan;
-    if (a.fused || gplan) {
+    if ((a.fused || gplan) && !c->l_win) {  // (a window tick uses no group rows)
         // group rows: fused, about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads
         // both); k_plan2, the smallest groups that make at most 64 rows (one workgroup each)
         int gs = 0;
@@ -577,9 +730,10 @@ int enqueue_tick(fb_ctx *c) {
     const int nbfe = (int)cdiv(nbf, 4);
     const size_t bm16 = (size_t)(((W + 63) / 64 + 1) / 2) * 16;
     a.f_emit = (defer && a.fused && !a.f_sep && c->f_emit && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
-                bm16 <= (size_t)c->max_lds) ? 1 : 0;
-    c->l_oseg = a.f_emit != 0;
+                bm16 <= (size_t)c->max_lds && !c->l_win) ? 1 : 0;
+    c->l_oseg = a.f_emit != 0 || c->l_win;
     c->l_nbf = nbf;
+    c->evict_ok = false;
     c->dense_ok = false;
     const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
     c->l_used_ll = false;
@@ -635,7 +789,8 @@ int enqueue_tick(fb_ctx *c) {
         ea.now = c->l_now;
         ea.st = c->st;
         ea.free_out = c->free_[nxt];
-        ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep || a.f_emit)) ? c->dmask : nullptr;
+        ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep || a.f_emit || c->l_win)) ? c->dmask : nullptr;
+        ea.wpart = c->l_win ? c->wpart : nullptr;
         ea.wcnt = c->wcnt;
         ea.grp = a.grp_on ? a.grp : nullptr;
         ea.ngrp = a.ngrp;
@@ -755,11 +910,13 @@ int enqueue_tick(fb_ctx *c) {
     a.reg = c->reg;
     a.hb = c->hb;
     a.free_in = c->free_[cur];
-    a.queue_in = c->queue[cur];
+    // the committed queue: the window [qoff, qoff + Qn) of the current queue buffers
+    const int qc = c->qcur, qn = c->qcur ^ 1;
+    a.queue_in = c->queue[qc] + c->qoff;
     a.qaos = (!c->shard && c->qaos) ? 1 : 0;
     a.cq_direct = (c->cq_direct && E == 0 && a.qaos && a.segw && !c->deque) ? 1 : 0;
-    a.qfree_in = c->qfree[cur];
-    a.qhb_in = c->qhb[cur];
+    a.qfree_in = c->qfree[qc] ? c->qfree[qc] + c->qoff : nullptr;
+    a.qhb_in = c->qhb[qc] ? c->qhb[qc] + c->qoff : nullptr;
     a.touched = c->touched;
     a.tbits = c->tbits;
     a.post = c->post;
@@ -798,9 +955,11 @@ int enqueue_tick(fb_ctx *c) {
     a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !c->no_arena32) ? 1 : 0;
     a.log_slot = c->log_slot;
     a.free_out = c->free_[nxt];
-    a.queue_out = c->queue[nxt];
-    a.qfree_out = c->qfree[nxt];
-    a.qhb_out = c->qhb[nxt];
+    a.queue_out = c->queue[qn];
+    a.qfree_out = c->qfree[qn];
+    a.qhb_out = c->qhb[qn];
+    // a general tick of a window context writes where each slot of its next queue sits
+    if (c->win_cap && !c->l_win) a.pos_out = c->pos_of[qn];
     a.c_hb = c->c_hb;
     a.orphans = c->orphans;
     a.evicted = c->evicted;
@@ -837,6 +996,43 @@ int enqueue_tick(fb_ctx *c) {
         a.dbg = c->dbg;
     }
 #endif
+    if (c->l_win) {
+        // window tick (E > 0, purge in the apply launch): k_logscan's count workgroups count
+        // the chunks of [backs][fronts][window prefix] while its log workgroups write the
+        // orphans into per-tile segments; k_emit_win serves, appends and reports the window
+        a.win = 1;
+        a.wseg = 1;
+        a.nbf = nbf;
+        a.wq_off = c->qoff;
+        a.wq_tail = c->qoff + Qn;
+        a.wq_cap = c->qcap;
+        a.q_cap = c->Wq_cap;  // the next window (tombstones included) must fit the general path
+        a.wq_buf = c->queue[qc];
+        a.wqf_buf = c->qfree[qc];
+        a.wqh_buf = c->qhb[qc];
+        a.nchB = (int)cdiv(E, kWinCh);
+        a.nchF = a.nchB;
+        a.nchW = c->l_nchW;
+        a.wagg = c->wagg;
+        a.wpart = c->wpart;
+        a.wnpos = c->wnpos;
+        a.lstamp = c->lstamp;
+        const int nch = a.nchB + a.nchF + a.nchW;
+        a.ls_cnt_blocks = (int)cdiv(nch, kLsBS / 64);
+        a.ls_log_blocks = head > 0 ? std::max(1, std::min(c->ncu - a.ls_cnt_blocks, (int)cdiv(nbf, kLsBS / 64))) : 0;
+        a.lpart = c->lpart;
+        a.n_lpart = a.ls_log_blocks;
+        {
+            Timer t(c, "logscan");
+            launch_logscan(a, a.ls_cnt_blocks + a.ls_log_blocks, t.st());
+        }
+        {
+            Timer t(c, "emit");
+            launch_emit_win(a, nch, t.st());
+        }
+        HIPCHK(c, hipGetLastError());
+        return FB_OK;
+    }
     if (a.shard == 1) {
         // phase 1: own slots' purge, orphan flags and free counts into the exchange buffer
         if (!a.slots_in_scan) {
@@ -944,14 +1140,28 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     const size_t W = (size_t)max_workers, E = (size_t)c->E_cap, F = (size_t)max_log;
     const size_t Wq = (size_t)c->Wq_cap;  // queue entries are global slots
     const size_t Qlog = Wq + 2 * E;
+    // window-capable contexts (one GPU, heartbeat loop): each queue buffer holds a window
+    // that slides right by the served prefix and grows at its tail (<= 2 E + tasks per tick)
+    // (large tables, or FAASBAL_WINDOW=1; fb_set_window allocates them later for others)
+    const char *wenv = getenv("FAASBAL_WINDOW");
+    c->win_cap = !shard && !c->deque && (wenv ? atoi(wenv) > 0 : W > (size_t)kLdsBitmapSlots);
+    c->qcap = c->win_cap ? (int64_t)(2 * Wq + 2 * E + 4096) : (int64_t)Wq;
+    const size_t Wqb = (size_t)c->qcap;
     ArenaPlan ap;
     for (int i = 0; i < 2; ++i) {
         ap.add(&c->free_[i], W);
-        ap.add(&c->queue[i], Wq);
+        ap.add(&c->queue[i], Wqb);
         if (!shard) {
-            ap.add(&c->qfree[i], Wq);
-            ap.add(&c->qhb[i], Wq);
+            ap.add(&c->qfree[i], Wqb);
+            ap.add(&c->qhb[i], Wqb);
         }
+        if (c->win_cap) ap.add(&c->pos_of[i], W);
+    }
+    if (c->win_cap) {
+        ap.add(&c->wnpos, W);
+        ap.add(&c->wagg, (size_t)kWinMaxCh);
+        ap.add(&c->lpart, (size_t)1024);
+        ap.add(&c->wpart, (size_t)64 * 32);
     }
     ap.add(&c->reg, W);
     ap.add(&c->hb, W);
@@ -1072,6 +1282,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_PURGE_APPLY")) c->purge_apply = atoi(getenv("FAASBAL_PURGE_APPLY"));
     if (!rc && getenv("FAASBAL_CQ_DIRECT")) c->cq_direct = atoi(getenv("FAASBAL_CQ_DIRECT"));
     if (!rc && getenv("FAASBAL_F_EMIT")) c->f_emit = atoi(getenv("FAASBAL_F_EMIT"));
+    if (!rc && getenv("FAASBAL_WINDOW")) c->win = atoi(getenv("FAASBAL_WINDOW"));
     if (!rc) {
         c->scan_ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
         c->post_eager = getenv_int("FAASBAL_POST_EAGER");
@@ -1157,6 +1368,7 @@ int fb_destroy(fb_ctx *c) {
         hipFree(c->opre);
     }
     if (c->oA_owned) hipFree(c->oA);
+    if (c->win_owned) hipFree(c->win_mem);
     if (c->dbg) hipFree(c->dbg);
     if (c->arena) hipFree(c->arena);
     if (c->hout) hipHostFree(c->hout);
@@ -1222,6 +1434,14 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
+    c->qcur = 0;
+    c->qoff = 0;
+    if (c->win_cap && W) {
+        // a queued slot's position (others: never read)
+        std::vector<int32_t> pos(W, 0);
+        for (int64_t i = 0; i < queue_len; ++i) pos[queue[i]] = (int32_t)i;
+        HIPCHK(c, hipMemcpy(c->pos_of[0], pos.data(), W * 4, hipMemcpyHostToDevice));
+    }
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
         std::vector<int2> fq(W);
@@ -1273,9 +1493,12 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
     }
     c->W = n_workers;
     c->Qn = queue_len;
+    c->Qtrue = queue_len;
     c->head = log_len;
     c->tick += 1;
     c->maxc_hint = maxc;
+    c->last_L = -1;
+    c->last_O = 0;
     c->launched = c->waited = false;
     return FB_OK;
 }
@@ -1297,8 +1520,17 @@ int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, doubl
         if (last_heartbeat) HIPCHK(c, hipMemcpy(last_heartbeat, c->hb, W * sizeof(double), hipMemcpyDeviceToHost));
         if (epoch) HIPCHK(c, hipMemcpy(epoch, c->epoch, W * sizeof(uint32_t), hipMemcpyDeviceToHost));
     }
-    if (queue && c->Qn) HIPCHK(c, hipMemcpy(queue, c->queue[c->cur], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
-    if (queue_len) *queue_len = c->Qn;
+    if (c->win_cap) {
+        // the window without its tombstones
+        std::vector<int32_t> q, f;
+        int64_t n = 0;
+        if (int rc = win_read(c, q, f, nullptr, n)) return rc;
+        if (queue && n) memcpy(queue, q.data(), (size_t)n * 4);
+        if (queue_len) *queue_len = n;
+    } else {
+        if (queue && c->Qn) HIPCHK(c, hipMemcpy(queue, c->queue[c->qcur], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
+        if (queue_len) *queue_len = c->Qn;
+    }
     const int64_t nlog = c->shard ? c->head_local : c->head;
     if (log_slot && nlog) HIPCHK(c, hipMemcpy(log_slot, c->log_slot, (size_t)nlog * 4, hipMemcpyDeviceToHost));
     if (log_len) *log_len = nlog;
@@ -1351,6 +1583,16 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     c->cur = 0;
+    c->qcur = 0;
+    c->qoff = 0;
+    c->qcur = 0;
+    c->qoff = 0;
+    if (c->win_cap && W) {
+        // a queued slot's position (others: never read)
+        std::vector<int32_t> pos(W, 0);
+        for (int64_t i = 0; i < queue_len; ++i) pos[queue[i]] = (int32_t)i;
+        HIPCHK(c, hipMemcpy(c->pos_of[0], pos.data(), W * 4, hipMemcpyHostToDevice));
+    }
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
         std::vector<int2> fq(W);
@@ -1591,6 +1833,7 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->l_head = c->head;
     c->l_head_local = c->head_local;
     c->l_Qn = c->Qn;
+    c->l_qoff = c->qoff;
     c->phase = 1;
     c->tick += 1;  // per-launch stamp: a relaunch with other messages never sees this launch's marks
     if (c->tbitsb[0]) c->tbits = c->tbitsb[c->tick & 1];  // the last tick's bits stay for its deferred commit
@@ -1605,6 +1848,7 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->waited = false;
     c->l_purge_only = c->next_purge_only;
     c->next_purge_only = false;
+    c->l_win = win_plan(c);
     const int rc = enqueue_tick(c);
     if (rc) return rc;
     if (E) {
@@ -1646,6 +1890,20 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             // functional tick again, grouped by the radix sort
             if (c->reruns > 4) return fail(c, FB_EHIP, "event regrouping did not converge");
             c->l_resort = true;
+            c->l_win = false;  // the sorted path purges in k_scan: a general tick
+            c->reruns++;
+            int rc = enqueue_tick(c);
+            if (rc) return rc;
+            continue;
+        }
+        if (c->l_win && (c->hout->status == 3 || c->hout->win_ovf)) {
+            // the window tick could not finish inside its window (a fill level above 0, an
+            // unserved front, a first unserved element past the scanned prefix, no room at
+            // the tail): the same functional tick on the general path
+            if (c->hout->status == 3 && (int64_t)c->l_nchW * kWinCh < c->l_Qn)  // the scanned prefix was short
+                c->win_slack = std::min<int64_t>(2 * c->win_slack, 1 << 24);
+            c->l_win = false;
+            c->win_fallbacks++;
             c->reruns++;
             int rc = enqueue_tick(c);
             if (rc) return rc;
@@ -1682,7 +1940,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     fb_tick_result r{};
     r.n_assigned = p.N_eff;
     r.n_orphans = p.O;
-    r.queue_len = (int64_t)p.new_qlen;
+    r.queue_len = c->l_win ? p.win_qlen : (int64_t)p.new_qlen;
     r.log_head = c->l_head + p.N_eff;
     r.n_evicted = (int32_t)p.n_evicted;
     r.fill_level = p.L;
@@ -1729,7 +1987,24 @@ int fb_tick_commit(fb_ctx *c) {
         a.ev_clr = c->ev_clr;
         a.bud = c->bud;
         a.bud_next = c->bud_next;
-        const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS);
+        if (c->l_win) {
+            // the window moves: positions of slots that left become tombstones, kept slots that
+            // got messages take their post-message counts, appended slots their positions
+            const HostOut &p = *c->hout;
+            a.win = 1;
+            a.wq_head = p.win_head;
+            a.wq_tail = c->l_qoff + c->l_Qn;
+            a.napp = p.win_head + p.new_qlen - a.wq_tail;
+            a.nbap = (int)cdiv(a.napp, kBS);
+            a.wq_buf = c->queue[c->qcur];
+            a.wqf = c->qfree[c->qcur];
+            a.wqh = c->qhb[c->qcur];
+            a.pos = c->pos_of[c->qcur];
+            a.wnpos = c->wnpos;
+            a.wstamp = c->lstamp;
+            a.post_rf = c->post_rf;
+        }
+        const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + a.nbap;
         if (c->ev_head && c->ev_ll && !c->commit_now) {
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
@@ -1747,8 +2022,22 @@ int fb_tick_commit(fb_ctx *c) {
     if (c->shard) c->shard_R = c->last.fill_level + 2 > kRFused ? c->l_R : 0;
     c->head = c->last.log_head;
     c->head_local += c->shard ? c->last.n_local : 0;
-    c->Qn = c->last.queue_len;
-    c->maxc_hint = std::max(1, c->last.max_free);
+    c->Qtrue = c->last.queue_len;
+    c->last_L = c->last.fill_level;
+    c->last_O = c->last.n_orphans;
+    if (c->l_win) {
+        // the queue stays in its buffers: the window slid and grew
+        c->qoff = c->hout->win_head;
+        c->Qn = c->hout->new_qlen;
+        c->win_ticks++;
+        // the scanned prefix saw only part of the queue: keep the larger hint
+        c->maxc_hint = std::max(c->maxc_hint, std::max(1, c->last.max_free));
+    } else {
+        c->qcur ^= 1;
+        c->qoff = 0;
+        c->Qn = c->last.queue_len;
+        c->maxc_hint = std::max(1, c->last.max_free);
+    }
     c->launched = c->waited = false;
     c->phase = 0;
     return FB_OK;
@@ -1820,6 +2109,15 @@ static int orph_out(fb_ctx *c, int64_t *dst, int64_t n) {
     }
     return d2h(c, dst, orph_dense_dev(c), (size_t)n * 8);
 }
+// A window tick leaves its evicted slots to the per-slot status bytes: the ascending list
+// is built (once per tick) when something reads it.
+static int evict_ready(fb_ctx *c) {
+    if (!c->l_win || c->evict_ok || !c->last.n_evicted) return FB_OK;
+    launch_evict_gather(c->evicted, c->st, c->wcnt, c->wpre, c->W, Stream(c->stream));
+    HIPCHK(c, hipGetLastError());
+    c->evict_ok = true;
+    return FB_OK;
+}
 static int copy_out(fb_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!bytes) return FB_OK;
     if (int rc = d2h(c, dst, src, bytes)) return rc;
@@ -1849,6 +2147,8 @@ int fb_get_evicted(fb_ctx *c, int32_t n, int32_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (n < 0 || n > c->last.n_evicted) return fail(c, FB_EINVAL, "evicted count");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (int rc = evict_ready(c)) return rc;
     return copy_out(c, dst, c->evicted, (size_t)n * 4);
 }
 
@@ -1862,8 +2162,29 @@ int fb_get_outputs(fb_ctx *c, int32_t *assign, int64_t *orphans, int32_t *evicte
     if (assign && c->last.n_assigned && (rc = d2h(c, assign, c->log_slot + c->l_head, (size_t)c->last.n_assigned * 4)))
         return rc;
     if (orphans && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
+    if (evicted && (rc = evict_ready(c))) return rc;
     if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
+    return FB_OK;
+}
+
+int fb_set_window(fb_ctx *c, int mode) {
+    if (!c) return FB_EINVAL;
+    if (c->shard || c->deque) return fail(c, FB_ESTATE, "window ticks exist on one-GPU heartbeat contexts only");
+    if (mode < -1 || mode > 1) return fail(c, FB_EINVAL, "window mode %d (-1 auto, 0 off, 1 on)", mode);
+    if (c->launched) return fail(c, FB_ESTATE, "fb_set_window between ticks only");
+    if (int rc = flush_commit(c)) return rc;
+    if (mode > 0) {
+        if (int rc = win_alloc(c)) return rc;
+    }
+    c->win = mode;
+    return FB_OK;
+}
+
+int fb_window_stats(fb_ctx *c, int64_t *window_ticks, int64_t *fallbacks) {
+    if (!c) return FB_EINVAL;
+    if (window_ticks) *window_ticks = c->win_ticks;
+    if (fallbacks) *fallbacks = c->win_fallbacks;
     return FB_OK;
 }
 
@@ -2062,9 +2383,16 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     v->last_heartbeat = c->hb;
     v->last_heartbeat_stride = (int32_t)sizeof(double);
     v->registered = c->reg;
-    v->queue = c->queue[c->cur];
+    if (c->win_cap && (c->qoff != 0 || c->Qn != c->Qtrue)) {
+        if (int rc = win_normalize(c)) return rc;
+    }
+    v->queue = c->queue[c->qcur];
     v->log_slot = c->log_slot;
     v->orphans = orph_dense_dev(c);
+    if (c->waited) {
+        if (int rc = evict_ready(c)) return rc;
+        HIPCHK(c, hipStreamSynchronize(c->stream));
+    }
     v->evicted = c->evicted;
     v->n_workers = c->W;
     v->queue_len = c->Qn;

@@ -51,6 +51,15 @@ constexpr uint8_t kRfCleared = 16;
 // k_emit2's log tiles (one-GPU fused ticks): at most this many log workgroups (4 tiles
 // of kFTile entries each; k_orph_gather sums up to 4 x this many tile counts per block)
 constexpr int kFEmitMaxBlocks = 1024;
+// window ticks (sliding level-0 queue, one GPU): 1024-element chunks of the
+// virtual order [backs][fronts][window prefix], counted by k_logscan's count waves (one
+// wave per chunk) and emitted by k_emit_win (one workgroup per chunk, which reads every
+// chunk's counts: at most kWinMaxCh of them)
+constexpr int kWinCh = 1024;
+constexpr int kWinMaxCh = 2048;
+constexpr int32_t kTomb = INT32_MIN;  // qfree of a window position whose slot left the queue
+// st bit: the slot was in the committed queue at tick start (window commits)
+constexpr uint8_t kStQ0 = 8;
 
 // Committed per-slot heartbeat: last_heartbeat, NaN when the slot holds no record
 // (so the log scan's one 8-byte gather per in-flight entry decides liveness
@@ -79,11 +88,18 @@ struct HostOut {
     int64_t cap_total;  // sum of c over live queued workers
     int32_t L;          // fill level
     int32_t maxc;       // max c
-    int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full
+    int32_t status;     // 1 = round table too narrow (rerun wider), 2 = in-flight log full,
+                        // 3 = window tick cannot finish in its window (rerun as a general tick)
                         // (deque contexts: new_qlen > token capacity is checked by the host)
     int32_t resort;     // k_ev_apply_ll: a slot got too many messages, rerun through the sort
     int64_t n_local;   // sharded: tasks appended to this rank's log shard
     int64_t O_local;    // sharded: this rank's orphans
+    // window ticks: the next window [win_head, win_head + new_qlen) of the queue buffer
+    // (tombstones included), the LRU queue's true length, and a store past the buffer
+    int64_t win_head;
+    int64_t win_qlen;
+    int32_t win_ovf;
+    int32_t pad_;
 };
 
 // totals computed by k_plan (large grids only; device memory, no atomics)
@@ -119,6 +135,21 @@ struct CommitArgs {
     const uint32_t *lseq;      // sharded: global sequence of each local entry (ascending)
     int64_t head_local;        // sharded: local entries
     int shard;
+    // window ticks: the committed window keeps [wq_head, wq_tail) of the queue
+    // buffer; per slot that was queued at tick start (st & kStQ0) and sits there, its
+    // position is tombstoned when the slot died or its messages moved it, refreshed with the
+    // post-message free count / heartbeat when they kept it; a touched slot the tick
+    // appended takes its new position from wnpos (tagged with the launch stamp), the
+    // untouched appended ones from the nbap blocks walking [wq_tail, wq_tail + napp)
+    int win;
+    int64_t wq_head, wq_tail, napp;
+    int nbap;
+    int32_t *wq_buf, *wqf;
+    double *wqh;
+    int32_t *pos;
+    const int2 *wnpos;
+    uint32_t wstamp;
+    const uint8_t *post_rf;
 };
 
 struct EvArgs {
@@ -186,6 +217,9 @@ struct EvArgs {
     uint32_t *wcnt;             // evictions per 256-slot tile, zeroed by k_ev_link, atomicAdd
     uint32_t *grp;              // group rows (null: none); evictions into column R + 2
     int ngrp, gstride, R;
+    // window ticks: evictions and live queued slots as 64 partials (128-byte lines, word 0 /
+    // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
+    uint32_t *wpart;
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -267,6 +301,24 @@ struct TickArgs {
     DevTotals *P_rep;   // [64]
     // outputs
     int32_t *log_slot;
+    // ---- window ticks (one GPU, heartbeat loop, level 0).  The committed queue
+    // is the window [wq_off, wq_tail) of a buffer of wq_cap entries (qfree kTomb: a position
+    // whose slot left); k_logscan's count waves count 1024-element chunks of [backs][fronts]
+    // [window prefix] (wagg), k_emit_win serves the first N live elements (fronts, then the
+    // window), appends the live backs and then the served workers with c > 1 at the tail
+    int win;
+    int64_t wq_off, wq_tail, wq_cap;
+    int32_t *wq_buf, *wqf_buf;
+    double *wqh_buf;
+    int nchB, nchF, nchW;
+    int4 *wagg;                  // per chunk {live fronts / window, of them c > 1, live backs, max c}
+    uint32_t *lpart;             // k_logscan: orphans per log workgroup
+    int n_lpart;
+    uint32_t *wpart;             // evictions / live queued slots, 64 partials (EvArgs::wpart)
+    int2 *wnpos;                 // touched slots appended: {position, launch stamp}
+    int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
+    int ls_cnt_blocks, ls_log_blocks;  // k_logscan grid: count workgroups first, then log workgroups
+    int32_t *pos_out;            // general ticks of window contexts: next-queue position per slot
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
     int32_t *rb_slot;   // compact assignments (null: off): slot per LRU position, -1 none
     uint8_t *rb_c;      // ... and min(c, L + 1) (clamped to 255)
@@ -348,6 +400,10 @@ void launch_plan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);
 void launch_emit_shard(const TickArgs &a, Stream st);
+void launch_emit_win(const TickArgs &a, int grid, Stream st);
+// evicted slots in ascending order from the per-slot status bytes and per-tile counts (two
+// launches: a one-workgroup scan of the tile counts, then one block per tile)
+void launch_evict_gather(int32_t *dst, const uint8_t *st, const uint32_t *wcnt, int64_t *wpre, int W, Stream s);
 void launch_commit(const CommitArgs &a, int grid, Stream st);
 // dst[i] = src[i], i < n (dst may be host memory mapped for the device: stores cross PCIe)
 void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st);

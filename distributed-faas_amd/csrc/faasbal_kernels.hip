@@ -656,7 +656,7 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
 // (task_dispatcher.py:343-390 per message, the purge of the preceding loop
 // iteration at the message's own clock first).  s: local slot, gs: global slot.
 struct SlotRun {
-    int reg, inq, qstat, qidx, cur_is_start, died_start;
+    int reg, inq, q0, qstat, qidx, cur_is_start, died_start;
     int32_t fr;
     double hb;
     uint32_t epoch;
@@ -672,6 +672,7 @@ struct SlotRun {
         infl0 = (a.defer_clr && reg) ? (uint32_t)(a.bud[s] - fq.x) : 0u;
         ncl = 0;
         inq = fq.y;
+        q0 = fq.y;
         qstat = inq ? kQsKeep : kQsOut;
         qidx = -1;
         cur_is_start = reg;
@@ -737,7 +738,7 @@ struct SlotRun {
         return cleared;
     }
     // the purge at the tick's clock of this touched slot (k_ev_apply_ll's launch)
-    __device__ __forceinline__ void purge(const EvArgs &a, uint32_t s, int reg0);
+    __device__ __forceinline__ bool purge(const EvArgs &a, uint32_t s, int reg0, bool &evicted);
     __device__ __forceinline__ void finish(const EvArgs &a, uint32_t s, uint32_t gs) {
         a.post[s] = PostRec{hb, fr, epoch};
         a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1) | (ncl ? kRfCleared : 0));
@@ -786,6 +787,17 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 
 // ------------------------------------------------------------ commit
 __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
+    const int nclr = (a.n_clr + kBS - 1) / kBS;
+    if (a.win && blk >= a.nbw + a.nbo + nclr) {
+        // window tick: positions the tick appended take their slots' pos (the touched ones
+        // take theirs from wnpos in the slot sweep)
+        const int64_t i = (int64_t)(blk - a.nbw - a.nbo - nclr) * kBS + threadIdx.x;
+        if (i >= a.napp) return;
+        const int64_t p = a.wq_tail + i;
+        const int s = a.wq_buf[p];
+        if (!(a.E > 0 && got_msg(a, s))) a.pos[s] = (int32_t)p;
+        return;
+    }
     if (blk >= a.nbw + a.nbo) {
         // entries the committed tick's results completed (one-GPU heartbeat contexts keep
         // the log read-only during the tick): they leave the in-flight log now
@@ -815,6 +827,30 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
     const int s = blk * kBS + threadIdx.x;
     if (s >= a.W) return;
     const uint8_t stt = a.st[s];
+    if (a.win) {
+        // window tick: the committed position of a slot queued at tick start that the tick
+        // did not serve -- tombstoned when the slot died or its messages moved it, else
+        // refreshed with its post-message free count and heartbeat if it got messages
+        const bool t = a.E > 0 && got_msg(a, s);
+        if (stt & kStQ0) {
+            const int32_t p = a.pos[s];
+            const bool inw = p >= a.wq_head && p < a.wq_tail;
+            if (inw && a.wq_buf[inw ? p : 0] == s) {
+                const bool moved = t && ((a.post_rf[s] >> 2) & 3) != kQsKeep;
+                if (!(stt & kStAlive) || moved) {
+                    a.wqf[p] = kTomb;
+                } else if (t) {
+                    const PostRec pr = a.post[s];
+                    a.wqf[p] = pr.free;
+                    a.wqh[p] = pr.hb;
+                }
+            }
+        }
+        if (t) {
+            const int2 np = a.wnpos[s];
+            if ((uint32_t)np.y == a.wstamp) a.pos[s] = np.x;
+        }
+    }
     // committed hb is NaN for slots without a record (k_scan's log role relies on it)
     if (a.E > 0 && got_msg(a, s)) {
         const bool alive = (stt & kStAlive) != 0;
@@ -853,7 +889,12 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
         return;
     }
     const int t = blockIdx.x * kBS + (int)threadIdx.x, nt = lb * kBS;
-    if (t == 0) a.hout->resort = 0;
+    if (t == 0) {
+        a.hout->resort = 0;
+        a.hout->win_ovf = 0;
+    }
+    // window ticks: the purge's partial counts (words 0 and 1 of 64 lines)
+    if (a.wpart && t < 128) a.wpart[(t >> 1) * 32 + (t & 1)] = 0u;
     for (int w = t; w < a.tbits_words; w += nt) a.tbits[w] = 0u;
     // the counters k_ev_apply_ll's slot purge accumulates with atomics
     for (int w = t; w < a.nbw; w += nt) a.wcnt[w] = 0u;
@@ -882,17 +923,27 @@ __device__ __forceinline__ int32_t log_peek(const EvArgs &a, int64_t seq) {
 // committed record, touched ones from the owner thread's post-message registers.
 // infl: the slot's in-flight entries after its messages; returns the orphans it leaves
 // (the entries of a registration that died), and writes the next in-flight count.
+// q0: the slot was in the committed queue at tick start (kStQ0, read by a window commit);
+// queued_out: a live position of this tick's LRU queue (window ticks count them).
 __device__ __forceinline__ uint32_t purge_slot(const EvArgs &a, int s, bool t, int reg0, int reg, double hb,
-                                               int32_t fr, int died_flag, bool queued_if_alive, uint32_t infl,
-                                               bool &died, bool &evicted, bool &alive_out) {
+                                               int32_t fr, int died_flag, bool queued_if_alive, int q0, uint32_t infl,
+                                               bool &died, bool &evicted, bool &alive_out, bool &queued_out) {
     const bool dead = reg && ((a.now - hb) > a.tte);
     const bool alive = reg && !dead;
     died = reg0 && (dead || died_flag);
     evicted = (reg0 || t) && !alive;
-    a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
-    a.free_out[s] = make_int2(alive ? fr : INT32_MIN, (alive && queued_if_alive) ? 1 : 0);
+    a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died ? kStDiedStart : 0) | (evicted ? kStEvicted : 0) |
+                        (q0 ? kStQ0 : 0));
+    queued_out = alive && queued_if_alive;
+    a.free_out[s] = make_int2(alive ? fr : INT32_MIN, queued_out ? 1 : 0);
     alive_out = alive;
     return died ? infl : 0u;
+}
+// window ticks: a wave's evictions and live queued slots into partial `part` (one line each)
+__device__ __forceinline__ void count_wpart(const EvArgs &a, int part, uint32_t ne, uint32_t nq) {
+    uint32_t *w = a.wpart + (size_t)(part & 63) * 32;
+    if (ne) atomicAdd(w, ne);
+    if (nq) atomicAdd(w + 1, nq);
 }
 __device__ __forceinline__ void count_evicted(const EvArgs &a, int tile, uint32_t n) {
     atomicAdd(&a.wcnt[tile], n);
@@ -904,17 +955,21 @@ __device__ __forceinline__ void count_orphans(const EvArgs &a, int tile, uint32_
     if (a.orph_grp && n) atomicAdd(&a.grp[(tile % a.ngrp) * a.gstride + a.R + 1], n);
 }
 
-__device__ __forceinline__ void SlotRun::purge(const EvArgs &a, uint32_t s, int reg0) {
-    bool died, evicted, alive;
-    const uint32_t no = purge_slot(a, (int)s, true, reg0, reg, hb, fr, died_start, qstat != kQsOut, infl0 - ncl,
-                                   died, evicted, alive);
+__device__ __forceinline__ bool SlotRun::purge(const EvArgs &a, uint32_t s, int reg0, bool &evicted) {
+    bool died, alive, queued;
+    const uint32_t no = purge_slot(a, (int)s, true, reg0, reg, hb, fr, died_start, qstat != kQsOut, q0, infl0 - ncl,
+                                   died, evicted, alive, queued);
     // the budget the commit installs: a new registration after a death starts with no
     // in-flight entries (a dead slot's budget is never read)
     if (a.bud_next) a.bud_next[s] = (int32_t)((alive && !died) ? infl0 - ncl : 0u) + fr;
     if (died && a.dmask) atomicOr(&a.dmask[s >> 6], 1ull << (s & 63));
     if (evicted) count_evicted(a, (int)(s >> 8), 1u);
     count_orphans(a, (int)(s >> 8), no);
+    return queued;
 }
+
+__device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t s, int e, int hidx, int kind0,
+                                          int32_t val0, double ts0, int64_t seq0, int reg0, bool &ev);
 
 __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     prefetch_args(a);
@@ -922,7 +977,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     if ((int)blockIdx.x >= nba) {
         const int blk = (int)blockIdx.x - nba;
         const int s = blk * kBS + (int)threadIdx.x;
-        bool died = false, evicted = false;
+        bool died = false, evicted = false, queued = false;
         uint32_t no = 0;
         if (s < a.W) {
             // the link stamp says whether the slot got messages (its owner purges it); the
@@ -934,15 +989,19 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
             const int32_t b0 = a.bud ? a.bud[s] : 0;
             const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(b0 - fq0.x) : 0u;
             bool alive;
-            if (!t) no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, in0, died, evicted, alive);
+            if (!t)
+                no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, fq0.y, in0, died, evicted, alive,
+                                queued);
         }
         const uint64_t dm = __ballot(died);
         const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
+        const uint32_t nq = (uint32_t)__popcll(__ballot(queued));
         const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
         if (lane_id() == 0) {
             if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
             if (ne) count_evicted(a, blk, ne);
             count_orphans(a, blk, nw);
+            if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
         }
         return;
     }
@@ -962,12 +1021,26 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     SlotRun r;
     r.init(a, s);
     const int reg0 = r.reg;
+    bool qd = false, ev = false;  // window ticks: this slot queued after the purge / evicted
     if (hidx == e) {  // the slot's only message (most slots)
         r.step<true>(a, s, e, kind0, val0, ts0, seq0, logv0);
         r.finish(a, s, s);
-        if (a.nbw) r.purge(a, s, reg0);
-        return;
+        if (a.nbw) qd = r.purge(a, s, reg0, ev);
+    } else {
+        qd = apply_run(a, r, s, e, hidx, kind0, val0, ts0, seq0, reg0, ev);
     }
+    if (a.wpart) {
+        // one atomic per wave, by its first owner lane (the others returned above)
+        const uint64_t act = __ballot(true);
+        const uint32_t ne = (uint32_t)__popcll(__ballot(ev)), nq = (uint32_t)__popcll(__ballot(qd));
+        if (lane_id() == (int)__builtin_ctzll(act)) count_wpart(a, (int)blockIdx.x * kWaves + wave_id(), ne, nq);
+    }
+}
+
+// A slot with several messages (k_ev_apply_ll): walk head -> ... -> e, restore arrival
+// order, apply them in order, purge.  Returns whether the slot is queued after the purge.
+__device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t s, int e, int hidx, int kind0,
+                                          int32_t val0, double ts0, int64_t seq0, int reg0, bool &ev) {
     // walk head -> ... -> e (link order), each message's payload loaded with its link
     int idx[kLinkMax], kd[kLinkMax];
     int32_t vl[kLinkMax];
@@ -992,7 +1065,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     }
     if (!done) {  // too many messages for the registers: the host reruns through the sort
         a.hout->resort = 1;
-        return;
+        return false;
     }
     // sort the messages into arrival order (bitonic network, static register indices;
     // padding entries carry INT32_MAX and stay last).  n <= 4: the first four suffice.
@@ -1046,7 +1119,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
         }
     }
     r.finish(a, s, s);
-    if (a.nbw) r.purge(a, s, reg0);
+    return a.nbw ? r.purge(a, s, reg0, ev) : false;
 }
 
 
@@ -1231,7 +1304,8 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         const bool alive = c.reg && !dead;
         died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
         evicted = !a.deque && (c.reg0 || c.t) && !alive;  // start() never deletes a record
-        a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0));
+        a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0) |
+                            (c.q0 ? kStQ0 : 0));
         // queued: a live position of this tick's LRU queue (committed and kept, or a
         // front / back insertion) -- k_emit2 then rewrites only the slots it serves
         const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
@@ -1506,8 +1580,10 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 const PostRec pr = a.post[sq];
                 hbq = pr.hb;
                 raw = ((rf & 1) && !((a.now - pr.hb) > a.tte)) ? pr.free : INT32_MIN;
-                // moved to the front, re-appended or removed by this tick's messages
-                if (((rf >> 2) & 3) != kQsKeep) raw = INT32_MIN;
+                // moved to the front, re-appended or removed by this tick's messages; or a
+                // window position whose slot had left the queue (kTomb: its slot may be queued
+                // again at a later position)
+                if (((rf >> 2) & 3) != kQsKeep || fq == kTomb) raw = INT32_MIN;
             }
         } else {
             s = lq_slot(a, pos);
@@ -1664,6 +1740,101 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     STAMP(a, SO, 15);
 }
 
+// ------------------------------------------------------------ window ticks
+// A level-0 tick serves the first N = O + T live positions of fronts ++ queue ++ backs
+// and its next queue is the rest followed by the served workers with c > 1, so when
+// every front is served and the N-th live position falls inside the committed window,
+// the tick touches only the window's served prefix: the suffix stays where it is, the
+// live backs and then the served workers with c > 1 are appended at the window's tail.
+// The elements are numbered in the order [backs][fronts][window]: 1024-element chunks,
+// counted by k_logscan's count waves, emitted by k_emit_win.
+struct WinEl {
+    int s;        // slot, -1: a hole of a list
+    int32_t raw;  // free count of a live queued position, INT32_MIN otherwise
+    double hb;
+    bool t;       // the slot got messages this tick
+};
+// region of chunk ch: 0 backs, 1 fronts, 2 window; [i0, i1) its element range in the region
+__device__ __forceinline__ int win_region(const TickArgs &a, int ch, int64_t &i0, int64_t &i1) {
+    if (ch < a.nchB) {
+        i0 = (int64_t)ch * kWinCh;
+        i1 = min(i0 + kWinCh, (int64_t)a.E);
+        return 0;
+    }
+    if (ch < a.nchB + a.nchF) {
+        i0 = (int64_t)(ch - a.nchB) * kWinCh;
+        i1 = min(i0 + kWinCh, (int64_t)a.E);
+        return 1;
+    }
+    i0 = a.wq_off + (int64_t)(ch - a.nchB - a.nchF) * kWinCh;
+    i1 = min(i0 + kWinCh, a.wq_tail);
+    return 2;
+}
+// The element's slot and raw free count, as k_scan's queue role classifies a position:
+// a list entry (a front / back insertion of this tick) from the purge's next free count,
+// a committed window position from its ride-along free count and heartbeat unless the
+// slot got messages (then its post-message record) or the position is a tombstone.
+// Loads are issued before the tests (clamped indices).
+__device__ __forceinline__ WinEl win_elem(const TickArgs &a, int reg, int64_t i, bool in) {
+    WinEl e;
+    if (reg < 2) {
+        const int32_t *lst = reg == 0 ? a.back_list : a.front_list;
+        const int64_t ic = in ? i : 0;
+        const int s1 = a.E > 0 ? lst[ic] : 0;
+        const int sc = s1 > 0 ? s1 - 1 : 0;
+        const int32_t fr = a.free_out[sc].x;
+        const double h = a.post[sc].hb;
+        e.s = s1 - 1;
+        e.raw = (in && s1 > 0) ? fr : INT32_MIN;
+        e.hb = h;
+        e.t = true;
+    } else {
+        const int64_t ic = in ? i : a.wq_off;
+        const int sq = a.wq_buf[ic];
+        const int32_t fq = a.wqf_buf[ic];
+        const double hq = a.wqh_buf[ic];
+        const bool tq = got_msg(a, sq);
+        int32_t raw = ((a.now - hq) > a.tte) ? INT32_MIN : fq;
+        double hb = hq;
+        if (tq) {
+            const uint8_t rf = a.post_rf[sq];
+            const PostRec pr = a.post[sq];
+            hb = pr.hb;
+            raw = ((rf & 1) && !((a.now - pr.hb) > a.tte) && ((rf >> 2) & 3) == kQsKeep) ? pr.free : INT32_MIN;
+        }
+        if (fq == kTomb || !in) raw = INT32_MIN;
+        e.s = sq;
+        e.raw = raw;
+        e.hb = hb;
+        e.t = tq;
+    }
+    return e;
+}
+__device__ __forceinline__ int win_c(int32_t raw) { return raw != INT32_MIN ? (raw > 1 ? raw : 1) : 0; }
+
+// Count wave of k_logscan's launch (window ticks): chunk ch, lane l takes elements
+// i0 + 64 g + l (g < 16, all loads of a round in flight): live elements, those with
+// c > 1 (fronts / window) or live backs, and the largest c -> wagg[ch].
+__device__ __forceinline__ void win_count(const TickArgs &a, int ch) {
+    int64_t i0, i1;
+    const int reg = win_region(a, ch, i0, i1);
+    const int lane = lane_id();
+    uint32_t nl = 0, ng = 0, mx = 0;
+#pragma unroll 4
+    for (int g = 0; g < kWinCh / 64; ++g) {
+        const int64_t i = i0 + 64 * g + lane;
+        const WinEl e = win_elem(a, reg, i, i < i1);
+        const int c = win_c(e.raw);
+        nl += c > 0 ? 1u : 0u;
+        ng += c > 1 ? 1u : 0u;
+        mx = (uint32_t)c > mx ? (uint32_t)c : mx;
+    }
+    nl = wave_sum_u32(nl);
+    ng = wave_sum_u32(ng);
+    mx = wave_max_u32(mx);
+    if (lane == 0) a.wagg[ch] = reg == 0 ? make_int4(0, 0, (int)nl, (int)mx) : make_int4((int)nl, (int)ng, 0, (int)mx);
+}
+
 // ------------------------------------------------------------ k_logscan
 // The log role of k_scan as its own launch for large tables (a.f_sep): past 128K
 // slots a gather per in-flight entry -- into the 16-byte records or the global
@@ -1677,6 +1848,15 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long bm[];
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows
     STAMP(a, SO, 0);
+    // window ticks: the first ls_cnt_blocks workgroups count the tick's chunks (one wave
+    // per chunk), the rest are the log role
+    if ((int)blockIdx.x < a.ls_cnt_blocks) {
+        const int ch = (int)blockIdx.x * (kLsBS / 64) + (int)(threadIdx.x >> 6);
+        if (ch < a.nchB + a.nchF + a.nchW) win_count(a, ch);
+        return;
+    }
+    const int lblk = (int)blockIdx.x - a.ls_cnt_blocks;
+    const int nlblk = (int)gridDim.x - a.ls_cnt_blocks;
     const int n4 = (((a.W + 63) >> 6) + 1) >> 1;
     const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
     for (int i0 = 0; i0 < n4; i0 += kLsBS * 8) {
@@ -1700,7 +1880,8 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
     const int lane = lane_id();
     constexpr int nw = kLsBS / 64;
     const int64_t nlog = a.shard ? a.head_local : a.head_in;
-    for (int b = blockIdx.x * nw + (int)(threadIdx.x >> 6); b < a.nbf; b += gridDim.x * nw) {
+    uint32_t wtot = 0;  // this wave's orphans (window ticks: the workgroup's partial)
+    for (int b = lblk * nw + (int)(threadIdx.x >> 6); b < a.nbf; b += nlblk * nw) {
         int32_t v[4][kFItems];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -1729,15 +1910,38 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
                 flags |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
             }
             flags = drop_completed(a, flags, v[k], (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems);
-            a.ofl[(size_t)b * kBS + k * 64 + lane] = (uint8_t)flags;
-            cnt += (uint32_t)__popc(flags);
+            if (a.wseg) {
+                // the tile's orphans, ascending, into its own segment (orphans[b*2048 + i]):
+                // entry order is k, then lane, then j
+                const uint32_t n = (uint32_t)__popc(flags);
+                const uint32_t inc = wave_incl_scan_u32(n);
+                int64_t o = (int64_t)b * kFTile + cnt + inc - n;
+                const int64_t e0 = (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems;
+                for (uint32_t m = flags; m; m &= m - 1) a.orphans[o++] = e0 + __builtin_ctz(m);
+                cnt += (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+            } else {
+                a.ofl[(size_t)b * kBS + k * 64 + lane] = (uint8_t)flags;
+                cnt += (uint32_t)__popc(flags);
+            }
         }
-        cnt = wave_sum_u32(cnt);
+        if (!a.wseg) cnt = wave_sum_u32(cnt);
+        wtot += cnt;
         if (lane == 0) {
             a.fcnt[b] = cnt;
             if (FAASBAL_GRP_OW && a.grp_on && cnt) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], cnt);
             if (a.shard && cnt)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)cnt);
+        }
+    }
+    if (a.wseg) {
+        // the workgroup's orphans (k_emit_win sums the partials for O)
+        __shared__ uint32_t lp[kLsBS / 64];
+        if (lane == 0) lp[threadIdx.x >> 6] = wtot;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+            for (int q = 0; q < kLsBS / 64; ++q) t += lp[q];
+            a.lpart[lblk] = t;
         }
     }
     STAMP(a, SO, 15);
@@ -2206,6 +2410,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
                 a.qhb_out[np] = hbp;
+                if (a.pos_out) a.pos_out[s] = (int32_t)np;
             }
         }
         STAMPR(a, SO, 14);
@@ -2684,6 +2889,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 wt_store(a.queue_out + np, s);
                 wt_store(a.qfree_out + np, raw - (int32_t)n_q);
                 wt_store(a.qhb_out + np, hb0);
+                if (a.pos_out) a.pos_out[s] = (int32_t)np;  // window contexts: where the slot sits next
             }
         }
         STAMP(a, SO, 15);
@@ -2739,6 +2945,164 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         for (uint32_t m = e; m; m &= m - 1) wt_store(a.evicted + o++, (int32_t)(s0 + __builtin_ctz(m)));
     }
     STAMP(a, SO, 15);
+}
+
+// ------------------------------------------------------------ k_emit_win
+// The level-0 emission of a window tick (see win_elem): one workgroup per 1024-element
+// chunk, thread t takes elements i0 + 256 j + t (j < 4).  Every workgroup first reads all
+// chunk counts (<= 8 int4 loads per thread), the log workgroups' orphan partials and the
+// purge's eviction / queued partials, so each knows N = O + T, the live fronts LF, the
+// live window prefix LW, the live backs LB and its own exclusive prefixes; then the
+// tick is decided the same way in every workgroup: it needs LF <= N < LF + LW (every
+// front served, the first unserved live element inside the scanned window), else
+// status 3 and the host reruns the tick on the general path.  Live element k < N takes
+// task k (k_emit2's round 0); live backs are appended at the tail in order, then the
+// served workers with c > 1 in order (A_0[p:] ++ [served, c > 1]); the element of rank
+// N - 1 knows where the next window starts and how long it is.
+__global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
+    prefetch_args(a);
+    __shared__ uint32_t red[kWaves][12];
+    __shared__ uint32_t wt[4][kWaves][2];
+    const int ch = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int nch = a.nchB + a.nchF + a.nchW;
+    // ---- the tick's totals and this chunk's prefixes
+    uint32_t LB = 0, LF = 0, LW = 0, blx = 0, lvx = 0, g1x = 0, mx = 0, O = 0, nev = 0, nq = 0;
+    {
+        int4 v[kWinMaxCh / kBS];
+#pragma unroll
+        for (int k = 0; k < kWinMaxCh / kBS; ++k) v[k] = a.wagg[min(tid + k * kBS, nch - 1)];
+        const uint32_t op = tid < a.n_lpart ? a.lpart[tid] : 0u;
+        const uint32_t e0 = tid < 64 ? a.wpart[(size_t)tid * 32] : 0u, q0 = tid < 64 ? a.wpart[(size_t)tid * 32 + 1] : 0u;
+#pragma unroll
+        for (int k = 0; k < kWinMaxCh / kBS; ++k) {
+            const int i = tid + k * kBS;
+            const bool ok = i < nch, B = i < a.nchB, F = !B && i < a.nchB + a.nchF;
+            const uint32_t lv = ok ? (uint32_t)v[k].x : 0u, g1 = ok ? (uint32_t)v[k].y : 0u, bl = ok ? (uint32_t)v[k].z : 0u;
+            LB += B ? bl : 0u;
+            LF += F ? lv : 0u;
+            LW += (!B && !F) ? lv : 0u;
+            blx += i < ch ? bl : 0u;
+            lvx += i < ch ? lv : 0u;
+            g1x += i < ch ? g1 : 0u;
+            mx = (ok && (uint32_t)v[k].w > mx) ? (uint32_t)v[k].w : mx;
+        }
+        O = op;
+        nev = e0;
+        nq = q0;
+        uint32_t x[10] = {LB, LF, LW, blx, lvx, g1x, O, nev, nq, 0};
+#pragma unroll
+        for (int q = 0; q < 9; ++q) x[q] = wave_sum_u32(x[q]);
+        x[9] = wave_max_u32(mx);
+        if (lane == 0)
+#pragma unroll
+            for (int q = 0; q < 10; ++q) red[w][q] = x[q];
+        lds_barrier();
+#pragma unroll
+        for (int q = 0; q < 9; ++q) x[q] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
+        x[9] = max(max(red[0][9], red[1][9]), max(red[2][9], red[3][9]));
+        LB = x[0]; LF = x[1]; LW = x[2]; blx = x[3]; lvx = x[4]; g1x = x[5]; O = x[6]; nev = x[7]; nq = x[8];
+        mx = x[9];
+    }
+    const int64_t N = (int64_t)O + a.T;
+    int status = 0;
+    if (N < (int64_t)LF || N >= (int64_t)LF + LW) status = 3;  // not a window tick: the general path
+    else if (a.head_in + N > a.log_cap) status = 2;            // never write past the in-flight log
+    if (ch == 0 && tid == 0) {
+        a.hout->O = O;
+        a.hout->n_evicted = nev;
+        a.hout->cap_total = -1;  // beyond the scanned prefix (a window tick never needs it)
+        a.hout->maxc = (int32_t)mx;
+        a.hout->L = 0;
+        a.hout->status = status;
+        a.hout->N_eff = status ? 0 : N;
+        a.hout->p = N;
+        a.hout->AL = (int64_t)LF + LW + LB;  // at least
+        if (N == 0) {
+            a.hout->win_head = a.wq_off;
+            a.hout->new_qlen = a.wq_tail + LB - a.wq_off;
+            a.hout->win_qlen = nq;
+            if (a.wq_tail + LB - a.wq_off > a.q_cap) a.hout->win_ovf = 1;
+        }
+    }
+    if (status) return;
+    int64_t i0, i1;
+    const int reg = win_region(a, ch, i0, i1);
+    if (reg != 0 && (int64_t)lvx >= N) return;  // every element of the chunk stays put
+    // ---- elements: classification, then one LDS round for the in-chunk ranks
+    WinEl e[4];
+    uint64_t ml[4], mg[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int64_t i = i0 + j * kBS + tid;
+        e[j] = win_elem(a, reg, i, i < i1);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int c = win_c(e[j].raw);
+        ml[j] = __ballot(c > 0);
+        mg[j] = __ballot(c > 1);
+        if (lane == 0) {
+            wt[j][w][0] = (uint32_t)__popcll(ml[j]);
+            wt[j][w][1] = (uint32_t)__popcll(mg[j]);
+        }
+    }
+    lds_barrier();
+    uint32_t bl = 0, bg = 0;  // elements of the earlier sub-rounds / waves
+    int32_t *const q = a.wq_buf;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        uint32_t rl = bl, rg = bg;
+#pragma unroll
+        for (int u = 0; u < kWaves; ++u) {
+            rl += u < w ? wt[j][u][0] : 0u;
+            rg += u < w ? wt[j][u][1] : 0u;
+            bl += wt[j][u][0];
+            bg += wt[j][u][1];
+        }
+        rl += (uint32_t)popc_lt(ml[j]);
+        rg += (uint32_t)popc_lt(mg[j]);
+        const WinEl &x = e[j];
+        const int c = win_c(x.raw);
+        if (c == 0) continue;
+        if (reg == 0) {
+            // a live back: appended in order
+            const int64_t pq = a.wq_tail + blx + rl;
+            if (pq < a.wq_cap) {
+                q[pq] = x.s;
+                a.wqf_buf[pq] = x.raw;
+                a.wqh_buf[pq] = x.hb;
+                a.wnpos[x.s] = make_int2((int)pq, (int)a.lstamp);
+            } else {
+                a.hout->win_ovf = 1;
+            }
+            continue;
+        }
+        const int64_t k = (int64_t)lvx + rl;
+        if (k >= N) continue;
+        // served: task k, one fewer free process; c > 1 stays queued, appended after the backs
+        if (a.head_in + k < a.log_cap) a.log_slot[a.head_in + k] = x.s;
+        a.free_out[x.s] = make_int2(x.raw - 1, c > 1 ? 1 : 0);
+        const int64_t G = (int64_t)g1x + rg + (c > 1 ? 1 : 0);  // served workers with c > 1 so far
+        if (c > 1) {
+            const int64_t pq = a.wq_tail + LB + G - 1;
+            if (pq < a.wq_cap) {
+                q[pq] = x.s;
+                a.wqf_buf[pq] = x.raw - 1;
+                a.wqh_buf[pq] = x.hb;
+                if (x.t) a.wnpos[x.s] = make_int2((int)pq, (int)a.lstamp);
+            } else {
+                a.hout->win_ovf = 1;
+            }
+        }
+        if (k == N - 1) {
+            const int64_t head = reg == 2 ? i0 + j * kBS + tid + 1 : a.wq_off;
+            a.hout->win_head = head;
+            a.hout->new_qlen = a.wq_tail + LB + G - head;
+            a.hout->win_qlen = (int64_t)nq - (N - G);
+            // the next window, tombstones included, must fit a general tick's position arrays
+            if (a.wq_tail + LB + G - head > a.q_cap) a.hout->win_ovf = 1;
+        }
+    }
 }
 
 // ------------------------------------------------------------ k_emit_shard
@@ -3139,6 +3503,23 @@ __global__ __launch_bounds__(kBS) void k_orph_gather(int64_t *__restrict__ dst, 
     for (uint32_t i = threadIdx.x; i < n; i += kBS) dst[off + i] = src[(int64_t)t * kFTile + i];
 }
 
+// Evicted slots in ascending order when the tick did not compact them (window ticks):
+// one workgroup scans the per-tile eviction counts, then one block per 256-slot tile
+// writes its evicted slots at its offset (dst may be host-mapped memory).
+__global__ __launch_bounds__(kBS) void k_wscan(const uint32_t *__restrict__ wcnt, int ntile, int64_t *__restrict__ wpre) {
+    __shared__ unsigned long long l4[kWaves];
+    run_excl_scan(wcnt, 1, ntile, wpre, 1, l4);
+}
+__global__ __launch_bounds__(kBS) void k_evict_compact(int32_t *__restrict__ dst, const uint8_t *__restrict__ st,
+                                                      const int64_t *__restrict__ wpre, int W) {
+    __shared__ uint32_t l4[kWaves];
+    const int b = blockIdx.x, s = b * kBS + threadIdx.x;
+    const uint32_t e = (s < W) & ((st[min(s, W > 0 ? W - 1 : 0)] & kStEvicted) != 0);
+    uint32_t tot;
+    const uint32_t ex = block_excl_scan_u32(e, l4, tot);
+    if (e) dst[wpre[b] + ex] = s;
+}
+
 // ------------------------------------------------------------ readback
 // Several word copies in one launch (a tick's outputs into pinned host memory with one
 // kernel instead of one per array): copy i takes the blocks [b_i, b_{i+1}) of the grid.
@@ -3272,7 +3653,8 @@ void launch_scan(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
 }
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
-    const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
+    // + the spare slot; no bitmap without log workgroups (a window tick without a log)
+    const size_t lds = grid > a.ls_cnt_blocks ? (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16 : 0;
     hipExtLaunchKernelGGL(k_logscan, dim3(grid), dim3(kLsBS), lds, st.s, st.e0, st.e1, 0, a);
 }void launch_plan(const TickArgs &a, Stream st) {
     if (a.grp_on)
@@ -3312,6 +3694,15 @@ void launch_emit_shard(const TickArgs &a, Stream st) {
     }
     hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4), dim3(kBS), 0, st.s, st.e0,
                           st.e1, 0, a);
+}
+void launch_evict_gather(int32_t *dst, const uint8_t *st, const uint32_t *wcnt, int64_t *wpre, int W, Stream s) {
+    const int nt = cdiv(W, kBS);
+    if (nt <= 0) return;
+    hipExtLaunchKernelGGL(k_wscan, dim3(1), dim3(kBS), 0, s.s, s.e0, nullptr, 0, wcnt, nt, wpre);
+    hipExtLaunchKernelGGL(k_evict_compact, dim3(nt), dim3(kBS), 0, s.s, nullptr, s.e1, 0, dst, st, (const int64_t *)wpre, W);
+}
+void launch_emit_win(const TickArgs &a, int grid, Stream st) {
+    hipExtLaunchKernelGGL(k_emit_win, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_commit(const CommitArgs &a, int grid, Stream st) {
     hipExtLaunchKernelGGL(k_commit, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -233,6 +233,17 @@ class GpuBalancer:
                 None if orphans is None else orphans[: r["n_orphans_local"]],
                 None if evicted is None else evicted[: r["n_evicted"]])
 
+    def set_window(self, mode=1):
+        """Window ticks (fb_set_window): -1 auto (contexts of more than 128K workers), 0 off,
+        1 whenever the last tick was at fill level 0.  Results are identical either way."""
+        self._chk(self.lib.fb_set_window(self.h, int(mode)))
+
+    def window_stats(self):
+        """(committed window ticks, launches that fell back to the general path)."""
+        a, b = C.c_int64(0), C.c_int64(0)
+        self._chk(self.lib.fb_window_stats(self.h, C.byref(a), C.byref(b)))
+        return a.value, b.value
+
     def set_compact(self, on=True):
         """Ticks launched afterwards also write the compact assignment form (slot and
         min(c, L + 1) per LRU position): ``outputs_compact`` then reads 5 bytes per

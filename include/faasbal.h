@@ -168,6 +168,19 @@ int fb_get_outputs(fb_ctx *ctx, int32_t *assign, int64_t *orphans, int32_t *evic
  * when L + 1 > 255); fb_expand_compact turns it into fb_get_assignments' array on the
  * host (result->n_assigned slots). */
 int fb_set_compact(fb_ctx *ctx, int enable);
+
+/* Window ticks (one-GPU heartbeat contexts).  A tick at fill level 0
+ * (fewer tasks than live queued workers, the streaming case) serves a prefix of the LRU
+ * queue; as a window tick it leaves the rest of the queue where it is and appends the
+ * re-queued workers at its tail, so its work is O(tasks + messages) instead of O(queue).
+ * Results are identical either way (the closed form of task_dispatcher.py:393-419);
+ * a tick that turns out not to qualify is rerun on the general path.  mode: -1 auto
+ * (the default: contexts of more than 128K workers, after a level-0 tick), 0 off, 1
+ * whenever the last tick was not above level 0 (allocates the window buffers on contexts
+ * created without them).  Between ticks only. */
+int fb_set_window(fb_ctx *ctx, int mode);
+/* Committed window ticks, and launches that fell back to the general path. */
+int fb_window_stats(fb_ctx *ctx, int64_t *window_ticks, int64_t *fallbacks);
 int fb_get_outputs_compact(fb_ctx *ctx, int32_t *slot, uint8_t *c, int64_t cap, int64_t *n_pos, int64_t *orphans,
                            int32_t *evicted);
 int fb_expand_compact(fb_ctx *ctx, const int32_t *slot, const uint8_t *c, int64_t n_pos, int32_t *assign);

@@ -69,10 +69,13 @@ def _cmp(a, b, t):
 
 
 @pytest.mark.gpu
-def test_gpu_stream_1m_workers_matches_oracle():
+@pytest.mark.parametrize("window", [-1, 0], ids=["auto", "general"])
+def test_gpu_stream_1m_workers_matches_oracle(window):
     """configs[4] per GPU: 1M workers, 64K new tasks + 64K results + joins +
     heartbeats per tick, the clock advancing so silent workers expire; committed
-    ticks, every output and the post-state compared with the oracle (heap purge)."""
+    ticks, every output and the post-state compared with the oracle (heap purge).
+    auto: level-0 ticks after the first run as window ticks; general:
+    every tick on the general path (fb_set_window(0))."""
     from faasbal import GpuBalancer
     from oracle import Oracle
     W, T = 1 << 20, 65536
@@ -82,6 +85,7 @@ def test_gpu_stream_1m_workers_matches_oracle():
     cap = len(st["log"]) + 8 * T
     E = max(len(t["ev_kind"]) for t in ticks)
     g = GpuBalancer(W, cap, max_events=E, device=0)
+    g.set_window(window)
     g.load(st)
     o = Oracle(W, cap, purge_mode=2)  # heap purge: per-event clocks over 1M slots
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
@@ -102,6 +106,8 @@ def test_gpu_stream_1m_workers_matches_oracle():
     m = so["reg"].astype(bool)
     np.testing.assert_array_equal(sg["free"][m], so["free"][m])
     np.testing.assert_array_equal(sg["hb"][m], so["hb"][m])
+    wt, _ = g.window_stats()
+    assert (wt >= 2) if window else (wt == 0), "window ticks: %d" % wt
     g.close()
 
 

@@ -1,0 +1,162 @@
+"""Window ticks (the sliding level-0 queue) vs the oracle.
+
+A level-0 tick serves a prefix of the LRU queue; as a window tick it leaves the rest
+of the queue in place (positions whose slot left become tombstones) and appends the
+re-queued workers at the tail.  Every output and the post-tick state must equal the
+oracle's (task_dispatcher.py:324-419 restated) whichever path a tick takes, including
+general ticks that read a window with tombstones and window ticks that fall back to
+the general path.  Window mode is forced on small contexts (fb_set_window(1)); the
+1M-worker stream of tests/test_full_size.py runs it in its default (auto) mode.
+"""
+import numpy as np
+import pytest
+
+from faasbal import GpuBalancer, synth
+from oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _pair(st, log_cap, max_events, window=1, purge_mode=1):
+    W = len(st["reg"])
+    g = GpuBalancer(W, log_cap, max_events=max_events)
+    g.set_window(window)
+    g.load(st)
+    o = Oracle(W, log_cap, purge_mode=purge_mode)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    return g, o
+
+
+def _cmp(g, o, a, b, t):
+    for k in ("reconnect", "assign", "orphans", "evicted"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg="tick %d: %s" % (t, k))
+    assert a["result"]["queue_len"] == len(o.export()["queue"]), "tick %d: queue length" % t
+    sg, so = g.read_state(), o.export()
+    np.testing.assert_array_equal(sg["reg"], so["reg"], err_msg="tick %d reg" % t)
+    reg = so["reg"].astype(bool)
+    np.testing.assert_array_equal(sg["free"][reg], so["free"][reg], err_msg="tick %d free" % t)
+    np.testing.assert_array_equal(sg["hb"][reg], so["hb"][reg], err_msg="tick %d hb" % t)
+    np.testing.assert_array_equal(sg["queue"], so["queue"], err_msg="tick %d queue" % t)
+    np.testing.assert_array_equal(sg["log"], so["log"], err_msg="tick %d log" % t)
+
+
+def _stream(seed, W, T, dt, n_ticks, hb_frac=0.01, join_frac=0.002):
+    st = synth.zipf_state(W=W, seed=seed, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=n_ticks, seed=seed + 7, tasks_per_tick=T, results_per_tick=T,
+                               dt=dt, hb_frac=hb_frac, join_frac=join_frac)
+    return st, ticks
+
+
+@pytest.mark.parametrize("seed,W,T,dt", [(0, 8192, 512, 0.5), (1, 8192, 1024, 0.6), (2, 4096, 256, 0.5),
+                                         (3, 20000, 2048, 0.05), (4, 8192, 64, 1.0)])
+def test_window_stream_vs_oracle(seed, W, T, dt):
+    """configs[4]'s event mix at reduced size: results of in-flight tasks, joins (moved
+    to the front), heartbeats (kept in place, refreshed at commit), expiry by the clock
+    (tombstones); most ticks run as window ticks."""
+    st, ticks = _stream(seed, W, T, dt, n_ticks=10)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g, o = _pair(st, 3 * len(st["log"]) + 20 * T + 16, max_events=E, purge_mode=2)
+    carried = 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp(g, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    wt, fb = g.window_stats()
+    assert wt >= 5, "window ticks: %d (fallbacks %d)" % (wt, fb)
+    g.close()
+
+
+@pytest.mark.parametrize("seed", range(24))
+def test_window_random_vs_oracle(seed):
+    """Every message kind and edge case of the random scenarios (register 0 / -1 of a
+    queued worker, reconnects, unknown ids, repeated results, deaths between a slot's
+    own messages) with window mode on; task counts vary so ticks alternate between
+    window ticks, fallbacks (a fill level above 0, unserved fronts) and general ticks
+    that read a window holding tombstones."""
+    W = [300, 1000, 3000][seed % 3]
+    scen = synth.random_scenario(9000 + seed, W=W, n_ticks=10, max_events=[50, 400, 1500][(seed // 3) % 3],
+                                 max_new=[40, 150, 600, 4000][(seed // 9) % 3 + (seed % 2)])
+    st = dict(reg=scen["init_reg"], free=scen["init_free"], hb=scen["init_hb"], epoch=scen["init_epoch"],
+              queue=scen["init_queue"], log=scen["init_log"])
+    g, o = _pair(st, 2 * len(scen["init_log"]) + 60000, max_events=4096)
+    carried = 0
+    for t, tk in enumerate(scen["ticks"]):
+        log = o.export()["log"]
+        seq = np.full(len(tk["ev_kind"]), -1, np.int64)
+        for i in np.nonzero(tk["ev_kind"] == synth.EV_RESULT)[0]:
+            mine = np.nonzero(log == tk["ev_slot"][i])[0]
+            if len(mine) and tk["ev_pick"][i] % 5 != 4:
+                seq[i] = mine[tk["ev_pick"][i] % len(mine)]
+        n = carried + tk["n_new"]
+        args = (tk["now"], scen["tte"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], seq, n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp(g, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    g.close()
+
+
+def test_window_relaunch_without_commit_is_identical():
+    """A window tick reads only committed state: relaunched uncommitted it computes the
+    same assignments, orphans and evicted slots; committed once, the state matches."""
+    st, ticks = _stream(5, 8192, 1024, 1.0, n_ticks=3)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g, o = _pair(st, 2 * len(st["log"]) + 8 * 1024 + 16, max_events=E, purge_mode=2)
+    carried = 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        outs = [g.tick(*args, commit=False) for _ in range(2)]
+        for k in ("assign", "orphans", "evicted", "reconnect"):
+            np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg="tick %d %s" % (t, k))
+        g.commit()
+        b = o.tick(*args)
+        _cmp(g, o, outs[1], b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert g.window_stats()[0] >= 2
+
+
+def test_window_device_view_is_dense():
+    """The device view of a window context is the dense LRU queue (the window is
+    rewritten from position 0 first), and ticks continue from it."""
+    st, ticks = _stream(6, 4096, 256, 2.0, n_ticks=4)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g, o = _pair(st, 2 * len(st["log"]) + 8 * 256 + 16, max_events=E, purge_mode=2)
+    carried = 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp(g, o, a, b, t)
+        v = g.device_view()
+        assert v.queue_len == len(o.export()["queue"])
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert g.window_stats()[0] >= 2
+
+
+def test_window_off_and_auto_agree():
+    """The same stream with window ticks off, forced on and in auto mode (contexts of
+    <= 128K workers: off): identical outputs."""
+    st, ticks = _stream(7, 8192, 512, 1.0, n_ticks=5)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    res = []
+    for mode in (0, 1, -1):
+        g = GpuBalancer(8192, 2 * len(st["log"]) + 6 * 512 + 16, max_events=E)
+        g.set_window(mode)
+        g.load(st)
+        carried, outs = 0, []
+        for tk in ticks:
+            n = carried + tk["n_new"]
+            a = g.tick(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+            outs.append(a)
+            carried = n + len(a["orphans"]) - len(a["assign"])
+        res.append((outs, g.read_state(), g.window_stats()))
+        g.close()
+    assert res[0][2][0] == 0 and res[1][2][0] >= 3 and res[2][2][0] == 0
+    for outs, sg, _ in res[1:]:
+        for a, b in zip(res[0][0], outs):
+            for k in ("assign", "orphans", "evicted", "reconnect"):
+                np.testing.assert_array_equal(a[k], b[k])
+        for k in ("queue", "reg", "log"):
+            np.testing.assert_array_equal(res[0][1][k], sg[k])
