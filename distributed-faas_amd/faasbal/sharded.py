@@ -279,12 +279,153 @@ def _settle(bal, op, outs):
     return bad
 
 
+# DistShardGroup's wire format per call: a fixed header tensor broadcast from rank 0
+# (operation, event count, tasks, clock), then for ticks / purges the event batch packed
+# into one byte tensor (25 B per message), and back a fixed header per rank (all
+# gathered: every rank commits only when all succeeded) plus one padded byte tensor
+# per rank gathered to rank 0 (tasks, slots, orphans, evicted).  Loads and state reads
+# (not per tick) and failure messages travel as pickled objects.
+_OP_CODES = {"tick": 1, "purge": 2, "load": 3, "read": 4, "stop": 5}
+_OP_NAMES = {v: k for k, v in _OP_CODES.items()}
+_HDR = 8  # int64 words of the call header / the per-rank result header
+
+
+def _dev(dist):
+    import torch
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def _pack_events(kw):
+    k = np.ascontiguousarray(kw["ev_kind"], np.uint8)
+    parts = [k.view(np.uint8), np.ascontiguousarray(kw["ev_slot"], np.int32).view(np.uint8),
+             np.ascontiguousarray(kw["ev_val"], np.int32).view(np.uint8),
+             np.ascontiguousarray(kw["ev_ts"], np.float64).view(np.uint8),
+             np.ascontiguousarray(kw["ev_seq"], np.int64).view(np.uint8)]
+    return np.concatenate(parts) if len(k) else np.zeros(0, np.uint8)
+
+
+def _unpack_events(buf, E):
+    o = [0, E, 5 * E, 9 * E, 17 * E, 25 * E]
+    return dict(ev_kind=buf[o[0]:o[1]].copy(), ev_slot=buf[o[1]:o[2]].view(np.int32).copy(),
+                ev_val=buf[o[2]:o[3]].view(np.int32).copy(), ev_ts=buf[o[3]:o[4]].view(np.float64).copy(),
+                ev_seq=buf[o[4]:o[5]].view(np.int64).copy())
+
+
+def _bcast_call(dist, dev, op, kw):
+    """Rank 0: the call to every rank.  Returns nothing; the ranks read it with _recv_call."""
+    import torch
+    h = torch.zeros(_HDR, dtype=torch.int64)
+    h[0] = _OP_CODES[op]
+    if op in ("tick", "purge"):
+        E = len(kw.get("ev_kind", ())) if op == "tick" else 0
+        h[1] = E
+        h[2] = int(kw.get("n_pending", 0))
+        h[3] = int(np.float64(kw["now"]).view(np.int64))
+        h[4] = int(np.float64(kw["tte"]).view(np.int64))
+    dist.broadcast(h.to(dev), src=0)
+    if op in ("tick", "purge"):
+        if int(h[1]):
+            dist.broadcast(torch.from_numpy(_pack_events(kw)).to(dev), src=0)
+    elif op != "stop":
+        dist.broadcast_object_list([kw], src=0)
+
+
+def _recv_call(dist, dev):
+    """Ranks > 0: the next call of rank 0 as (op, kw)."""
+    import torch
+    h = torch.zeros(_HDR, dtype=torch.int64, device=dev)
+    dist.broadcast(h, src=0)
+    h = h.cpu().numpy()
+    op = _OP_NAMES[int(h[0])]
+    if op not in ("tick", "purge"):
+        if op == "stop":
+            return op, {}
+        box = [None]
+        dist.broadcast_object_list(box, src=0)
+        return op, box[0]
+    E = int(h[1])
+    kw = dict(now=float(h[3:4].view(np.float64)[0]), tte=float(h[4:5].view(np.float64)[0]), n_pending=int(h[2]))
+    if op == "tick":
+        if E:
+            buf = torch.empty(25 * E, dtype=torch.uint8, device=dev)
+            dist.broadcast(buf, src=0)
+            kw.update(_unpack_events(buf.cpu().numpy(), E))
+        else:
+            z = np.zeros(0)
+            kw.update(ev_kind=z.astype(np.uint8), ev_slot=z.astype(np.int32), ev_val=z.astype(np.int32),
+                      ev_ts=z.astype(np.float64), ev_seq=z.astype(np.int64))
+    return op, kw
+
+
+def _gather_results(dist, dev, op, guarded):
+    """Every rank: its guarded result of a tick / purge.  Returns, on every rank, the
+    list of (ok, value | (code, message)) in rank order -- values complete on rank 0
+    (the other ranks get headers only, enough to settle the commit)."""
+    import torch
+    ok, val = guarded
+    rank, world = dist.get_rank(), dist.get_world_size()
+    h = torch.zeros(_HDR, dtype=torch.int64)
+    payload = np.zeros(0, np.uint8)
+    if ok:
+        r = val["result"]
+        task = np.asarray(val.get("task", np.zeros(0)), np.int64)
+        slot = np.asarray(val.get("slot", np.zeros(0)), np.int32)
+        orph = np.asarray(val["orphans"], np.int64)
+        evic = np.asarray(val["evicted"], np.int32)
+        h[0] = 1
+        h[2], h[3], h[4] = int(r.get("n_local", 0)), int(r.get("n_orphans_local", 0)), int(r["n_evicted"])
+        h[5], h[6], h[7] = len(task), len(orph), len(evic)
+        if rank != 0:
+            payload = np.concatenate([task.view(np.uint8), slot.view(np.uint8), orph.view(np.uint8),
+                                      evic.view(np.uint8)])
+    else:
+        h[1] = val[0] if val[0] is not None else 0
+    hs = [torch.zeros(_HDR, dtype=torch.int64, device=dev) for _ in range(world)]
+    dist.all_gather(hs, h.to(dev))
+    hs = [x.cpu().numpy() for x in hs]
+    if not all(x[0] for x in hs):
+        # a rank failed: its message (pickled: failures only)
+        msgs = [None] * world
+        dist.all_gather_object(msgs, None if ok else val)
+        return [(bool(x[0]), None if x[0] else msgs[i]) for i, x in enumerate(hs)]
+    nbytes = [int(x[5]) * 12 + int(x[6]) * 8 + int(x[7]) * 4 for x in hs]
+    mx = max(nbytes[1:], default=0)
+    outs = [(True, val if rank == 0 else None)] + [(True, None)] * (world - 1)
+    if world > 1 and mx > 0:
+        mine = torch.zeros(mx, dtype=torch.uint8)
+        if rank != 0:
+            mine[:len(payload)] = torch.from_numpy(payload)
+        bufs = [torch.zeros(mx, dtype=torch.uint8, device=dev) for _ in range(world)] if rank == 0 else None
+        dist.gather(mine.to(dev), bufs, dst=0)
+        if rank == 0:
+            for i in range(1, world):
+                b = bufs[i].cpu().numpy()
+                nt, no, ne = int(hs[i][5]), int(hs[i][6]), int(hs[i][7])
+                o = [0, 8 * nt, 12 * nt, 12 * nt + 8 * no, 12 * nt + 8 * no + 4 * ne]
+                res = dict(n_local=int(hs[i][2]), n_orphans_local=int(hs[i][3]), n_evicted=int(hs[i][4]))
+                d = dict(result=res, orphans=b[o[2]:o[3]].view(np.int64).copy(),
+                         evicted=b[o[3]:o[4]].view(np.int32).copy(), reconnect=None)
+                if op == "tick":
+                    d.update(task=b[o[0]:o[1]].view(np.int64).copy(), slot=b[o[1]:o[2]].view(np.int32).copy())
+                outs[i] = (True, d)
+    elif rank == 0:
+        for i in range(1, world):
+            res = dict(n_local=int(hs[i][2]), n_orphans_local=int(hs[i][3]), n_evicted=int(hs[i][4]))
+            d = dict(result=res, orphans=np.zeros(0, np.int64), evicted=np.zeros(0, np.int32), reconnect=None)
+            if op == "tick":
+                d.update(task=np.zeros(0, np.int64), slot=np.zeros(0, np.int32))
+            outs[i] = (True, d)
+    return outs
+
+
 class DistShardGroup(ShardGroup):
     """Rank 0's view of a table sharded over a torch.distributed group (one process
     per GPU): every call is broadcast to the ranks (serve_shard() runs on the
     others), each rank runs it on its own shard -- ticks with the exchange
     all-reduce over the group's backend (RCCL over xGMI for ``nccl``) -- and the
-    per-rank results come back through one all_gather_object."""
+    per-rank results come back to rank 0.  Ticks and purges travel as tensors (the
+    event batch in one broadcast, the results in one gather); loads and state reads
+    as pickled objects."""
 
     def __init__(self, balancer, n_workers):
         super().__init__(n_workers)
@@ -292,11 +433,16 @@ class DistShardGroup(ShardGroup):
         self.dist, self.bal = dist, balancer
         if dist.get_rank() != 0:
             raise FaasbalError(_lib.FB_ESTATE, "DistShardGroup lives on rank 0; run serve_shard() on the others")
+        self.dev = _dev(dist)
 
     def _each(self, op, **kw):
-        self.dist.broadcast_object_list([(op, kw)], src=0)
-        outs = [None] * self.dist.get_world_size()
-        self.dist.all_gather_object(outs, _serve_guarded(self.bal, op, kw))
+        _bcast_call(self.dist, self.dev, op, kw)
+        guarded = _serve_guarded(self.bal, op, kw)
+        if op in ("tick", "purge"):
+            outs = _gather_results(self.dist, self.dev, op, guarded)
+        else:
+            outs = [None] * self.dist.get_world_size()
+            self.dist.all_gather_object(outs, guarded)
         bad = _settle(self.bal, op, outs)
         if bad is not None:
             code, msg = bad
@@ -306,20 +452,23 @@ class DistShardGroup(ShardGroup):
         return [o[1] for o in outs]
 
     def close(self):
-        self.dist.broadcast_object_list([("stop", {})], src=0)
+        _bcast_call(self.dist, self.dev, "stop", {})
 
 
 def serve_shard(balancer):
     """Rank r > 0 of a DistShardGroup: run rank 0's calls on this shard until it stops."""
     import torch.distributed as dist
+    dev = _dev(dist)
     while True:
-        box = [None]
-        dist.broadcast_object_list(box, src=0)
-        op, kw = box[0]
+        op, kw = _recv_call(dist, dev)
         if op == "stop":
             return
-        outs = [None] * dist.get_world_size()
-        dist.all_gather_object(outs, _serve_guarded(balancer, op, kw))
+        guarded = _serve_guarded(balancer, op, kw)
+        if op in ("tick", "purge"):
+            outs = _gather_results(dist, dev, op, guarded)
+        else:
+            outs = [None] * dist.get_world_size()
+            dist.all_gather_object(outs, guarded)
         _settle(balancer, op, outs)  # rank 0 raises a failure; this rank keeps serving
 
 
