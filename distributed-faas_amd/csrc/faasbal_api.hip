@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
@@ -138,8 +139,11 @@ struct fb_ctx {
     int l_nchW = 0;            // ... and the window chunks it scans
     int64_t l_qoff = 0;
     int32_t *pos_of[2] = {nullptr, nullptr};
-    int2 *wnpos = nullptr;
-    int4 *wagg = nullptr;
+    // k_emit_win: per front / back list entry, the committed position of the queued slot it
+    // moved (-1: none), read by the tick's commit
+    int32_t *tomb = nullptr;
+    unsigned long long *wlb = nullptr;  // k_emit_win's look-back granules
+    uint32_t *wticket = nullptr;
     uint32_t *lpart = nullptr, *wpart = nullptr;
     int64_t win_slack = 8192;  // window positions scanned beyond the tasks' estimate (grows on a miss)
     int64_t last_O = 0;
@@ -203,7 +207,10 @@ struct fb_ctx {
     bool staged = false;       // fb_tick_stage done, fb_tick_launch_staged not yet
     int32_t st_E = 0, st_vmax = 0;
     double st_now = 0.0;
-    HostPool *pool = nullptr;  // staging workers (FAASBAL_STAGE_THREADS, default 4; 1 = none)
+    HostPool *pool = nullptr;  // staging workers (FAASBAL_STAGE_THREADS, default 8; 1 = none)
+    int stage_prof = 0;        // FAASBAL_STAGE_PROF=1: fb_tick_stage's time split to stderr
+    double sprof[4] = {0, 0, 0, 0};
+    int sprof_n = 0;
     // scan / plan / emit
     int32_t *c_arr = nullptr, *qbmax = nullptr, *qbm_raw = nullptr;
     unsigned long long *csum = nullptr;
@@ -542,8 +549,9 @@ int win_alloc(fb_ctx *c) {
     const size_t W = (size_t)c->W_cap, E = (size_t)c->E_cap, Wq = (size_t)c->Wq_cap;
     const size_t qcap = 2 * Wq + 2 * E + 4096;
     auto r256 = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    const size_t bytes = 2 * (r256(qcap * 4) * 2 + r256(qcap * 8) + r256(W * 4)) + r256(W * 8) + r256(kWinMaxCh * 16) +
-                         r256(1024 * 4) + r256(64 * 32 * 4);
+    const size_t bytes = 2 * (r256(qcap * 4) * 2 + r256(qcap * 8) + r256(W * 4)) + r256(2 * E * 4) +
+                         r256(kWinMaxCh * 8) +
+                         r256(256) + r256(1024 * 4) + r256(64 * 32 * 4);
     void *m = nullptr;
     hipError_t e = hipMalloc(&m, bytes);
     if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(window buffers %zu B) failed: %s", bytes, hipGetErrorString(e));
@@ -558,8 +566,9 @@ int win_alloc(fb_ctx *c) {
         nh[i] = (double *)take(qcap * 8);
         c->pos_of[i] = (int32_t *)take(W * 4);
     }
-    c->wnpos = (int2 *)take(W * 8);
-    c->wagg = (int4 *)take(kWinMaxCh * 16);
+    c->tomb = (int32_t *)take(2 * E * 4);
+    c->wlb = (unsigned long long *)take(kWinMaxCh * 8);
+    c->wticket = (uint32_t *)take(256);
     c->lpart = (uint32_t *)take(1024 * 4);
     c->wpart = (uint32_t *)take(64 * 32 * 4);
     const int k = c->qcur;
@@ -615,6 +624,7 @@ bool win_plan(fb_ctx *c) {
     const int64_t scan = std::min<int64_t>(c->Qn, want);
     if (mode < 0 && scan * 2 > c->Qn) return false;  // auto: only when most of the queue stays put
     const int nchW = (int)cdiv(scan, kWinCh);
+    if (nchW == 0) return false;
     if ((size_t)((c->W + 63) / 64 + 2) * 8 > (size_t)c->max_lds) return false;  // k_logscan's bitmap in LDS
     const int nchB = (int)cdiv(c->l_E, kWinCh);
     if (2 * nchB + nchW > kWinMaxCh) return false;
@@ -791,6 +801,11 @@ int enqueue_tick(fb_ctx *c) {
         ea.free_out = c->free_[nxt];
         ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep || a.f_emit || c->l_win)) ? c->dmask : nullptr;
         ea.wpart = c->l_win ? c->wpart : nullptr;
+        if (c->l_win) {  // k_emit_win's look-back granules and ticket start from zero
+            ea.wlb = c->wlb;
+            ea.wlb_n = 2 * (int)cdiv(E, kWinCh) + c->l_nchW;
+            ea.wticket = c->wticket;
+        }
         ea.wcnt = c->wcnt;
         ea.grp = a.grp_on ? a.grp : nullptr;
         ea.ngrp = a.ngrp;
@@ -1013,18 +1028,18 @@ int enqueue_tick(fb_ctx *c) {
         a.nchB = (int)cdiv(E, kWinCh);
         a.nchF = a.nchB;
         a.nchW = c->l_nchW;
-        a.wagg = c->wagg;
+        a.wlb = c->wlb;
+        a.wticket = c->wticket;
         a.wpart = c->wpart;
-        a.wnpos = c->wnpos;
+        a.pos_in = c->pos_of[qc];
+        a.tomb = c->tomb;
         a.lstamp = c->lstamp;
         const int nch = a.nchB + a.nchF + a.nchW;
-        a.ls_cnt_blocks = (int)cdiv(nch, kLsBS / 64);
-        a.ls_log_blocks = head > 0 ? std::max(1, std::min(c->ncu - a.ls_cnt_blocks, (int)cdiv(nbf, kLsBS / 64))) : 0;
         a.lpart = c->lpart;
-        a.n_lpart = a.ls_log_blocks;
-        {
+        a.n_lpart = head > 0 ? ls_grid : 0;
+        if (head > 0) {
             Timer t(c, "logscan");
-            launch_logscan(a, a.ls_cnt_blocks + a.ls_log_blocks, t.st());
+            launch_logscan(a, ls_grid, t.st());
         }
         {
             Timer t(c, "emit");
@@ -1158,8 +1173,9 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         if (c->win_cap) ap.add(&c->pos_of[i], W);
     }
     if (c->win_cap) {
-        ap.add(&c->wnpos, W);
-        ap.add(&c->wagg, (size_t)kWinMaxCh);
+        ap.add(&c->tomb, 2 * E);
+        ap.add(&c->wlb, (size_t)kWinMaxCh);
+        ap.add(&c->wticket, (size_t)64);
         ap.add(&c->lpart, (size_t)1024);
         ap.add(&c->wpart, (size_t)64 * 32);
     }
@@ -1252,6 +1268,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->ctag, F);
         ap.add(&c->orph_dense, F);
     }
+    // window ticks leave their orphans in per-tile segments too (gathered when read)
+    if (c->win_cap && !(!shard && !c->deque && W <= (size_t)kLdsBitmapSlots)) ap.add(&c->orph_dense, F);
     if (shard) {
         ap.add(&c->lseq, F);
         ap.add(&c->ocnt, tab);
@@ -1283,6 +1301,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_CQ_DIRECT")) c->cq_direct = atoi(getenv("FAASBAL_CQ_DIRECT"));
     if (!rc && getenv("FAASBAL_F_EMIT")) c->f_emit = atoi(getenv("FAASBAL_F_EMIT"));
     if (!rc && getenv("FAASBAL_WINDOW")) c->win = atoi(getenv("FAASBAL_WINDOW"));
+    if (!rc) c->stage_prof = getenv_int("FAASBAL_STAGE_PROF");
     if (!rc) {
         c->scan_ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
         c->post_eager = getenv_int("FAASBAL_POST_EAGER");
@@ -1306,7 +1325,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && getenv("FAASBAL_FORK")) c->fork = atoi(getenv("FAASBAL_FORK"));
     if (!rc && getenv("FAASBAL_D2H_KERNEL")) c->d2h_kernel = atoi(getenv("FAASBAL_D2H_KERNEL"));
     if (!rc) {
-        int nt = getenv("FAASBAL_STAGE_THREADS") ? atoi(getenv("FAASBAL_STAGE_THREADS")) : 4;
+        int nt = getenv("FAASBAL_STAGE_THREADS") ? atoi(getenv("FAASBAL_STAGE_THREADS")) : 8;
         nt = std::max(1, std::min(nt, 16));
         if (nt > 1 && E >= kStagePar) c->pool = new HostPool(nt);
     }
@@ -1691,6 +1710,24 @@ int fb_tick_continue(fb_ctx *c) {
     return enqueue_tick(c);
 }
 
+// H2D copies of a staged batch into device half `half` on the copy stream, after the
+// last tick that read that half; the launch waits for stage_ev[half].
+static int stage_copies(fb_ctx *c, int half, const void *sk, const void *ss, const void *sv, const void *st,
+                        const void *sq, int E) {
+    if (c->use_rec[half]) HIPCHK(c, hipStreamWaitEvent(c->cp_s, c->use_ev[half], 0));
+    HIPCHK(c, hipMemcpyAsync(c->evk[half], sk, E, hipMemcpyHostToDevice, c->cp_s));
+    HIPCHK(c, hipMemcpyAsync(c->evsl[half], ss, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
+    HIPCHK(c, hipMemcpyAsync(c->evv[half], sv, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
+    HIPCHK(c, hipMemcpyAsync(c->evt[half], st, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+    if (sq)
+        HIPCHK(c, hipMemcpyAsync(c->evq[half], sq, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
+    else
+        HIPCHK(c, hipMemsetAsync(c->evq[half], 0xff, (size_t)E * 8, c->cp_s));  // -1 for every event
+    HIPCHK(c, hipEventRecord(c->stage_ev[half], c->cp_s));
+    c->stage_rec[half] = true;
+    return FB_OK;
+}
+
 // Validate a tick's events and stage them into the pinned half the next launch
 // copies from.  Two halves: staging tick t+1 on the host overlaps tick t on the
 // device (the half's previous copies were enqueued two launches ago; its event
@@ -1712,6 +1749,8 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     // dispatcher that parses messages straight into them) the pass only validates, and
     // the H2D copies read the caller's arrays; they must stay unchanged until the tick
     // that uses them has been waited for.
+    using clk = std::chrono::steady_clock;
+    const auto tp0 = clk::now();
     bool direct = E > 0;
     if (direct) {
         const void *ptrs[5] = {kind, slot, val, ts, seq};
@@ -1724,6 +1763,15 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
             }
         }
     }
+    // pinned inputs: their H2D copies go out first and overlap the validation below (a
+    // batch that fails validation is never launched, so copying it first is harmless)
+    bool copied = false;
+    const auto tp1 = clk::now();
+    if (E && direct) {
+        if (int rc = stage_copies(c, half, kind, slot, val, ts, seq, E)) return rc;
+        copied = true;
+    }
+    const auto tp2 = clk::now();
     if (E) {
         const size_t ecap = (size_t)c->E_cap;
         char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
@@ -1779,29 +1827,25 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
                 return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
         }
     }
-    if (E) {
-        // H2D on the copy stream, after the last tick that read this device half
+    const auto tp3 = clk::now();
+    if (E && !copied) {
         const size_t ecap = (size_t)c->E_cap;
         char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
-        if (c->use_rec[half]) HIPCHK(c, hipStreamWaitEvent(c->cp_s, c->use_ev[half], 0));
-        const void *sk = h, *ss = h + ecap, *sv = h + ecap * 5, *st = h + ecap * 9, *sq = h + ecap * 17;
-        if (direct) {
-            sk = kind;
-            ss = slot;
-            sv = val;
-            st = ts;
-            sq = seq;
+        if (int rc = stage_copies(c, half, h, h + ecap, h + ecap * 5, h + ecap * 9, h + ecap * 17, E)) return rc;
+    }
+    if (c->stage_prof) {  // FAASBAL_STAGE_PROF=1: where fb_tick_stage's time goes (diagnostics)
+        const auto tp4 = clk::now();
+        auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+        c->sprof[0] += us(tp0, tp1);
+        c->sprof[1] += us(tp1, tp2);
+        c->sprof[2] += us(tp2, tp3);
+        c->sprof[3] += us(tp3, tp4);
+        if (++c->sprof_n == 16) {
+            fprintf(stderr, "fb_tick_stage us: pointer checks %.1f, copies %.1f, validation %.1f, copies (staged) %.1f\n",
+                    c->sprof[0] / 16, c->sprof[1] / 16, c->sprof[2] / 16, c->sprof[3] / 16);
+            c->sprof[0] = c->sprof[1] = c->sprof[2] = c->sprof[3] = 0;
+            c->sprof_n = 0;
         }
-        HIPCHK(c, hipMemcpyAsync(c->evk[half], sk, E, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evsl[half], ss, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evv[half], sv, (size_t)E * 4, hipMemcpyHostToDevice, c->cp_s));
-        HIPCHK(c, hipMemcpyAsync(c->evt[half], st, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
-        if (sq)
-            HIPCHK(c, hipMemcpyAsync(c->evq[half], sq, (size_t)E * 8, hipMemcpyHostToDevice, c->cp_s));
-        else
-            HIPCHK(c, hipMemsetAsync(c->evq[half], 0xff, (size_t)E * 8, c->cp_s));  // -1 for every event
-        HIPCHK(c, hipEventRecord(c->stage_ev[half], c->cp_s));
-        c->stage_rec[half] = true;
     }
     c->staged = true;
     c->st_E = E;
@@ -1979,9 +2023,10 @@ int fb_tick_commit(fb_ctx *c) {
         a.head_local = c->l_head_local;
         a.shard = c->shard;
         a.nbo = (int)cdiv(n_orph, kBS);
-        if (c->l_oseg && n_orph > 0) {  // per-tile segments: one block per log tile
+        if (c->l_oseg && n_orph > 0) {  // per-tile segments: a wave per 64 log tiles
             a.oseg = c->fcnt;
-            a.nbo = c->l_nbf;
+            a.oseg_tiles = c->l_nbf;
+            a.nbo = (int)cdiv(c->l_nbf, 64 * kWaves);
         }
         a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
         a.ev_clr = c->ev_clr;
@@ -2000,12 +2045,12 @@ int fb_tick_commit(fb_ctx *c) {
             a.wqf = c->qfree[c->qcur];
             a.wqh = c->qhb[c->qcur];
             a.pos = c->pos_of[c->qcur];
-            a.wnpos = c->wnpos;
-            a.wstamp = c->lstamp;
+            a.tomb = c->tomb;
+            a.n_tomb = 2 * c->l_E;
             a.post_rf = c->post_rf;
         }
-        const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + a.nbap;
-        if (c->ev_head && c->ev_ll && !c->commit_now) {
+        const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) : 0);
+        if (c->ev_head && c->ev_ll && !c->commit_now && !c->l_win) {  // (a window tick's commit runs at once)
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
             c->cm_grid = grid;

@@ -48,15 +48,17 @@ constexpr int kQsKeep = 0, kQsOut = 1, kQsFront = 2, kQsBack = 3;
 // slot's in-flight entries (ctag[q] == the launch stamp names which); the log itself is
 // cleared only by the commit, so an orphan test of that slot's entries checks ctag
 constexpr uint8_t kRfCleared = 16;
+// post_rf bit 5: the slot was in the committed queue at tick start (window ticks: a front /
+// back insertion of such a slot leaves a position to tombstone)
+constexpr uint8_t kRfQ0 = 32;
 // k_emit2's log tiles (one-GPU fused ticks): at most this many log workgroups (4 tiles
 // of kFTile entries each; k_orph_gather sums up to 4 x this many tile counts per block)
 constexpr int kFEmitMaxBlocks = 1024;
 // window ticks (sliding level-0 queue, one GPU): 1024-element chunks of the
-// virtual order [backs][fronts][window prefix], counted by k_logscan's count waves (one
-// wave per chunk) and emitted by k_emit_win (one workgroup per chunk, which reads every
-// chunk's counts: at most kWinMaxCh of them)
+// virtual order [backs][fronts][window prefix], one k_emit_win workgroup each (at most
+// kWinMaxCh: the look-back granules hold 22-bit prefixes)
 constexpr int kWinCh = 1024;
-constexpr int kWinMaxCh = 2048;
+constexpr int kWinMaxCh = 4096;
 constexpr int32_t kTomb = INT32_MIN;  // qfree of a window position whose slot left the queue
 // st bit: the slot was in the committed queue at tick start (window commits)
 constexpr uint8_t kStQ0 = 8;
@@ -116,7 +118,8 @@ struct CommitArgs {
     int32_t *bud;              // one-GPU heartbeat: touched slots get bud_next[s] (budget after the tick)
     const int32_t *bud_next;
     const uint32_t *oseg;  // non-null: orphans in per-tile segments (orphans[t*2048 + i], i < oseg[t]),
-                           // blocks [nbw, nbw + nbo) one per tile
+                           // blocks [nbw, nbw + nbo) a wave per 64 of the oseg_tiles tiles
+    int oseg_tiles;
     int nbo;            // ... then blocks [nbw + nbo, + ceil(n_clr / 256)) clear the entries the
     int n_clr;          // committed tick's results completed: log_slot[ev_clr[e]] = -1, e < n_clr
     const int32_t *ev_clr;
@@ -137,18 +140,18 @@ struct CommitArgs {
     int shard;
     // window ticks: the committed window keeps [wq_head, wq_tail) of the queue
     // buffer; per slot that was queued at tick start (st & kStQ0) and sits there, its
-    // position is tombstoned when the slot died or its messages moved it, refreshed with the
-    // post-message free count / heartbeat when they kept it; a touched slot the tick
-    // appended takes its new position from wnpos (tagged with the launch stamp), the
-    // untouched appended ones from the nbap blocks walking [wq_tail, wq_tail + napp)
+    // position is tombstoned when the slot died or its messages took it out of the queue,
+    // refreshed with the post-message free count / heartbeat when they kept it; the nbap
+    // blocks walking [wq_tail, wq_tail + napp) give every appended slot its position, the
+    // blocks after them tombstone the positions in k_emit_win's tomb list (n_tomb entries)
     int win;
     int64_t wq_head, wq_tail, napp;
-    int nbap;
+    int nbap;                  // blocks over the appended positions, then over the tomb list
     int32_t *wq_buf, *wqf;
     double *wqh;
     int32_t *pos;
-    const int2 *wnpos;
-    uint32_t wstamp;
+    const int32_t *tomb;       // committed positions of queued slots moved to the front / back
+    int n_tomb;                // entries of tomb (-1: nothing to tombstone)
     const uint8_t *post_rf;
 };
 
@@ -220,6 +223,9 @@ struct EvArgs {
     // window ticks: evictions and live queued slots as 64 partials (128-byte lines, word 0 /
     // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
     uint32_t *wpart;
+    unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
+    int wlb_n;                  // zeroed here
+    uint32_t *wticket;
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -303,21 +309,23 @@ struct TickArgs {
     int32_t *log_slot;
     // ---- window ticks (one GPU, heartbeat loop, level 0).  The committed queue
     // is the window [wq_off, wq_tail) of a buffer of wq_cap entries (qfree kTomb: a position
-    // whose slot left); k_logscan's count waves count 1024-element chunks of [backs][fronts]
-    // [window prefix] (wagg), k_emit_win serves the first N live elements (fronts, then the
-    // window), appends the live backs and then the served workers with c > 1 at the tail
+    // whose slot left); k_emit_win takes 1024-element chunks of [backs][fronts][window
+    // prefix], serves the first N live elements (fronts, then the window), appends the live
+    // backs and then the served workers with c > 1 at the tail
     int win;
     int64_t wq_off, wq_tail, wq_cap;
     int32_t *wq_buf, *wqf_buf;
     double *wqh_buf;
     int nchB, nchF, nchW;
-    int4 *wagg;                  // per chunk {live fronts / window, of them c > 1, live backs, max c}
+    unsigned long long *wlb;     // look-back granules: [0, nchB) the back chain, then the front / window chain
+    uint32_t *wticket;           // chunk tickets (zeroed by k_ev_link)
     uint32_t *lpart;             // k_logscan: orphans per log workgroup
     int n_lpart;
     uint32_t *wpart;             // evictions / live queued slots, 64 partials (EvArgs::wpart)
-    int2 *wnpos;                 // touched slots appended: {position, launch stamp}
+    const int32_t *pos_in;       // committed position of each queued slot
+    int32_t *tomb;               // per back / front list entry: the committed position of a queued slot
+                                 // it moved (-1: none), 2 E entries
     int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
-    int ls_cnt_blocks, ls_log_blocks;  // k_logscan grid: count workgroups first, then log workgroups
     int32_t *pos_out;            // general ticks of window contexts: next-queue position per slot
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
     int32_t *rb_slot;   // compact assignments (null: off): slot per LRU position, -1 none

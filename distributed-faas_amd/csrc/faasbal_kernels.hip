@@ -741,7 +741,7 @@ struct SlotRun {
     __device__ __forceinline__ bool purge(const EvArgs &a, uint32_t s, int reg0, bool &evicted);
     __device__ __forceinline__ void finish(const EvArgs &a, uint32_t s, uint32_t gs) {
         a.post[s] = PostRec{hb, fr, epoch};
-        a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1) | (ncl ? kRfCleared : 0));
+        a.post_rf[s] = (uint8_t)(reg | ((died_start | (qstat << 1)) << 1) | (ncl ? kRfCleared : 0) | (q0 ? kRfQ0 : 0));
         if (a.defer_clr) a.post_infl[s] = infl0 - ncl;
         if (a.tbits) atomicOr(&a.tbits[s >> 5], 1u << (s & 31));  // the bitmap is the stamp
         else a.touched[s] = a.tick;
@@ -789,13 +789,20 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
     const int nclr = (a.n_clr + kBS - 1) / kBS;
     if (a.win && blk >= a.nbw + a.nbo + nclr) {
-        // window tick: positions the tick appended take their slots' pos (the touched ones
-        // take theirs from wnpos in the slot sweep)
-        const int64_t i = (int64_t)(blk - a.nbw - a.nbo - nclr) * kBS + threadIdx.x;
-        if (i >= a.napp) return;
-        const int64_t p = a.wq_tail + i;
-        const int s = a.wq_buf[p];
-        if (!(a.E > 0 && got_msg(a, s))) a.pos[s] = (int32_t)p;
+        const int rb = blk - a.nbw - a.nbo - nclr;
+        if (rb < a.nbap) {
+            // window tick: the slot at each appended position has its position there
+            const int64_t i = (int64_t)rb * kBS + threadIdx.x;
+            if (i < a.napp) a.pos[a.wq_buf[a.wq_tail + i]] = (int32_t)(a.wq_tail + i);
+            return;
+        }
+        // the committed positions of queued slots a front / back insertion moved (recorded
+        // by k_emit_win per list entry, before any position changed) become tombstones
+        const int64_t j = (int64_t)(rb - a.nbap) * kBS + threadIdx.x;
+        if (j < a.n_tomb) {
+            const int32_t p = a.tomb[j];
+            if (p >= a.wq_head && p < a.wq_tail) a.wqf[p] = kTomb;
+        }
         return;
     }
     if (blk >= a.nbw + a.nbo) {
@@ -808,10 +815,21 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
         return;
     }
     if (blk >= a.nbw && a.oseg) {
-        // orphans in per-tile segments (fused one-GPU tick): one block per tile
-        const int t = blk - a.nbw;
-        const uint32_t n = a.oseg[t];
-        for (uint32_t i = threadIdx.x; i < n; i += kBS) a.log_slot[a.orphans[(int64_t)t * kFTile + i]] = -1;
+        // orphans in per-tile segments (fused one-GPU and window ticks): a wave per 64 tiles
+        // (one count load each), then the tiles that hold orphans one after another
+        // lane per tile: each lane clears its tile's orphans (window ticks leave about one
+        // per tile, so one load round and one store round for the whole wave)
+        const int t = ((blk - a.nbw) * kWaves + wave_id()) * 64 + lane_id();
+        const uint32_t n = t < a.oseg_tiles ? a.oseg[t] : 0u;
+        const int64_t *src = a.orphans + (int64_t)t * kFTile;
+        for (uint32_t i = 0; i < n; i += 4) {
+            int64_t q[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) q[k] = src[i + k < n ? i + k : i];
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                if (i + k < n) a.log_slot[q[k]] = -1;
+        }
         return;
     }
     if (blk >= a.nbw) {
@@ -829,26 +847,26 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
     const uint8_t stt = a.st[s];
     if (a.win) {
         // window tick: the committed position of a slot queued at tick start that the tick
-        // did not serve -- tombstoned when the slot died or its messages moved it, else
-        // refreshed with its post-message free count and heartbeat if it got messages
+        // did not serve -- tombstoned when the slot died or its messages took it out of the
+        // queue, refreshed with its post-message free count and heartbeat when they kept it
+        // there (a queued slot that lives on untouched keeps its position as it is).  Slots
+        // moved to the front or the back were recorded by k_emit_win (the tomb list above):
+        // they may also be appended, so their pos is rewritten in this launch.
         const bool t = a.E > 0 && got_msg(a, s);
-        if (stt & kStQ0) {
-            const int32_t p = a.pos[s];
-            const bool inw = p >= a.wq_head && p < a.wq_tail;
-            if (inw && a.wq_buf[inw ? p : 0] == s) {
-                const bool moved = t && ((a.post_rf[s] >> 2) & 3) != kQsKeep;
-                if (!(stt & kStAlive) || moved) {
-                    a.wqf[p] = kTomb;
-                } else if (t) {
-                    const PostRec pr = a.post[s];
-                    a.wqf[p] = pr.free;
-                    a.wqh[p] = pr.hb;
+        if ((stt & kStQ0) && (t || !(stt & kStAlive))) {
+            const int qs = t ? (a.post_rf[s] >> 2) & 3 : kQsKeep;
+            if (!(stt & kStAlive) || qs == kQsOut || qs == kQsKeep) {
+                const int32_t p = a.pos[s];  // exact for a queued slot
+                if (p >= a.wq_head && p < a.wq_tail) {
+                    if (!(stt & kStAlive) || qs == kQsOut) {
+                        a.wqf[p] = kTomb;
+                    } else {
+                        const PostRec pr = a.post[s];
+                        a.wqf[p] = pr.free;
+                        a.wqh[p] = pr.hb;
+                    }
                 }
             }
-        }
-        if (t) {
-            const int2 np = a.wnpos[s];
-            if ((uint32_t)np.y == a.wstamp) a.pos[s] = np.x;
         }
     }
     // committed hb is NaN for slots without a record (k_scan's log role relies on it)
@@ -893,8 +911,11 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
         a.hout->resort = 0;
         a.hout->win_ovf = 0;
     }
-    // window ticks: the purge's partial counts (words 0 and 1 of 64 lines)
+    // window ticks: the purge's partial counts (words 0 and 1 of 64 lines), k_emit_win's
+    // look-back granules and its ticket
     if (a.wpart && t < 128) a.wpart[(t >> 1) * 32 + (t & 1)] = 0u;
+    for (int i = t; i < a.wlb_n; i += nt) a.wlb[i] = 0ull;
+    if (a.wlb_n && t == 0) *a.wticket = 0u;
     for (int w = t; w < a.tbits_words; w += nt) a.tbits[w] = 0u;
     // the counters k_ev_apply_ll's slot purge accumulates with atomics
     for (int w = t; w < a.nbw; w += nt) a.wcnt[w] = 0u;
@@ -1747,12 +1768,13 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
 // the tick touches only the window's served prefix: the suffix stays where it is, the
 // live backs and then the served workers with c > 1 are appended at the window's tail.
 // The elements are numbered in the order [backs][fronts][window]: 1024-element chunks,
-// counted by k_logscan's count waves, emitted by k_emit_win.
+// one k_emit_win workgroup each.
 struct WinEl {
     int s;        // slot, -1: a hole of a list
     int32_t raw;  // free count of a live queued position, INT32_MIN otherwise
     double hb;
     bool t;       // the slot got messages this tick
+    int32_t mv;   // list entries: the committed position the slot left (-1: it was not queued)
 };
 // region of chunk ch: 0 backs, 1 fronts, 2 window; [i0, i1) its element range in the region
 __device__ __forceinline__ int win_region(const TickArgs &a, int ch, int64_t &i0, int64_t &i1) {
@@ -1784,10 +1806,13 @@ __device__ __forceinline__ WinEl win_elem(const TickArgs &a, int reg, int64_t i,
         const int sc = s1 > 0 ? s1 - 1 : 0;
         const int32_t fr = a.free_out[sc].x;
         const double h = a.post[sc].hb;
+        const uint8_t rf = a.post_rf[sc];
+        const int32_t p0 = a.pos_in[sc];
         e.s = s1 - 1;
         e.raw = (in && s1 > 0) ? fr : INT32_MIN;
         e.hb = h;
         e.t = true;
+        e.mv = (s1 > 0 && (rf & kRfQ0)) ? p0 : -1;
     } else {
         const int64_t ic = in ? i : a.wq_off;
         const int sq = a.wq_buf[ic];
@@ -1807,33 +1832,11 @@ __device__ __forceinline__ WinEl win_elem(const TickArgs &a, int reg, int64_t i,
         e.raw = raw;
         e.hb = hb;
         e.t = tq;
+        e.mv = -1;
     }
     return e;
 }
 __device__ __forceinline__ int win_c(int32_t raw) { return raw != INT32_MIN ? (raw > 1 ? raw : 1) : 0; }
-
-// Count wave of k_logscan's launch (window ticks): chunk ch, lane l takes elements
-// i0 + 64 g + l (g < 16, all loads of a round in flight): live elements, those with
-// c > 1 (fronts / window) or live backs, and the largest c -> wagg[ch].
-__device__ __forceinline__ void win_count(const TickArgs &a, int ch) {
-    int64_t i0, i1;
-    const int reg = win_region(a, ch, i0, i1);
-    const int lane = lane_id();
-    uint32_t nl = 0, ng = 0, mx = 0;
-#pragma unroll 4
-    for (int g = 0; g < kWinCh / 64; ++g) {
-        const int64_t i = i0 + 64 * g + lane;
-        const WinEl e = win_elem(a, reg, i, i < i1);
-        const int c = win_c(e.raw);
-        nl += c > 0 ? 1u : 0u;
-        ng += c > 1 ? 1u : 0u;
-        mx = (uint32_t)c > mx ? (uint32_t)c : mx;
-    }
-    nl = wave_sum_u32(nl);
-    ng = wave_sum_u32(ng);
-    mx = wave_max_u32(mx);
-    if (lane == 0) a.wagg[ch] = reg == 0 ? make_int4(0, 0, (int)nl, (int)mx) : make_int4((int)nl, (int)ng, 0, (int)mx);
-}
 
 // ------------------------------------------------------------ k_logscan
 // The log role of k_scan as its own launch for large tables (a.f_sep): past 128K
@@ -1848,15 +1851,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long bm[];
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows
     STAMP(a, SO, 0);
-    // window ticks: the first ls_cnt_blocks workgroups count the tick's chunks (one wave
-    // per chunk), the rest are the log role
-    if ((int)blockIdx.x < a.ls_cnt_blocks) {
-        const int ch = (int)blockIdx.x * (kLsBS / 64) + (int)(threadIdx.x >> 6);
-        if (ch < a.nchB + a.nchF + a.nchW) win_count(a, ch);
-        return;
-    }
-    const int lblk = (int)blockIdx.x - a.ls_cnt_blocks;
-    const int nlblk = (int)gridDim.x - a.ls_cnt_blocks;
+    const int lblk = (int)blockIdx.x, nlblk = (int)gridDim.x;
     const int n4 = (((a.W + 63) >> 6) + 1) >> 1;
     const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
     for (int i0 = 0; i0 < n4; i0 += kLsBS * 8) {
@@ -2949,104 +2944,196 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 
 // ------------------------------------------------------------ k_emit_win
 // The level-0 emission of a window tick (see win_elem): one workgroup per 1024-element
-// chunk, thread t takes elements i0 + 256 j + t (j < 4).  Every workgroup first reads all
-// chunk counts (<= 8 int4 loads per thread), the log workgroups' orphan partials and the
-// purge's eviction / queued partials, so each knows N = O + T, the live fronts LF, the
-// live window prefix LW, the live backs LB and its own exclusive prefixes; then the
-// tick is decided the same way in every workgroup: it needs LF <= N < LF + LW (every
-// front served, the first unserved live element inside the scanned window), else
-// status 3 and the host reruns the tick on the general path.  Live element k < N takes
+// chunk, taken in ticket order (back chunks first), thread t holding elements
+// i0 + 256 j + t (j < 4) in registers from their classification to their stores.  A
+// chunk's counts travel by decoupled look-back along two chains -- the back chunks
+// (live backs) and the front / window chunks (live elements, those with c > 1) -- as
+// 8-byte granules {state, live, c > 1, max c} written by one agent-scope store each
+// (MI355X_MICROARCH.md, visibility: a granule needs no further ordering) and read with
+// agent-scope loads, 64 predecessors per wave load.  Live element k < N = O + T takes
 // task k (k_emit2's round 0); live backs are appended at the tail in order, then the
 // served workers with c > 1 in order (A_0[p:] ++ [served, c > 1]); the element of rank
-// N - 1 knows where the next window starts and how long it is.
+// N - 1 reports where the next window starts and how long it is.  A tick that is not a
+// window tick after all -- an unserved front, or no unserved live element inside the
+// scanned prefix -- is flagged (win_ovf) and the host reruns it on the general path.
+constexpr uint64_t kGrA = (1ull << 22) - 1, kGrM = (1ull << 18) - 1;
+__device__ __forceinline__ uint64_t gr_pack(uint32_t st, uint32_t lv, uint32_t g1, uint32_t mx) {
+    return ((uint64_t)st << 62) | ((uint64_t)(mx < kGrM ? mx : kGrM) << 44) | ((uint64_t)g1 << 22) | (uint64_t)lv;
+}
+__device__ __forceinline__ uint64_t gr_load(const unsigned long long *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void gr_store(unsigned long long *p, uint64_t v) {
+    __hip_atomic_store(p, (unsigned long long)v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Wave 0: publish this chunk's aggregate at chain index i, resolve its exclusive prefix
+// from the predecessors (aggregates summed back to the first inclusive one), publish the
+// inclusive value.  Returns the exclusive {live, c > 1, max c}; false if a predecessor
+// never published (a bound on the wait that only a fault can reach).
+__device__ __forceinline__ bool gr_lookback(unsigned long long *g, int i, uint32_t lv, uint32_t g1, uint32_t mx,
+                                            uint32_t &elv, uint32_t &eg1, uint32_t &emx) {
+    const int lane = lane_id();
+    elv = eg1 = emx = 0;
+    if (i == 0) {
+        if (lane == 0) gr_store(g, gr_pack(2, lv, g1, mx));
+        return true;
+    }
+    if (lane == 0) gr_store(g + i, gr_pack(1, lv, g1, mx));
+    int j = i - 1;  // the newest predecessor not yet summed
+    for (int spin = 0; spin < (1 << 22);) {
+        const int q = j - lane;
+        uint64_t v = q >= 0 ? gr_load(g + q) : gr_pack(2, 0, 0, 0);
+        // wait until every lane of this window has a published granule
+        while (__ballot((v >> 62) == 0) && spin < (1 << 22)) {
+            __builtin_amdgcn_s_sleep(1);
+            ++spin;
+            if ((v >> 62) == 0) v = gr_load(g + q);
+        }
+        if (__ballot((v >> 62) == 0)) return false;
+        const uint64_t incl = __ballot((v >> 62) == 2);
+        const int first = incl ? (int)__builtin_ctzll(incl) : 64;  // nearest inclusive predecessor
+        const bool take = lane <= first;
+        uint32_t a = take ? (uint32_t)(v & kGrA) : 0u, b = take ? (uint32_t)((v >> 22) & kGrA) : 0u;
+        uint32_t m = take ? (uint32_t)((v >> 44) & kGrM) : 0u;
+        elv += wave_sum_u32(a);
+        eg1 += wave_sum_u32(b);
+        emx = max(emx, wave_max_u32(m));
+        if (first < 64) {
+            if (lane == 0) gr_store(g + i, gr_pack(2, elv + lv, eg1 + g1, max(emx, mx)));
+            return true;
+        }
+        j -= 64;
+    }
+    return false;
+}
+// The inclusive value of chain index i once published (wave 0); false on the wait bound.
+__device__ __forceinline__ bool gr_wait_incl(const unsigned long long *g, int i, uint32_t &lv, uint32_t &mx) {
+    uint64_t v = gr_load(g + i);
+    for (int spin = 0; (v >> 62) != 2; ++spin) {
+        if (spin >= (1 << 22)) return false;
+        __builtin_amdgcn_s_sleep(1);
+        v = gr_load(g + i);
+    }
+    lv = (uint32_t)(v & kGrA);
+    mx = (uint32_t)((v >> 44) & kGrM);
+    return true;
+}
+
 __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
     prefetch_args(a);
-    __shared__ uint32_t red[kWaves][12];
+    __shared__ uint32_t red[kWaves][4];
     __shared__ uint32_t wt[4][kWaves][2];
-    const int ch = blockIdx.x, tid = threadIdx.x, lane = lane_id(), w = wave_id();
-    const int nch = a.nchB + a.nchF + a.nchW;
-    // ---- the tick's totals and this chunk's prefixes
-    uint32_t LB = 0, LF = 0, LW = 0, blx = 0, lvx = 0, g1x = 0, mx = 0, O = 0, nev = 0, nq = 0;
-    {
-        int4 v[kWinMaxCh / kBS];
-#pragma unroll
-        for (int k = 0; k < kWinMaxCh / kBS; ++k) v[k] = a.wagg[min(tid + k * kBS, nch - 1)];
-        const uint32_t op = tid < a.n_lpart ? a.lpart[tid] : 0u;
-        const uint32_t e0 = tid < 64 ? a.wpart[(size_t)tid * 32] : 0u, q0 = tid < 64 ? a.wpart[(size_t)tid * 32 + 1] : 0u;
-#pragma unroll
-        for (int k = 0; k < kWinMaxCh / kBS; ++k) {
-            const int i = tid + k * kBS;
-            const bool ok = i < nch, B = i < a.nchB, F = !B && i < a.nchB + a.nchF;
-            const uint32_t lv = ok ? (uint32_t)v[k].x : 0u, g1 = ok ? (uint32_t)v[k].y : 0u, bl = ok ? (uint32_t)v[k].z : 0u;
-            LB += B ? bl : 0u;
-            LF += F ? lv : 0u;
-            LW += (!B && !F) ? lv : 0u;
-            blx += i < ch ? bl : 0u;
-            lvx += i < ch ? lv : 0u;
-            g1x += i < ch ? g1 : 0u;
-            mx = (ok && (uint32_t)v[k].w > mx) ? (uint32_t)v[k].w : mx;
-        }
-        O = op;
-        nev = e0;
-        nq = q0;
-        uint32_t x[10] = {LB, LF, LW, blx, lvx, g1x, O, nev, nq, 0};
-#pragma unroll
-        for (int q = 0; q < 9; ++q) x[q] = wave_sum_u32(x[q]);
-        x[9] = wave_max_u32(mx);
-        if (lane == 0)
-#pragma unroll
-            for (int q = 0; q < 10; ++q) red[w][q] = x[q];
-        lds_barrier();
-#pragma unroll
-        for (int q = 0; q < 9; ++q) x[q] = red[0][q] + red[1][q] + red[2][q] + red[3][q];
-        x[9] = max(max(red[0][9], red[1][9]), max(red[2][9], red[3][9]));
-        LB = x[0]; LF = x[1]; LW = x[2]; blx = x[3]; lvx = x[4]; g1x = x[5]; O = x[6]; nev = x[7]; nq = x[8];
-        mx = x[9];
-    }
-    const int64_t N = (int64_t)O + a.T;
-    int status = 0;
-    if (N < (int64_t)LF || N >= (int64_t)LF + LW) status = 3;  // not a window tick: the general path
-    else if (a.head_in + N > a.log_cap) status = 2;            // never write past the in-flight log
-    if (ch == 0 && tid == 0) {
-        a.hout->O = O;
-        a.hout->n_evicted = nev;
-        a.hout->cap_total = -1;  // beyond the scanned prefix (a window tick never needs it)
-        a.hout->maxc = (int32_t)mx;
-        a.hout->L = 0;
-        a.hout->status = status;
-        a.hout->N_eff = status ? 0 : N;
-        a.hout->p = N;
-        a.hout->AL = (int64_t)LF + LW + LB;  // at least
-        if (N == 0) {
-            a.hout->win_head = a.wq_off;
-            a.hout->new_qlen = a.wq_tail + LB - a.wq_off;
-            a.hout->win_qlen = nq;
-            if (a.wq_tail + LB - a.wq_off > a.q_cap) a.hout->win_ovf = 1;
-        }
-    }
-    if (status) return;
+    __shared__ uint32_t xs[8];
+    const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    if (tid == 0) xs[0] = atomicAdd(a.wticket, 1u);  // chunk = ticket: predecessors already run
+    // the orphan partials of the log workgroups and the purge's eviction / queued partials
+    const uint32_t op = tid < a.n_lpart ? a.lpart[tid] : 0u;
+    const uint32_t e0 = tid < 64 ? a.wpart[(size_t)tid * 32] : 0u, q0 = tid < 64 ? a.wpart[(size_t)tid * 32 + 1] : 0u;
+    lds_barrier();
+    const int ch = (int)xs[0];
     int64_t i0, i1;
     const int reg = win_region(a, ch, i0, i1);
-    if (reg != 0 && (int64_t)lvx >= N) return;  // every element of the chunk stays put
-    // ---- elements: classification, then one LDS round for the in-chunk ranks
+    // ---- this chunk's elements: classification (loads in flight), in-chunk ranks
     WinEl e[4];
-    uint64_t ml[4], mg[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int64_t i = i0 + j * kBS + tid;
         e[j] = win_elem(a, reg, i, i < i1);
     }
+    uint64_t ml[4], mg[4];
+    uint32_t cmx = 0;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
         const int c = win_c(e[j].raw);
         ml[j] = __ballot(c > 0);
         mg[j] = __ballot(c > 1);
+        cmx = (uint32_t)c > cmx ? (uint32_t)c : cmx;
         if (lane == 0) {
             wt[j][w][0] = (uint32_t)__popcll(ml[j]);
             wt[j][w][1] = (uint32_t)__popcll(mg[j]);
         }
     }
+    {
+        const uint32_t x0 = wave_sum_u32(op), x1 = wave_sum_u32(e0), x2 = wave_sum_u32(q0), x3 = wave_max_u32(cmx);
+        if (lane == 0) {
+            red[w][0] = x0;
+            red[w][1] = x1;
+            red[w][2] = x2;
+            red[w][3] = x3;
+        }
+    }
     lds_barrier();
+    const uint32_t O = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+    const uint32_t nev = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+    const uint32_t nq = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+    const uint32_t bmx = max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
+    uint32_t tl = 0, tg = 0;  // the chunk's live elements / those with c > 1
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int u = 0; u < kWaves; ++u) {
+            tl += wt[j][u][0];
+            tg += wt[j][u][1];
+        }
+    const int64_t N = (int64_t)O + a.T;
+    const bool logfull = a.head_in + N > a.log_cap;
+    const int nfw = a.nchF + a.nchW;
+    const int ci = reg == 0 ? ch : ch - a.nchB;  // index in its chain
+    unsigned long long *const gch = reg == 0 ? a.wlb : a.wlb + a.nchB;
+    // ---- the chains (wave 0), then the totals this chunk needs
+    if (w == 0) {
+        uint32_t elv, eg1, emx, LB = 0, bmax = 0;
+        bool ok = gr_lookback(gch, ci, reg == 0 ? tl : tl, reg == 0 ? 0u : tg, bmx, elv, eg1, emx);
+        // front / window chunks append after the live backs: the back chain's total
+        if (ok && reg != 0) ok = gr_wait_incl(a.wlb, a.nchB - 1, LB, bmax);
+        if (lane == 0) {
+            xs[1] = elv;
+            xs[2] = eg1;
+            xs[3] = LB;
+            xs[4] = ok ? 1u : 0u;
+            if (!ok) a.hout->win_ovf = 1;
+            if (ch == 0) {
+                a.hout->O = O;
+                a.hout->n_evicted = nev;
+                a.hout->cap_total = -1;  // beyond the scanned prefix (a window tick never needs it)
+                a.hout->L = 0;
+                a.hout->status = logfull ? 2 : 0;
+                a.hout->N_eff = logfull ? 0 : N;
+                a.hout->p = N;
+            }
+            if (ok && reg != 0) {
+                const int64_t inc = (int64_t)elv + tl;  // live fronts / window up to this chunk's end
+                // every front served: the last front chunk's total may not exceed N
+                if (ch == a.nchB + a.nchF - 1 && inc > N) a.hout->win_ovf = 1;
+                if (ci == nfw - 1) {
+                    // the first unserved live element must lie in the scanned prefix
+                    if (inc <= N) a.hout->win_ovf = 1;
+                    a.hout->maxc = (int32_t)max(max(emx, bmx), bmax);
+                    a.hout->AL = inc + LB;  // at least
+                }
+                if (ci == 0 && N == 0) {
+                    a.hout->win_head = a.wq_off;
+                    a.hout->new_qlen = a.wq_tail + LB - a.wq_off;
+                    a.hout->win_qlen = nq;
+                    if (a.wq_tail + LB - a.wq_off > a.q_cap) a.hout->win_ovf = 1;
+                }
+            }
+        }
+    }
+    lds_barrier();
+    if (!xs[4] || logfull) return;
+    if (reg < 2) {
+        // a queued slot moved to the front or the back: its committed position (read-only
+        // during the tick) is tombstoned by the commit; one entry per list position
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int64_t i = i0 + j * kBS + tid;
+            if (i < i1) a.tomb[(reg == 1 ? a.E : 0) + i] = e[j].mv;
+        }
+    }
+    const uint32_t lvx = xs[1], g1x = xs[2], LB = xs[3];
+    const uint32_t blx = lvx;  // back chunks: their chain counts live backs
+    if (reg != 0 && (int64_t)lvx >= N) return;  // every element of the chunk stays put
     uint32_t bl = 0, bg = 0;  // elements of the earlier sub-rounds / waves
     int32_t *const q = a.wq_buf;
 #pragma unroll
@@ -3071,7 +3158,6 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
                 q[pq] = x.s;
                 a.wqf_buf[pq] = x.raw;
                 a.wqh_buf[pq] = x.hb;
-                a.wnpos[x.s] = make_int2((int)pq, (int)a.lstamp);
             } else {
                 a.hout->win_ovf = 1;
             }
@@ -3080,7 +3166,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
         const int64_t k = (int64_t)lvx + rl;
         if (k >= N) continue;
         // served: task k, one fewer free process; c > 1 stays queued, appended after the backs
-        if (a.head_in + k < a.log_cap) a.log_slot[a.head_in + k] = x.s;
+        a.log_slot[a.head_in + k] = x.s;
         a.free_out[x.s] = make_int2(x.raw - 1, c > 1 ? 1 : 0);
         const int64_t G = (int64_t)g1x + rg + (c > 1 ? 1 : 0);  // served workers with c > 1 so far
         if (c > 1) {
@@ -3089,7 +3175,6 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
                 q[pq] = x.s;
                 a.wqf_buf[pq] = x.raw - 1;
                 a.wqh_buf[pq] = x.hb;
-                if (x.t) a.wnpos[x.s] = make_int2((int)pq, (int)a.lstamp);
             } else {
                 a.hout->win_ovf = 1;
             }
@@ -3653,8 +3738,7 @@ void launch_scan(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
 }
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
-    // + the spare slot; no bitmap without log workgroups (a window tick without a log)
-    const size_t lds = grid > a.ls_cnt_blocks ? (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16 : 0;
+    const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
     hipExtLaunchKernelGGL(k_logscan, dim3(grid), dim3(kLsBS), lds, st.s, st.e0, st.e1, 0, a);
 }void launch_plan(const TickArgs &a, Stream st) {
     if (a.grp_on)

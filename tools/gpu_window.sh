@@ -16,3 +16,7 @@ tail -2 gpurun_out/${TAG}_pytest.log
 timeout -k 10 300 python -u bench.py --workload stream > gpurun_out/${TAG}_stream.json 2> gpurun_out/${TAG}_stream.err \
     || { tail -20 gpurun_out/${TAG}_stream.err; exit 3; }
 cat gpurun_out/${TAG}_stream.json
+timeout -k 10 300 python -u tools/stream_probe.py --pinned > gpurun_out/${TAG}_probe.log 2>&1 || { tail -20 gpurun_out/${TAG}_probe.log; exit 5; }
+cat gpurun_out/${TAG}_probe.log
+FAASBAL_COMMIT_NOW=1 timeout -k 10 300 python -u bench.py --workload stream > gpurun_out/${TAG}_stream_cnow.json 2>/dev/null || exit 6
+python -c "import json; d=json.load(open('gpurun_out/${TAG}_stream_cnow.json')); print('commit_now', d['ms_per_step'], d['tick']['kernels_us_per_launch'])"
