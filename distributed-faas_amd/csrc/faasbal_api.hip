@@ -208,6 +208,8 @@ struct fb_ctx {
     int32_t st_E = 0, st_vmax = 0;
     double st_now = 0.0;
     HostPool *pool = nullptr;  // staging workers (FAASBAL_STAGE_THREADS, default 8; 1 = none)
+    const double *st_ts = nullptr;  // staged batch whose timestamps k_ev_link checks (caller's pinned array)
+    const double *l_ts = nullptr;   // ... of the launched tick
     int stage_prof = 0;        // FAASBAL_STAGE_PROF=1: fb_tick_stage's time split to stderr
     double sprof[4] = {0, 0, 0, 0};
     int sprof_n = 0;
@@ -777,6 +779,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_slot = c->ev_slot;
         ea.ev_head = c->ev_head;
         ea.ev_next = c->ev_next;
+        ea.check_ts = c->l_ts != nullptr;
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         ea.link = c->link;
         ea.hout = c->hout_dev;
@@ -1787,7 +1790,28 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
         const int np = (c->pool && E >= kStagePar) ? c->pool->size() : 1;
         uint32_t pbad[16] = {0};
         int32_t pvmax[16] = {0};
+        // pinned batches of contexts whose first launch is k_ev_link: the timestamps are
+        // checked there (fb_tick_wait names the first offending event); the host pass then
+        // reads only what memory safety needs -- slots and kinds -- and the free counts
+        // of registrations (the round-table hint)
+        const bool dev_ts = direct && c->ev_head && c->ev_ll;
+        auto part_slim = [&](int pi) {
+            const int lo = (int)((int64_t)E * pi / np), hi = (int)((int64_t)E * (pi + 1) / np);
+            uint32_t bad = 0;
+            int32_t vm = 0;
+            for (int i = lo; i < hi; ++i) {
+                const uint8_t k = kind[i];
+                bad |= (uint32_t)((uint32_t)slot[i] >= Wv) | (uint32_t)(k > FB_EV_OTHER);
+                if (k <= FB_EV_RECONNECT) vm = std::max(vm, val[i]);
+            }
+            pbad[pi] = bad;
+            pvmax[pi] = vm;
+        };
         auto part = [&](int pi) {
+            if (dev_ts) {
+                part_slim(pi);
+                return;
+            }
             const int lo = (int)((int64_t)E * pi / np), hi = (int)((int64_t)E * (pi + 1) / np);
             uint32_t bad = 0;
             int32_t vm = 0;
@@ -1826,6 +1850,7 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
             if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
                 return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
         }
+        c->st_ts = dev_ts ? ts : nullptr;  // checked by k_ev_link (fb_tick_wait reports)
     }
     const auto tp3 = clk::now();
     if (E && !copied) {
@@ -1893,6 +1918,8 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->l_purge_only = c->next_purge_only;
     c->next_purge_only = false;
     c->l_win = win_plan(c);
+    c->l_ts = E ? c->st_ts : nullptr;
+    c->hout->bad_ts = 0;  // set by k_ev_link when a timestamp is out of order or past now
     const int rc = enqueue_tick(c);
     if (rc) return rc;
     if (E) {
@@ -1929,6 +1956,15 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     HIPCHK(c, hipSetDevice(c->device));
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
+        if (c->l_ts && c->hout->bad_ts) {
+            // the batch's timestamps were left to the device: name the first offending event;
+            // the tick is not committed (its launch read only committed state)
+            c->launched = false;
+            for (int i = 0; i < c->l_E; ++i)
+                if (!(c->l_ts[i] <= c->l_now) || (i && c->l_ts[i] < c->l_ts[i - 1]))
+                    return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
+            return fail(c, FB_EINVAL, "timestamps must be non-decreasing and <= now");
+        }
         if (c->l_used_ll && c->hout->resort) {
             // a slot got more messages than k_ev_apply_ll sorts in registers: the same
             // functional tick again, grouped by the radix sort

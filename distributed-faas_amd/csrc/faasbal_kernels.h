@@ -101,7 +101,7 @@ struct HostOut {
     int64_t win_head;
     int64_t win_qlen;
     int32_t win_ovf;
-    int32_t pad_;
+    int32_t bad_ts;     // k_ev_link: a timestamp past now or out of order (cleared by the host)
 };
 
 // totals computed by k_plan (large grids only; device memory, no atomics)
@@ -223,6 +223,7 @@ struct EvArgs {
     // window ticks: evictions and live queued slots as 64 partials (128-byte lines, word 0 /
     // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
     uint32_t *wpart;
+    int check_ts;               // k_ev_link checks the timestamps (host-unchecked pinned batches)
     unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
     int wlb_n;                  // zeroed here
     uint32_t *wticket;

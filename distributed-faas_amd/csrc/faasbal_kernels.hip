@@ -923,6 +923,11 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
         for (int w = t; w < (a.W + 63) >> 6; w += nt) a.dmask[w] = 0ull;
     if (t < a.E) {
         const uint32_t s = (uint32_t)a.ev_slot[t];
+        if (a.check_ts) {
+            // timestamps non-decreasing and <= now (the host checked slots and kinds)
+            const double tt = a.ev_ts[t], tp = a.ev_ts[t > 0 ? t - 1 : 0];
+            if (!(tt <= a.now) || tt < tp) a.hout->bad_ts = 1;
+        }
         a.front_list[t] = 0;
         a.back_list[t] = 0;
         const unsigned long long old =

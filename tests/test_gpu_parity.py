@@ -323,6 +323,26 @@ def test_invalid_events_rejected():
         g.tick(1000.0, 10.0, [0, 0], [1, 2], [1, 1], [999.0, 998.0], [-1, -1], 0)  # ts decreasing
 
 
+@pytest.mark.parametrize("bad", ["decreasing", "future"])
+def test_invalid_timestamps_in_pinned_batches(bad):
+    """Pinned message arrays leave the timestamp checks to k_ev_link: the tick fails at
+    wait naming the first offending event, commits nothing, and the next tick runs."""
+    st = synth.uniform_state(W=64, seed=1)
+    g, o = _pair(st, 4000)
+    ts = np.array([999.0, 999.5, 998.0 if bad == "decreasing" else 999.6, 999.7])
+    if bad == "future":
+        ts[3] = 1000.5
+    k, s, v, t, q = g.pin_events(np.array([2, 2, 2, 2], np.uint8), np.array([1, 2, 3, 4], np.int32),
+                                 np.zeros(4, np.int32), ts, np.full(4, -1, np.int64))
+    with pytest.raises(FaasbalError, match="event %d" % (2 if bad == "decreasing" else 3)):
+        g.tick(1000.0, 10.0, k, s, v, t, q, 10)
+    args = (1000.0, 10.0, np.array([2], np.uint8), np.array([5], np.int32), np.zeros(1, np.int32),
+            np.array([999.0]), np.full(1, -1, np.int64), 10)
+    a, b = g.tick(*args), o.tick(*args)
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
+
+
 @pytest.fixture
 def force_plan(monkeypatch):
     """Route ticks through the 3-launch path (k_plan), used for large grids."""
