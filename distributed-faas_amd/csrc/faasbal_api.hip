@@ -208,8 +208,10 @@ struct fb_ctx {
     int32_t st_E = 0, st_vmax = 0;
     double st_now = 0.0;
     HostPool *pool = nullptr;  // staging workers (FAASBAL_STAGE_THREADS, default 8; 1 = none)
-    const double *st_ts = nullptr;  // staged batch whose timestamps k_ev_link checks (caller's pinned array)
-    const double *l_ts = nullptr;   // ... of the launched tick
+    // a staged pinned batch k_ev_link checks: the caller's kind / slot / ts arrays (read by
+    // the host only to name an offending event), and those of the launched tick
+    const void *st_chk[3] = {nullptr, nullptr, nullptr};
+    const void *l_chk[3] = {nullptr, nullptr, nullptr};
     int stage_prof = 0;        // FAASBAL_STAGE_PROF=1: fb_tick_stage's time split to stderr
     double sprof[4] = {0, 0, 0, 0};
     int sprof_n = 0;
@@ -779,7 +781,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_slot = c->ev_slot;
         ea.ev_head = c->ev_head;
         ea.ev_next = c->ev_next;
-        ea.check_ts = c->l_ts != nullptr;
+        ea.check_ev = c->l_chk[0] != nullptr;
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         ea.link = c->link;
         ea.hout = c->hout_dev;
@@ -1790,26 +1792,15 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
         const int np = (c->pool && E >= kStagePar) ? c->pool->size() : 1;
         uint32_t pbad[16] = {0};
         int32_t pvmax[16] = {0};
-        // pinned batches of contexts whose first launch is k_ev_link: the timestamps are
-        // checked there (fb_tick_wait names the first offending event); the host pass then
-        // reads only what memory safety needs -- slots and kinds -- and the free counts
-        // of registrations (the round-table hint)
-        const bool dev_ts = direct && c->ev_head && c->ev_ll;
-        auto part_slim = [&](int pi) {
-            const int lo = (int)((int64_t)E * pi / np), hi = (int)((int64_t)E * (pi + 1) / np);
-            uint32_t bad = 0;
-            int32_t vm = 0;
-            for (int i = lo; i < hi; ++i) {
-                const uint8_t k = kind[i];
-                bad |= (uint32_t)((uint32_t)slot[i] >= Wv) | (uint32_t)(k > FB_EV_OTHER);
-                if (k <= FB_EV_RECONNECT) vm = std::max(vm, val[i]);
-            }
-            pbad[pi] = bad;
-            pvmax[pi] = vm;
-        };
+        // pinned batches of contexts whose first launch is k_ev_link are checked there
+        // (slots, kinds, timestamps; fb_tick_wait names the first offending event and the
+        // tick commits nothing): the host does not read them at all.  The round table is
+        // then sized from the last tick's free counts (a wider one is a rerun away).
+        const bool dev_chk = direct && c->ev_head && c->ev_ll;
         auto part = [&](int pi) {
-            if (dev_ts) {
-                part_slim(pi);
+            if (dev_chk) {
+                pbad[pi] = 0;
+                pvmax[pi] = 0;
                 return;
             }
             const int lo = (int)((int64_t)E * pi / np), hi = (int)((int64_t)E * (pi + 1) / np);
@@ -1835,7 +1826,7 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
             pbad[pi] = bad;
             pvmax[pi] = vm;
         };
-        if (np > 1) c->pool->run(part);
+        if (np > 1 && !dev_chk) c->pool->run(part);
         else part(0);
         uint32_t bad = 0;
         for (int pi = 0; pi < np; ++pi) {
@@ -1850,7 +1841,13 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
             if (!(ts[i] <= now) || (i && ts[i] < ts[i - 1]))
                 return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
         }
-        c->st_ts = dev_ts ? ts : nullptr;  // checked by k_ev_link (fb_tick_wait reports)
+        if (dev_chk) {  // checked by k_ev_link (fb_tick_wait reports)
+            c->st_chk[0] = kind;
+            c->st_chk[1] = slot;
+            c->st_chk[2] = ts;
+        } else {
+            c->st_chk[0] = nullptr;
+        }
     }
     const auto tp3 = clk::now();
     if (E && !copied) {
@@ -1918,8 +1915,8 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->l_purge_only = c->next_purge_only;
     c->next_purge_only = false;
     c->l_win = win_plan(c);
-    c->l_ts = E ? c->st_ts : nullptr;
-    c->hout->bad_ts = 0;  // set by k_ev_link when a timestamp is out of order or past now
+    for (int j = 0; j < 3; ++j) c->l_chk[j] = E ? c->st_chk[j] : nullptr;
+    c->hout->bad_ev = 0;  // set by k_ev_link when it finds an invalid message
     const int rc = enqueue_tick(c);
     if (rc) return rc;
     if (E) {
@@ -1956,14 +1953,20 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     HIPCHK(c, hipSetDevice(c->device));
     for (;;) {
         HIPCHK(c, hipStreamSynchronize(c->stream));
-        if (c->l_ts && c->hout->bad_ts) {
-            // the batch's timestamps were left to the device: name the first offending event;
-            // the tick is not committed (its launch read only committed state)
+        if (c->l_chk[0] && c->hout->bad_ev) {
+            // the batch was left to the device's check: name the first offending event; the
+            // tick is not committed (its launch read only committed state)
             c->launched = false;
-            for (int i = 0; i < c->l_E; ++i)
-                if (!(c->l_ts[i] <= c->l_now) || (i && c->l_ts[i] < c->l_ts[i - 1]))
+            const uint8_t *k = (const uint8_t *)c->l_chk[0];
+            const int32_t *sl = (const int32_t *)c->l_chk[1];
+            const double *ts = (const double *)c->l_chk[2];
+            for (int i = 0; i < c->l_E; ++i) {
+                if ((uint32_t)sl[i] >= (uint32_t)c->W) return fail(c, FB_EINVAL, "event %d: slot %d outside [0, %d)", i, sl[i], c->W);
+                if (k[i] > FB_EV_OTHER) return fail(c, FB_EINVAL, "event %d: unknown kind %d", i, k[i]);
+                if (!(ts[i] <= c->l_now) || (i && ts[i] < ts[i - 1]))
                     return fail(c, FB_EINVAL, "event %d: timestamps must be non-decreasing and <= now", i);
-            return fail(c, FB_EINVAL, "timestamps must be non-decreasing and <= now");
+            }
+            return fail(c, FB_EINVAL, "invalid message in the batch");
         }
         if (c->l_used_ll && c->hout->resort) {
             // a slot got more messages than k_ev_apply_ll sorts in registers: the same

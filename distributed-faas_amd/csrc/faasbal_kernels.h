@@ -29,7 +29,7 @@ constexpr int kGrpWords = 64 * 132;  // fused path: group rows of round totals (
 constexpr int kShardMaxR = 4096;     // sharded round tables (k_emit_shard_wide: 64 chunks of 64 rounds)
 
 // event kinds / status (include/faasbal.h)
-constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3;
+constexpr int kEvRegister = 0, kEvReconnect = 1, kEvHeartbeat = 2, kEvResult = 3, kEvOther = 4;
 constexpr uint8_t kEvsApplied = 0, kEvsReconnect = 1;
 
 // deque mode (PushDispatcher.start): a committed token rank with this bit set sat in
@@ -101,7 +101,7 @@ struct HostOut {
     int64_t win_head;
     int64_t win_qlen;
     int32_t win_ovf;
-    int32_t bad_ts;     // k_ev_link: a timestamp past now or out of order (cleared by the host)
+    int32_t bad_ev;     // k_ev_link: an invalid message (slot, kind, timestamp; cleared by the host)
 };
 
 // totals computed by k_plan (large grids only; device memory, no atomics)
@@ -185,7 +185,7 @@ struct EvArgs {
     double tte;
     int64_t head_in;
     const uint32_t *skeys, *svals;
-    const uint8_t *ev_kind;
+    uint8_t *ev_kind;           // (k_ev_link may neutralise an invalid message of a pinned batch)
     const int32_t *ev_val;
     const double *ev_ts;
     const int64_t *ev_seq;
@@ -201,7 +201,7 @@ struct EvArgs {
     uint32_t *tbits;   // one GPU: bit s = slot s got a message this tick (cleared by the first sort pass)
     int32_t *front_list, *back_list;  // slot + 1 (0 = empty), zeroed before the tick
     // linked-list grouping (k_ev_link / k_ev_apply_ll; one GPU, heartbeat loop)
-    const int32_t *ev_slot;
+    int32_t *ev_slot;
     unsigned long long *ev_head;  // per slot: {link stamp, last linked message}
     int32_t *ev_next;             // per message: the message it displaced, -1 = first of its slot
     uint32_t link;                // this launch's stamp (never 0)
@@ -223,7 +223,7 @@ struct EvArgs {
     // window ticks: evictions and live queued slots as 64 partials (128-byte lines, word 0 /
     // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
     uint32_t *wpart;
-    int check_ts;               // k_ev_link checks the timestamps (host-unchecked pinned batches)
+    int check_ev;               // k_ev_link checks the messages (host-unchecked pinned batches)
     unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
     int wlb_n;                  // zeroed here
     uint32_t *wticket;
@@ -328,6 +328,7 @@ struct TickArgs {
                                  // it moved (-1: none), 2 E entries
     int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
     int32_t *pos_out;            // general ticks of window contexts: next-queue position per slot
+
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
     int32_t *rb_slot;   // compact assignments (null: off): slot per LRU position, -1 none
     uint8_t *rb_c;      // ... and min(c, L + 1) (clamped to 255)

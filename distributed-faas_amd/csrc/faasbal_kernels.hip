@@ -922,11 +922,20 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
     if (a.dmask)
         for (int w = t; w < (a.W + 63) >> 6; w += nt) a.dmask[w] = 0ull;
     if (t < a.E) {
-        const uint32_t s = (uint32_t)a.ev_slot[t];
-        if (a.check_ts) {
-            // timestamps non-decreasing and <= now (the host checked slots and kinds)
+        uint32_t s = (uint32_t)a.ev_slot[t];
+        if (a.check_ev) {
+            // a pinned batch the host did not read: slot in range, known kind, timestamps
+            // non-decreasing and <= now; an invalid message is made harmless (slot 0, a
+            // heartbeat) for the rest of the launch, whose tick the host then refuses
+            const uint8_t k = a.ev_kind[t];
             const double tt = a.ev_ts[t], tp = a.ev_ts[t > 0 ? t - 1 : 0];
-            if (!(tt <= a.now) || tt < tp) a.hout->bad_ts = 1;
+            const bool bad_sk = s >= (uint32_t)a.W || k > kEvOther;
+            if (bad_sk || !(tt <= a.now) || tt < tp) a.hout->bad_ev = 1;
+            if (bad_sk) {
+                s = 0;
+                a.ev_slot[t] = 0;
+                a.ev_kind[t] = kEvHeartbeat;
+            }
         }
         a.front_list[t] = 0;
         a.back_list[t] = 0;

@@ -323,18 +323,24 @@ def test_invalid_events_rejected():
         g.tick(1000.0, 10.0, [0, 0], [1, 2], [1, 1], [999.0, 998.0], [-1, -1], 0)  # ts decreasing
 
 
-@pytest.mark.parametrize("bad", ["decreasing", "future"])
-def test_invalid_timestamps_in_pinned_batches(bad):
-    """Pinned message arrays leave the timestamp checks to k_ev_link: the tick fails at
-    wait naming the first offending event, commits nothing, and the next tick runs."""
+@pytest.mark.parametrize("bad", ["decreasing", "future", "slot", "kind"])
+def test_invalid_messages_in_pinned_batches(bad):
+    """Pinned message arrays are checked by k_ev_link, not read by the host: the tick
+    fails at wait naming the first offending event, commits nothing (an out-of-range
+    slot or unknown kind is neutralised before any use), and the next tick runs."""
     st = synth.uniform_state(W=64, seed=1)
     g, o = _pair(st, 4000)
     ts = np.array([999.0, 999.5, 998.0 if bad == "decreasing" else 999.6, 999.7])
+    kinds = np.array([2, 2, 2, 2], np.uint8)
+    slots = np.array([1, 2, 3, 4], np.int32)
     if bad == "future":
         ts[3] = 1000.5
-    k, s, v, t, q = g.pin_events(np.array([2, 2, 2, 2], np.uint8), np.array([1, 2, 3, 4], np.int32),
-                                 np.zeros(4, np.int32), ts, np.full(4, -1, np.int64))
-    with pytest.raises(FaasbalError, match="event %d" % (2 if bad == "decreasing" else 3)):
+    if bad == "slot":
+        slots[2] = 1 << 20
+    if bad == "kind":
+        kinds[3] = 9
+    k, s, v, t, q = g.pin_events(kinds, slots, np.zeros(4, np.int32), ts, np.full(4, -1, np.int64))
+    with pytest.raises(FaasbalError, match="event %d" % (2 if bad in ("decreasing", "slot") else 3)):
         g.tick(1000.0, 10.0, k, s, v, t, q, 10)
     args = (1000.0, 10.0, np.array([2], np.uint8), np.array([5], np.int32), np.zeros(1, np.int32),
             np.array([999.0]), np.full(1, -1, np.int64), 10)
