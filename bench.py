@@ -226,6 +226,7 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
         run(i)
     kt = g.timing_read()
     g.timing_enable(False)
+    wstats = g.window_stats() if world == 1 else (0, 0)
     kern = {k: ms / max(n, 1) * 1e3 for k, (ms, n) in kt.items()}  # us per launch
     per_tick = {k: ms / K * 1e3 for k, (ms, n) in kt.items()}      # us per tick
     line = {
@@ -253,6 +254,9 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
         "tick": {"device_us_per_tick": sum(per_tick.values()), "kernels_us_per_tick": per_tick,
                  "kernels_us_per_launch": kern},
     }
+    if world == 1:
+        # window ticks among all the ticks this process ran, and fallbacks
+        line["tick"]["window_ticks"], line["tick"]["window_fallbacks"] = wstats
     if dist is not None:
         line["config"]["world_size_reported"] = dist.get_world_size()
         line["config"]["backend"] = dist.get_backend()

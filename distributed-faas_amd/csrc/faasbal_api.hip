@@ -2062,10 +2062,10 @@ int fb_tick_commit(fb_ctx *c) {
         a.head_local = c->l_head_local;
         a.shard = c->shard;
         a.nbo = (int)cdiv(n_orph, kBS);
-        if (c->l_oseg && n_orph > 0) {  // per-tile segments: a wave per 64 log tiles
+        if (c->l_oseg && n_orph > 0) {  // per-tile segments: a wave per log tile
             a.oseg = c->fcnt;
             a.oseg_tiles = c->l_nbf;
-            a.nbo = (int)cdiv(c->l_nbf, 64 * kWaves);
+            a.nbo = (int)cdiv(c->l_nbf, kWaves);
         }
         a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
         a.ev_clr = c->ev_clr;
@@ -2322,9 +2322,20 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
     if (evicted && c->last.n_evicted && !add(evicted, c->evicted, (int64_t)c->last.n_evicted * 4) &&
         (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4)))
         return rc;
+    // the orphans' segments gathered by the same launch when they go to pinned memory
+    bool orph_done = false;
+    if (orphans && c->l_oseg && c->d2h_kernel && c->last.n_orphans_local) {
+        if (int64_t *od = (int64_t *)mapped(orphans)) {
+            m.odst = od;
+            m.osrc = c->orphans;
+            m.ocnt = c->fcnt;
+            m.otiles = c->l_nbf;
+            orph_done = true;
+        }
+    }
     launch_copy_multi(m, Stream(c->stream));
     HIPCHK(c, hipGetLastError());
-    if (orphans && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
+    if (orphans && !orph_done && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return FB_OK;
 }

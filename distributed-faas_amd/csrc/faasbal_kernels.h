@@ -118,7 +118,7 @@ struct CommitArgs {
     int32_t *bud;              // one-GPU heartbeat: touched slots get bud_next[s] (budget after the tick)
     const int32_t *bud_next;
     const uint32_t *oseg;  // non-null: orphans in per-tile segments (orphans[t*2048 + i], i < oseg[t]),
-                           // blocks [nbw, nbw + nbo) a wave per 64 of the oseg_tiles tiles
+                           // blocks [nbw, nbw + nbo) a wave per tile of the oseg_tiles
     int oseg_tiles;
     int nbo;            // ... then blocks [nbw + nbo, + ceil(n_clr / 256)) clear the entries the
     int n_clr;          // committed tick's results completed: log_slot[ev_clr[e]] = -1, e < n_clr
@@ -425,6 +425,12 @@ struct CopyMulti {
     int64_t words[4];
     int blk0[4];
     int n;
+    // optional: the orphans' per-tile segments gathered into odst, one block per tile after
+    // the copies' blocks (k_orph_gather's work in the same launch)
+    int64_t *odst;
+    const int64_t *osrc;
+    const uint32_t *ocnt;
+    int otiles;
 };
 void launch_copy_multi(const CopyMulti &m, Stream st);
 // the dense orphan list from per-tile segments (dst may be host-mapped memory)

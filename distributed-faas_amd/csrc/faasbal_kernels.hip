@@ -817,19 +817,11 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
     if (blk >= a.nbw && a.oseg) {
         // orphans in per-tile segments (fused one-GPU and window ticks): a wave per 64 tiles
         // (one count load each), then the tiles that hold orphans one after another
-        // lane per tile: each lane clears its tile's orphans (window ticks leave about one
-        // per tile, so one load round and one store round for the whole wave)
-        const int t = ((blk - a.nbw) * kWaves + wave_id()) * 64 + lane_id();
+        // a wave per tile: 64 orphans per round (a fused tick leaves ~100 per tile, a
+        // window tick ~1; most of a window tick's waves read one count and stop)
+        const int t = (blk - a.nbw) * kWaves + wave_id();
         const uint32_t n = t < a.oseg_tiles ? a.oseg[t] : 0u;
-        const int64_t *src = a.orphans + (int64_t)t * kFTile;
-        for (uint32_t i = 0; i < n; i += 4) {
-            int64_t q[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) q[k] = src[i + k < n ? i + k : i];
-#pragma unroll
-            for (int k = 0; k < 4; ++k)
-                if (i + k < n) a.log_slot[q[k]] = -1;
-        }
+        for (uint32_t i = lane_id(); i < n; i += 64) a.log_slot[a.orphans[(int64_t)t * kFTile + i]] = -1;
         return;
     }
     if (blk >= a.nbw) {
@@ -3588,10 +3580,9 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
 // dense list is the segments in tile order.  One workgroup per tile: its offset is the
 // sum of the earlier tiles' counts (<= 4 loads per thread), then the copy.  dst may be
 // host memory mapped for the device (the readback into pinned memory).
-__global__ __launch_bounds__(kBS) void k_orph_gather(int64_t *__restrict__ dst, const int64_t *__restrict__ src,
-                                                    const uint32_t *__restrict__ cnt, int ntile) {
+__device__ __forceinline__ void orph_gather_tile(int64_t *__restrict__ dst, const int64_t *__restrict__ src,
+                                                 const uint32_t *__restrict__ cnt, int t) {
     __shared__ uint32_t l4[kWaves];
-    const int t = blockIdx.x;
     uint32_t pre = 0;
     for (int i = threadIdx.x; i < t; i += kBS) pre += cnt[i];
     pre = wave_sum_u32(pre);
@@ -3600,6 +3591,10 @@ __global__ __launch_bounds__(kBS) void k_orph_gather(int64_t *__restrict__ dst, 
     const int64_t off = (int64_t)l4[0] + l4[1] + l4[2] + l4[3];
     const uint32_t n = cnt[t];
     for (uint32_t i = threadIdx.x; i < n; i += kBS) dst[off + i] = src[(int64_t)t * kFTile + i];
+}
+__global__ __launch_bounds__(kBS) void k_orph_gather(int64_t *__restrict__ dst, const int64_t *__restrict__ src,
+                                                    const uint32_t *__restrict__ cnt, int ntile) {
+    orph_gather_tile(dst, src, cnt, blockIdx.x);
 }
 
 // Evicted slots in ascending order when the tick did not compact them (window ticks):
@@ -3623,12 +3618,17 @@ __global__ __launch_bounds__(kBS) void k_evict_compact(int32_t *__restrict__ dst
 // Several word copies in one launch (a tick's outputs into pinned host memory with one
 // kernel instead of one per array): copy i takes the blocks [b_i, b_{i+1}) of the grid.
 __global__ __launch_bounds__(kBS) void k_copy_multi(CopyMulti m) {
+    const int ob = (int)gridDim.x - m.otiles;  // the last otiles blocks gather orphan segments
+    if ((int)blockIdx.x >= ob) {
+        orph_gather_tile(m.odst, m.osrc, m.ocnt, (int)blockIdx.x - ob);
+        return;
+    }
     int i = 0;
     while (i + 1 < m.n && (int)blockIdx.x >= m.blk0[i + 1]) ++i;
     uint32_t *__restrict__ dst = m.dst[i];
     const uint32_t *__restrict__ src = m.src[i];
     const int64_t n = m.words[i];
-    const int64_t nb = (int64_t)(i + 1 < m.n ? m.blk0[i + 1] : (int)gridDim.x) - m.blk0[i];
+    const int64_t nb = (int64_t)(i + 1 < m.n ? m.blk0[i + 1] : ob) - m.blk0[i];
     const int64_t stride = nb * kBS * 4;
     for (int64_t q0 = ((int64_t)(blockIdx.x - m.blk0[i]) * kBS + threadIdx.x) * 4; q0 < n; q0 += stride) {
         uint32_t v[4];
@@ -3718,9 +3718,10 @@ void launch_ev_apply_ll(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_copy_multi(const CopyMulti &m, Stream st) {
-    if (m.n <= 0) return;
+    if (m.n <= 0 && m.otiles <= 0) return;
     const int last = m.n - 1;
-    const int grid = m.blk0[last] + (int)std::min<int64_t>(std::max<int64_t>(1, (m.words[last] + 4 * kBS - 1) / (4 * kBS)), 512);
+    const int grid = (m.n > 0 ? m.blk0[last] + (int)std::min<int64_t>(std::max<int64_t>(1, (m.words[last] + 4 * kBS - 1) / (4 * kBS)), 512) : 0) +
+                     m.otiles;
     hipExtLaunchKernelGGL(k_copy_multi, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, m);
 }
 void launch_orph_gather(int64_t *dst, const int64_t *src, const uint32_t *cnt, int ntile, Stream st) {
