@@ -125,6 +125,14 @@ struct fb_ctx {
     int32_t *rb_slot = nullptr;
     uint8_t *rb_c = nullptr;
     int compact = 0, l_compact = 0;    // the setting, and the one the last launch ran with
+    // fb_set_compact_out: pinned buffers the ticks write their compact outputs into directly
+    // (device views of them, the caller's pointers, capacities); l_cout: the last launch did
+    int32_t *cout_slot = nullptr, *cout_ev = nullptr;
+    uint8_t *cout_c = nullptr;
+    int64_t *cout_orph = nullptr;
+    const void *cout_host[4] = {nullptr, nullptr, nullptr, nullptr};
+    int64_t cout_cap = 0, cout_ocap = 0, cout_ecap = 0;
+    bool l_cout = false;
     HostPool *xpool = nullptr;         // fb_expand_compact's workers (created on first use)
     int32_t *trash = nullptr;  // kTrashRows x kBS words written by inactive lanes (never read)
     int64_t Qn = 0, head = 0;
@@ -162,7 +170,7 @@ struct fb_ctx {
     bool cm_pending = false;
     CommitArgs cm{};
     int cm_grid = 0;
-    int commit_now = 0;        // FAASBAL_COMMIT_NOW=1: never defer (A/B knob)
+    int commit_now = -1;       // FAASBAL_COMMIT_NOW: 1 never defer, 0 always, -1 window ticks' at once (A/B knob)
     PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
     uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
@@ -971,6 +979,15 @@ int enqueue_tick(fb_ctx *c) {
         a.rb_slot = c->rb_slot;
         a.rb_c = c->rb_c;
     }
+    // registered pinned outputs: the compact form and the evicted slots go straight to the
+    // host (fused ticks, whose orphans a gather launch after the emission sends there too)
+    c->l_cout = c->l_compact && c->cout_slot && a.fused && a.f_emit && Qlog <= c->cout_cap && W <= c->cout_ecap &&
+                head <= c->cout_ocap;
+    if (c->l_cout) {
+        a.rb_slot = c->cout_slot;
+        a.rb_c = c->cout_c;
+        a.evicted = c->cout_ev;
+    }
     a.arena = (char *)c->arena;
     a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !c->no_arena32) ? 1 : 0;
     a.log_slot = c->log_slot;
@@ -1118,6 +1135,7 @@ int enqueue_tick(fb_ctx *c) {
         if (a.segw) launch_emit2(a, t.st());
         else launch_emit(a, t.st());
     }
+    if (c->l_cout && head > 0) launch_orph_gather(c->cout_orph, c->orphans, c->fcnt, nbf, Stream(c->stream));
     HIPCHK(c, hipGetLastError());
     return FB_OK;
 }
@@ -2089,7 +2107,7 @@ int fb_tick_commit(fb_ctx *c) {
             a.post_rf = c->post_rf;
         }
         const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) : 0);
-        if (c->ev_head && c->ev_ll && !c->commit_now && !c->l_win) {  // (a window tick's commit runs at once)
+        if (c->ev_head && c->ev_ll && c->commit_now != 1 && !(c->l_win && c->commit_now < 0)) {  // (by default a window tick's commit runs at once)
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
             c->cm_grid = grid;
@@ -2232,6 +2250,10 @@ int fb_get_evicted(fb_ctx *c, int32_t n, int32_t *dst) {
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
     if (n < 0 || n > c->last.n_evicted) return fail(c, FB_EINVAL, "evicted count");
     HIPCHK(c, hipSetDevice(c->device));
+    if (c->l_cout) {  // the tick wrote them into the registered pinned buffer
+        if (n && dst != c->cout_host[3]) memcpy(dst, c->cout_host[3], (size_t)n * 4);
+        return FB_OK;
+    }
     if (int rc = evict_ready(c)) return rc;
     return copy_out(c, dst, c->evicted, (size_t)n * 4);
 }
@@ -2247,7 +2269,11 @@ int fb_get_outputs(fb_ctx *c, int32_t *assign, int64_t *orphans, int32_t *evicte
         return rc;
     if (orphans && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
     if (evicted && (rc = evict_ready(c))) return rc;
-    if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) return rc;
+    if (evicted && c->last.n_evicted && c->l_cout) {
+        if (evicted != c->cout_host[3]) memcpy(evicted, c->cout_host[3], (size_t)c->last.n_evicted * 4);
+    } else if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) {
+        return rc;
+    }
     HIPCHK(c, hipStreamSynchronize(c->stream));
     return FB_OK;
 }
@@ -2272,6 +2298,38 @@ int fb_window_stats(fb_ctx *c, int64_t *window_ticks, int64_t *fallbacks) {
     return FB_OK;
 }
 
+int fb_set_compact_out(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, int64_t *orphans, int64_t ocap,
+                       int32_t *evicted, int64_t ecap) {
+    if (!c) return FB_EINVAL;
+    if (c->shard) return fail(c, FB_ESTATE, "compact assignments exist on one-GPU contexts only");
+    if (c->launched && !c->waited) return fail(c, FB_ESTATE, "fb_set_compact_out with a tick in flight");
+    if (!slot) {  // unregister
+        c->cout_slot = nullptr;
+        return FB_OK;
+    }
+    if (!cnt || !orphans || !evicted || cap < 0 || ocap < 0 || ecap < 0) return FB_EINVAL;
+    void *dv[4];
+    const void *hp[4] = {slot, cnt, orphans, evicted};
+    for (int j = 0; j < 4; ++j) {
+        hipPointerAttribute_t at;
+        if (hipPointerGetAttributes(&at, hp[j]) != hipSuccess || at.type != hipMemoryTypeHost || !at.devicePointer) {
+            (void)hipGetLastError();
+            return fail(c, FB_EINVAL, "compact output buffers must be pinned host memory (fb_host_alloc)");
+        }
+        dv[j] = at.devicePointer;
+        c->cout_host[j] = hp[j];
+    }
+    c->cout_slot = (int32_t *)dv[0];
+    c->cout_c = (uint8_t *)dv[1];
+    c->cout_orph = (int64_t *)dv[2];
+    c->cout_ev = (int32_t *)dv[3];
+    c->cout_cap = cap;
+    c->cout_ocap = ocap;
+    c->cout_ecap = ecap;
+    c->compact = 1;
+    return FB_OK;
+}
+
 int fb_set_compact(fb_ctx *c, int enable) {
     if (!c) return FB_EINVAL;
     if (c->shard) return fail(c, FB_ESTATE, "compact assignments exist on one-GPU contexts only");
@@ -2288,6 +2346,10 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
         return fail(c, FB_ERANGE, "fill level %d: rounds beyond a byte, read fb_get_outputs", c->last.fill_level);
     const int64_t n = c->l_Qn + 2 * (int64_t)c->l_E;
     *n_pos = n;
+    // the tick wrote into the registered buffers: nothing left to copy into those
+    if (c->l_cout && (!slot || slot == c->cout_host[0]) && (!cnt || cnt == c->cout_host[1]) &&
+        (!orphans || orphans == c->cout_host[2]) && (!evicted || evicted == c->cout_host[3]))
+        return FB_OK;
     if ((slot || cnt) && cap < n) return fail(c, FB_EINVAL, "compact buffers of %lld < %lld positions", (long long)cap,
                                               (long long)n);
     HIPCHK(c, hipSetDevice(c->device));
@@ -2317,11 +2379,19 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
     };
     // the c bytes travel as whole words when the caller's buffer has room for the padding
     const int64_t cw = (n + 3) & ~(int64_t)3;
-    if (slot && n && !add(slot, c->rb_slot, n * 4) && (rc = d2h(c, slot, c->rb_slot, (size_t)n * 4))) return rc;
-    if (cnt && n && !(cw <= cap && add(cnt, c->rb_c, cw)) && (rc = d2h(c, cnt, c->rb_c, (size_t)n))) return rc;
-    if (evicted && c->last.n_evicted && !add(evicted, c->evicted, (int64_t)c->last.n_evicted * 4) &&
-        (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4)))
+    if (c->l_cout) {  // the tick wrote the compact form into the registered buffers
+        if (slot && n && slot != c->cout_host[0]) memcpy(slot, c->cout_host[0], (size_t)n * 4);
+        if (cnt && n && cnt != c->cout_host[1]) memcpy(cnt, c->cout_host[1], (size_t)n);
+    } else {
+        if (slot && n && !add(slot, c->rb_slot, n * 4) && (rc = d2h(c, slot, c->rb_slot, (size_t)n * 4))) return rc;
+        if (cnt && n && !(cw <= cap && add(cnt, c->rb_c, cw)) && (rc = d2h(c, cnt, c->rb_c, (size_t)n))) return rc;
+    }
+    if (evicted && c->last.n_evicted && c->l_cout) {
+        if (evicted != c->cout_host[3]) memcpy(evicted, c->cout_host[3], (size_t)c->last.n_evicted * 4);
+    } else if (evicted && c->last.n_evicted && !add(evicted, c->evicted, (int64_t)c->last.n_evicted * 4) &&
+               (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) {
         return rc;
+    }
     // the orphans' segments gathered by the same launch when they go to pinned memory
     bool orph_done = false;
     if (orphans && c->l_oseg && c->d2h_kernel && c->last.n_orphans_local) {
@@ -2488,7 +2558,7 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
         if (int rc = evict_ready(c)) return rc;
         HIPCHK(c, hipStreamSynchronize(c->stream));
     }
-    v->evicted = c->evicted;
+    v->evicted = c->l_cout ? c->cout_ev : c->evicted;
     v->n_workers = c->W;
     v->queue_len = c->Qn;
     v->log_head = c->head;

@@ -244,6 +244,19 @@ class GpuBalancer:
         self._chk(self.lib.fb_window_stats(self.h, C.byref(a), C.byref(b)))
         return a.value, b.value
 
+    def set_compact_out(self, slot, c, orphans, evicted):
+        """Register pinned arrays (``pinned()``) that fused ticks fill with their compact
+        outputs while they run (fb_set_compact_out); ``outputs_compact`` into the same
+        arrays then copies nothing.  ``slot=None`` unregisters."""
+        if slot is None:
+            self._chk(self.lib.fb_set_compact_out(self.h, None, None, 0, None, 0, None, 0))
+            return
+        if slot.dtype != np.int32 or c.dtype != np.uint8 or orphans.dtype != np.int64 or evicted.dtype != np.int32:
+            raise ValueError("slot int32, c uint8, orphans int64, evicted int32")
+        self._chk(self.lib.fb_set_compact_out(self.h, _p(slot), _p(c), min(len(slot), len(c)), _p(orphans),
+                                              len(orphans), _p(evicted), len(evicted)))
+        self._cout = (slot, c, orphans, evicted)  # keep them alive while registered
+
     def set_compact(self, on=True):
         """Ticks launched afterwards also write the compact assignment form (slot and
         min(c, L + 1) per LRU position): ``outputs_compact`` then reads 5 bytes per

@@ -184,6 +184,15 @@ int fb_window_stats(fb_ctx *ctx, int64_t *window_ticks, int64_t *fallbacks);
 int fb_get_outputs_compact(fb_ctx *ctx, int32_t *slot, uint8_t *c, int64_t cap, int64_t *n_pos, int64_t *orphans,
                            int32_t *evicted);
 int fb_expand_compact(fb_ctx *ctx, const int32_t *slot, const uint8_t *c, int64_t n_pos, int32_t *assign);
+/* Pinned buffers (fb_host_alloc) that ticks write their compact outputs into while they
+ * run: slot / c per position (cap entries), orphans (ocap), evicted slots (ecap); turns
+ * compact mode on.  A fused tick (the configs[2] shape) whose outputs fit leaves them
+ * there by the time fb_tick_wait returns, and fb_get_outputs_compact into the same
+ * buffers copies nothing; other ticks fill them through fb_get_outputs_compact as
+ * usual.  The buffers must not be touched between a launch and its wait.  slot = NULL
+ * unregisters. */
+int fb_set_compact_out(fb_ctx *ctx, int32_t *slot, uint8_t *c, int64_t cap, int64_t *orphans, int64_t ocap,
+                       int32_t *evicted, int64_t ecap);
 
 /* Pinned host memory: fb_get_* copies into it are single DMA transfers on the
  * context stream (the drop-in's readback of a tick's assignments). */

@@ -171,6 +171,45 @@ def test_compact_assignments_config2():
     assert _compact_matches(g, "configs[2]") == r["n_assigned"] > 0
 
 
+@pytest.mark.parametrize("shape", ["config2", "random"])
+def test_compact_outputs_written_during_the_tick(shape):
+    """fb_set_compact_out: the tick writes its compact form, orphans and evicted slots into
+    registered pinned arrays while it runs; after the wait they equal the per-task
+    readback (configs[2]: a fused tick), and outputs into other arrays copy them over."""
+    if shape == "config2":
+        st, T, E = synth.zipf_state(W=65536, seed=0), 1_000_000, 1
+        ticks = [dict(now=1000.0, ev=((), (), (), (), None), n=T)] * 2
+    else:
+        scen = synth.random_scenario(7100, W=1000, n_ticks=4, max_events=200, max_new=3000)
+        st, T, E = _state(scen), 3000, 256
+        ticks = [dict(now=tk["now"], ev=(tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"]),
+                      n=tk["n_new"]) for tk in scen["ticks"]]
+    W = len(st["reg"])
+    g = GpuBalancer(W, 3 * len(st["log"]) + 4 * T + 16, max_events=max(E, 256))
+    g.load(st)
+    cap = W + 2 * g.max_events + 16
+    bufs = (g.pinned(cap, np.int32), g.pinned(cap, np.uint8), g.pinned(3 * len(st["log"]) + 4 * T + 16, np.int64),
+            g.pinned(W, np.int32))
+    g.set_compact_out(*bufs)
+    for t, tk in enumerate(ticks):
+        g.launch(tk["now"], 10.0, *tk["ev"], tk["n"])
+        r = g.wait()
+        slot, c, orph, ev = g.outputs_compact(*bufs)
+        np.testing.assert_array_equal(g.expand(slot, c), g.assignments(), err_msg="tick %d assign" % t)
+        np.testing.assert_array_equal(orph, g.orphans(), err_msg="tick %d orphans" % t)
+        np.testing.assert_array_equal(ev, g.evicted(), err_msg="tick %d evicted" % t)
+        other = (g.pinned(cap, np.int32), g.pinned(cap, np.uint8), g.pinned(max(len(orph), 1), np.int64),
+                 g.pinned(max(len(ev), 1), np.int32))
+        s2, c2, o2, e2 = g.outputs_compact(*other)
+        np.testing.assert_array_equal(s2, slot)
+        np.testing.assert_array_equal(c2, c)
+        np.testing.assert_array_equal(e2, ev)
+        if shape == "config2" and t == 0:
+            assert r["n_orphans"] > 0 and r["n_evicted"] > 0
+        g.commit()
+    g.close()
+
+
 def _one_tick_full(st, T, now=1000.0, tte=10.0):
     cap = len(st["log"]) + T + len(st["log"]) + 16
     g, o = _pair(st, cap)

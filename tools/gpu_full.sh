@@ -16,3 +16,4 @@ cat gpurun_out/${TAG}_bench.json
 timeout -k 10 300 python -u bench.py --workload stream > gpurun_out/${TAG}_stream.json 2> gpurun_out/${TAG}_stream.err \
     || { tail -20 gpurun_out/${TAG}_stream.err; exit 4; }
 cat gpurun_out/${TAG}_stream.json
+bash tools/ab_stream.sh ${TAG}_ab "FAASBAL_COMMIT_NOW=-1" "FAASBAL_COMMIT_NOW=0" "FAASBAL_COMMIT_NOW=1" || exit 5
