@@ -147,6 +147,7 @@ struct fb_ctx {
     int l_nchW = 0;            // ... and the window chunks it scans
     int64_t l_qoff = 0;
     int32_t *pos_of[2] = {nullptr, nullptr};
+    bool pos_ok = false;       // pos_of[qcur] is exact for every queued slot (general ticks do not keep it)
     // k_emit_win: per front / back list entry, the committed position of the queued slot it
     // moved (-1: none), read by the tick's commit
     int32_t *tomb = nullptr;
@@ -549,6 +550,7 @@ int win_normalize(fb_ctx *c) {
     c->qcur = o;
     c->qoff = 0;
     c->Qn = n;
+    c->pos_ok = true;
     return FB_OK;
 }
 
@@ -600,6 +602,7 @@ int win_alloc(fb_ctx *c) {
     c->win_mem = m;
     c->win_owned = true;
     c->win_cap = true;
+    c->pos_ok = true;
     if (c->W && c->Qn) {
         std::vector<int32_t> q((size_t)c->Qn), pos((size_t)c->W, 0);
         HIPCHK(c, hipMemcpy(q.data(), c->queue[0], (size_t)c->Qn * 4, hipMemcpyDeviceToHost));
@@ -760,6 +763,11 @@ int enqueue_tick(fb_ctx *c) {
     const int ls_grid = std::max(1, std::min(c->ncu, (int)cdiv(nbf, kLsBS / 64)));
     c->l_used_ll = false;
     const bool ll = E > 0 && c->ev_head && c->ev_ll && !c->l_resort;
+    if (c->l_win && !c->pos_ok) {
+        // the first window tick after general ticks: every queued slot's position, once
+        launch_pos_rebuild(c->pos_of[c->qcur], c->queue[c->qcur], c->qfree[c->qcur], c->qoff, Qn, Stream(c->stream));
+        c->pos_ok = true;
+    }
     if (!ll && (rc = flush_commit(c))) return rc;
     if (ll) {
         // group the messages per slot by linked lists (no sort): two launches
@@ -995,8 +1003,7 @@ int enqueue_tick(fb_ctx *c) {
     a.queue_out = c->queue[qn];
     a.qfree_out = c->qfree[qn];
     a.qhb_out = c->qhb[qn];
-    // a general tick of a window context writes where each slot of its next queue sits
-    if (c->win_cap && !c->l_win) a.pos_out = c->pos_of[qn];
+
     a.c_hb = c->c_hb;
     a.orphans = c->orphans;
     a.evicted = c->evicted;
@@ -1484,6 +1491,7 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         for (int64_t i = 0; i < queue_len; ++i) pos[queue[i]] = (int32_t)i;
         HIPCHK(c, hipMemcpy(c->pos_of[0], pos.data(), W * 4, hipMemcpyHostToDevice));
     }
+    c->pos_ok = c->win_cap;
     if (W) {
         HIPCHK(c, hipMemcpy(c->reg, reg.data(), W, hipMemcpyHostToDevice));
         std::vector<int2> fq(W);
@@ -2137,6 +2145,7 @@ int fb_tick_commit(fb_ctx *c) {
     } else {
         c->qcur ^= 1;
         c->qoff = 0;
+        c->pos_ok = false;  // the new queue's positions are rebuilt by the next window tick
         c->Qn = c->last.queue_len;
         c->maxc_hint = std::max(1, c->last.max_free);
     }

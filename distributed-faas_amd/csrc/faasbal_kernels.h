@@ -327,7 +327,6 @@ struct TickArgs {
     int32_t *tomb;               // per back / front list entry: the committed position of a queued slot
                                  // it moved (-1: none), 2 E entries
     int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
-    int32_t *pos_out;            // general ticks of window contexts: next-queue position per slot
 
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
     int32_t *rb_slot;   // compact assignments (null: off): slot per LRU position, -1 none
@@ -411,6 +410,7 @@ void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);
 void launch_emit_shard(const TickArgs &a, Stream st);
 void launch_emit_win(const TickArgs &a, int grid, Stream st);
+void launch_pos_rebuild(int32_t *pos, const int32_t *queue, const int32_t *qfree, int64_t off, int64_t n, Stream st);
 // evicted slots in ascending order from the per-slot status bytes and per-tile counts (two
 // launches: a one-workgroup scan of the tile counts, then one block per tile)
 void launch_evict_gather(int32_t *dst, const uint8_t *st, const uint32_t *wcnt, int64_t *wpre, int W, Stream s);

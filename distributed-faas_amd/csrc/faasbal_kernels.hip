@@ -2411,7 +2411,6 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
                 a.queue_out[np] = s;
                 a.qfree_out[np] = raw - (int32_t)n_q;
                 a.qhb_out[np] = hbp;
-                if (a.pos_out) a.pos_out[s] = (int32_t)np;
             }
         }
         STAMPR(a, SO, 14);
@@ -2890,7 +2889,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 wt_store(a.queue_out + np, s);
                 wt_store(a.qfree_out + np, raw - (int32_t)n_q);
                 wt_store(a.qhb_out + np, hb0);
-                if (a.pos_out) a.pos_out[s] = (int32_t)np;  // window contexts: where the slot sits next
             }
         }
         STAMP(a, SO, 15);
@@ -3597,6 +3595,16 @@ __global__ __launch_bounds__(kBS) void k_orph_gather(int64_t *__restrict__ dst, 
     orph_gather_tile(dst, src, cnt, blockIdx.x);
 }
 
+// pos[queue[p]] = p over the committed window [off, off + n) (tombstones skipped): the
+// positions window ticks need, rebuilt once after general ticks (which do not keep them)
+__global__ __launch_bounds__(kBS) void k_pos_rebuild(int32_t *__restrict__ pos, const int32_t *__restrict__ queue,
+                                                    const int32_t *__restrict__ qfree, int64_t off, int64_t n) {
+    const int64_t i = (int64_t)blockIdx.x * kBS + threadIdx.x;
+    if (i >= n) return;
+    const int32_t s = queue[off + i];
+    if (qfree[off + i] != kTomb) pos[s] = (int32_t)(off + i);
+}
+
 // Evicted slots in ascending order when the tick did not compact them (window ticks):
 // one workgroup scans the per-tile eviction counts, then one block per 256-slot tile
 // writes its evicted slots at its offset (dst may be host-mapped memory).
@@ -3799,6 +3807,11 @@ void launch_evict_gather(int32_t *dst, const uint8_t *st, const uint32_t *wcnt, 
     if (nt <= 0) return;
     hipExtLaunchKernelGGL(k_wscan, dim3(1), dim3(kBS), 0, s.s, s.e0, nullptr, 0, wcnt, nt, wpre);
     hipExtLaunchKernelGGL(k_evict_compact, dim3(nt), dim3(kBS), 0, s.s, nullptr, s.e1, 0, dst, st, (const int64_t *)wpre, W);
+}
+void launch_pos_rebuild(int32_t *pos, const int32_t *queue, const int32_t *qfree, int64_t off, int64_t n, Stream st) {
+    if (n > 0)
+        hipExtLaunchKernelGGL(k_pos_rebuild, dim3(cdiv(n, kBS)), dim3(kBS), 0, st.s, st.e0, st.e1, 0, pos, queue, qfree,
+                              off, n);
 }
 void launch_emit_win(const TickArgs &a, int grid, Stream st) {
     hipExtLaunchKernelGGL(k_emit_win, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
