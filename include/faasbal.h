@@ -120,7 +120,12 @@ int fb_tick_launch(fb_ctx *ctx, double now, double tte, int32_t n_events, const 
  * while the device runs tick t (double-buffered pinned staging):
  * fb_tick_stage validates and copies the events (same rules and errors as
  * fb_tick_launch; no device work), fb_tick_launch_staged enqueues the tick on
- * the staged events with the stage's `now`.  fb_tick_launch = stage + launch. */
+ * the staged events with the stage's `now`.  fb_tick_launch = stage + launch.
+ * Events already in pinned memory (fb_host_alloc) are copied as they are and, on
+ * one-GPU heartbeat contexts, checked by the tick's first kernel instead of the
+ * host: an invalid message (slot, kind, timestamp) then fails fb_tick_wait with
+ * FB_EINVAL naming it, and nothing is committed.  Pinned arrays must stay
+ * unchanged until their tick was waited for. */
 int fb_tick_stage(fb_ctx *ctx, double now, int32_t n_events, const uint8_t *kind, const int32_t *slot,
                   const int32_t *val, const double *ts, const int64_t *seq);
 int fb_tick_launch_staged(fb_ctx *ctx, double tte, int64_t n_pending);
