@@ -151,6 +151,7 @@ struct fb_ctx {
     // k_emit_win: per front / back list entry, the committed position of the queued slot it
     // moved (-1: none), read by the tick's commit
     int32_t *tomb = nullptr;
+    int32_t *bad_min = nullptr;  // device word: first invalid message of a device-checked batch (0x7f7f7f7f: none)
     unsigned long long *wlb = nullptr;  // k_emit_win's look-back granules
     uint32_t *wticket = nullptr;
     uint32_t *lpart = nullptr, *wpart = nullptr;
@@ -221,6 +222,9 @@ struct fb_ctx {
     // the host only to name an offending event), and those of the launched tick
     const void *st_chk[3] = {nullptr, nullptr, nullptr};
     const void *l_chk[3] = {nullptr, nullptr, nullptr};
+    // device-resident batches (fb_tick_stage of arrays in this GPU's memory): read in place
+    bool st_res = false, l_res = false;
+    const void *st_dev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
     int stage_prof = 0;        // FAASBAL_STAGE_PROF=1: fb_tick_stage's time split to stderr
     double sprof[4] = {0, 0, 0, 0};
     int sprof_n = 0;
@@ -798,6 +802,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_head = c->ev_head;
         ea.ev_next = c->ev_next;
         ea.check_ev = c->l_chk[0] != nullptr;
+        ea.bad_min = c->bad_min;
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         ea.link = c->link;
         ea.hout = c->hout_dev;
@@ -1221,6 +1226,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->st, W);
     ap.add(&c->trash, (size_t)kTrashRows * kBS);
     ap.add(&c->dmask, (W + 63) / 64);
+    ap.add(&c->bad_min, (size_t)64);
     ap.add(&c->post, W);
     ap.add(&c->ev_status, E);
     for (int i = 0; i < 2; ++i) {
@@ -1308,6 +1314,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->oA, 128);
     }
     int rc = arena_commit(c, ap);
+    if (!rc && hipMemset(c->bad_min, 0x7f, 4) != hipSuccess) rc = fail(c, FB_EHIP, "hipMemset(bad_min) failed");
     if (!rc && getenv_int("FAASBAL_PRINT_ARENA"))  // diagnostics: placement of the arena
         fprintf(stderr, "faasbal arena %p, %zu bytes\n", c->arena, c->arena_bytes);
     if (!rc) {
@@ -1782,18 +1789,46 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     // that uses them has been waited for.
     using clk = std::chrono::steady_clock;
     const auto tp0 = clk::now();
-    bool direct = E > 0;
+    bool direct = E > 0, resident = E > 0;
     if (direct) {
         const void *ptrs[5] = {kind, slot, val, ts, seq};
-        for (int j = 0; j < 5 && direct; ++j) {
+        int nhost = 0, ndev = 0, n = 0;
+        for (int j = 0; j < 5; ++j) {
             if (!ptrs[j]) continue;  // seq may be NULL: filled with -1 on the device
+            ++n;
             hipPointerAttribute_t at;
-            if (hipPointerGetAttributes(&at, ptrs[j]) != hipSuccess || at.type != hipMemoryTypeHost) {
+            if (hipPointerGetAttributes(&at, ptrs[j]) != hipSuccess) {
                 (void)hipGetLastError();
-                direct = false;
+            } else if (at.type == hipMemoryTypeHost) {
+                ++nhost;
+            } else if (at.type == hipMemoryTypeDevice && at.device == c->device) {
+                ++ndev;
             }
         }
+        direct = nhost == n;
+        resident = ndev == n;
+        if (ndev && !resident) return fail(c, FB_EINVAL, "event arrays mix this GPU's memory with other memory");
     }
+    if (resident) {
+        // a batch already in this GPU's memory (e.g. parsed there, or staged ahead): the
+        // tick reads it in place and its first kernel checks it (an invalid message is
+        // overwritten with a harmless one and fb_tick_wait names it); no host pass
+        if (!(c->ev_head && c->ev_ll))
+            return fail(c, FB_EINVAL, "device-resident messages need a one-GPU heartbeat context");
+        c->st_dev[0] = kind;
+        c->st_dev[1] = slot;
+        c->st_dev[2] = val;
+        c->st_dev[3] = ts;
+        c->st_dev[4] = seq;
+        c->st_res = true;
+        c->st_chk[0] = c->st_chk[1] = c->st_chk[2] = kind;  // device-checked (names come from bad_min)
+        c->staged = true;
+        c->st_E = E;
+        c->st_vmax = 0;
+        c->st_now = now;
+        return FB_OK;
+    }
+    c->st_res = false;
     // pinned inputs: their H2D copies go out first and overlap the validation below (a
     // batch that fails validation is never launched, so copying it first is harmless)
     bool copied = false;
@@ -1909,12 +1944,25 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     HIPCHK(c, hipSetDevice(c->device));
     const int E = c->st_E;
     const int half = c->stage_half ^ 1;
-    if (E) HIPCHK(c, hipStreamWaitEvent(c->stream, c->stage_ev[half], 0));  // the staged copies
-    c->ev_kind = c->evk[half];
-    c->ev_slot = c->evsl[half];
-    c->ev_val = c->evv[half];
-    c->ev_ts = c->evt[half];
-    c->ev_seq = c->evq[half];
+    c->l_res = E && c->st_res;
+    if (c->l_res) {
+        c->ev_kind = (uint8_t *)c->st_dev[0];
+        c->ev_slot = (int32_t *)c->st_dev[1];
+        c->ev_val = (int32_t *)c->st_dev[2];
+        c->ev_ts = (double *)c->st_dev[3];
+        c->ev_seq = (int64_t *)c->st_dev[4];
+        if (!c->ev_seq) {  // -1 for every message
+            HIPCHK(c, hipMemsetAsync(c->evq[half], 0xff, (size_t)E * 8, c->stream));
+            c->ev_seq = c->evq[half];
+        }
+    } else {
+        if (E) HIPCHK(c, hipStreamWaitEvent(c->stream, c->stage_ev[half], 0));  // the staged copies
+        c->ev_kind = c->evk[half];
+        c->ev_slot = c->evsl[half];
+        c->ev_val = c->evv[half];
+        c->ev_ts = c->evt[half];
+        c->ev_seq = c->evq[half];
+    }
     c->stage_half = half;
     c->staged = false;
     const double now = c->st_now;
@@ -1983,6 +2031,15 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             // the batch was left to the device's check: name the first offending event; the
             // tick is not committed (its launch read only committed state)
             c->launched = false;
+            if (c->l_res) {
+                // a device-resident batch: the first offending message's index from the device
+                int32_t bi = 0x7f7f7f7f;
+                const int32_t none = 0x7f7f7f7f;
+                HIPCHK(c, hipMemcpy(&bi, c->bad_min, 4, hipMemcpyDeviceToHost));
+                HIPCHK(c, hipMemcpy(c->bad_min, &none, 4, hipMemcpyHostToDevice));
+                return fail(c, FB_EINVAL, "event %d: invalid message (slot outside [0, %d), unknown kind, or a "
+                            "timestamp decreasing or past now)", bi, c->W);
+            }
             const uint8_t *k = (const uint8_t *)c->l_chk[0];
             const int32_t *sl = (const int32_t *)c->l_chk[1];
             const double *ts = (const double *)c->l_chk[2];

@@ -224,6 +224,7 @@ struct EvArgs {
     // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
     uint32_t *wpart;
     int check_ev;               // k_ev_link checks the messages (host-unchecked pinned batches)
+    int32_t *bad_min;           // k_ev_link: the first invalid message's index (atomicMin; reset by the host)
     unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
     int wlb_n;                  // zeroed here
     uint32_t *wticket;

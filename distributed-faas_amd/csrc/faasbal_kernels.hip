@@ -922,7 +922,10 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
             const uint8_t k = a.ev_kind[t];
             const double tt = a.ev_ts[t], tp = a.ev_ts[t > 0 ? t - 1 : 0];
             const bool bad_sk = s >= (uint32_t)a.W || k > kEvOther;
-            if (bad_sk || !(tt <= a.now) || tt < tp) a.hout->bad_ev = 1;
+            if (bad_sk || !(tt <= a.now) || tt < tp) {
+                a.hout->bad_ev = 1;
+                if (a.bad_min) atomicMin(a.bad_min, t);
+            }
             if (bad_sk) {
                 s = 0;
                 a.ev_slot[t] = 0;

@@ -192,6 +192,27 @@ class GpuBalancer:
         self._chk(self.lib.fb_tick_stage(self.h, float(now), E, _p(k), _p(s), _p(v), _p(t), _p(q)))
         self._staged_E = E
 
+    def stage_device(self, now, ev_kind, ev_slot, ev_val, ev_ts, ev_seq=None):
+        """Stage a batch already in this GPU's memory (torch tensors on the context's
+        device: uint8 / int32 / int32 / float64 / int64): the tick reads it in place and
+        its first kernel checks it (an invalid message is overwritten with a harmless one
+        and wait() raises naming it).  The tensors must stay unchanged until that tick
+        was waited for."""
+        import torch
+        want = ((ev_kind, torch.uint8), (ev_slot, torch.int32), (ev_val, torch.int32), (ev_ts, torch.float64),
+                (ev_seq, torch.int64))
+        E = int(ev_kind.numel())
+        ptrs = []
+        for t, dt in want:
+            if t is None:
+                ptrs.append(None)
+                continue
+            if t.dtype != dt or not t.is_cuda or not t.is_contiguous() or t.numel() != E:
+                raise ValueError("device batch: contiguous %s tensors of %d elements on the GPU expected" % (dt, E))
+            ptrs.append(C.c_void_p(t.data_ptr()) if E else None)
+        self._chk(self.lib.fb_tick_stage(self.h, float(now), E, *ptrs))
+        self._staged_E = E
+
     def launch_staged(self, tte, n_pending=0):
         """Enqueue the tick on the events of the last stage() (its `now`)."""
         self._chk(self.lib.fb_tick_launch_staged(self.h, float(tte), int(n_pending)))

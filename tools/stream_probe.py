@@ -17,12 +17,19 @@ if "--pinned" in sys.argv:  # as bench.py: messages in pinned memory, staging on
     for tk in ticks:
         (tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"]) = g.pin_events(
             tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
+if "--resident" in sys.argv:  # as bench.py's value: every batch in HBM before the loop
+    import torch
+    for tk in ticks:
+        tk["dev"] = [torch.from_numpy(np.ascontiguousarray(tk[k])).to("cuda:0")
+                     for k in ("ev_kind", "ev_slot", "ev_val", "ev_ts", "ev_seq")]
 carried = 0
 acc = np.zeros(5)
 pc = time.perf_counter
 
 
 def stage(tk):
+    if "dev" in tk:
+        return g.stage_device(tk["now"], *tk["dev"])
     g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
 
 
