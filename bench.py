@@ -190,6 +190,7 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
 
         def start():
             g.load(st)
+            g.set_eager_commit(not args.no_eager)  # every tick is waited for and committed
             carried[0] = 0
             torch.cuda.synchronize()
             stage(ticks[0])
@@ -438,6 +439,8 @@ def main():
                          "configs[4], committed ticks with churn and 64K results each against 1M workers")
     ap.add_argument("--events", choices=("hbm", "pinned", "pageable"), default="hbm",
                     help="stream workload, one GPU: where each tick's message batch is when its tick starts")
+    ap.add_argument("--no-eager", action="store_true",
+                    help="stream workload: commit window ticks after the wait, not eagerly on the device")
     ap.add_argument("--no-pcie-pass", action="store_true",
                     help="stream workload: skip the PCIe-inclusive (pinned batches) pass beside the value")
     ap.add_argument("--pageable-events", action="store_true",

@@ -154,6 +154,7 @@ struct fb_ctx {
     int32_t *bad_min = nullptr;  // device word: first invalid message of a device-checked batch (0x7f7f7f7f: none)
     unsigned long long *wlb = nullptr;  // k_emit_win's look-back granules
     uint32_t *wticket = nullptr;
+    int64_t *cw = nullptr;  // commit word of the launched tick (device; eager commits read it)
     uint32_t *lpart = nullptr, *wpart = nullptr;
     int64_t win_slack = 8192;  // window positions scanned beyond the tasks' estimate (grows on a miss)
     int64_t last_O = 0;
@@ -173,6 +174,9 @@ struct fb_ctx {
     CommitArgs cm{};
     int cm_grid = 0;
     int commit_now = -1;       // FAASBAL_COMMIT_NOW: 1 never defer, 0 always, -1 window ticks' at once (A/B knob)
+    int eager = 0;             // fb_set_eager_commit: window ticks commit on the device right behind the tick
+    bool l_eager = false;      // the launched tick's eager commit is enqueued (until a rerun cancels it)
+    int spin = 1;              // FAASBAL_WAIT_SPIN=0: waits block in hipStreamSynchronize instead of polling
     PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
     uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
@@ -211,6 +215,8 @@ struct fb_ctx {
     int d2h_kernel = 1;                                 // FAASBAL_D2H_KERNEL=0: readbacks by hipMemcpyAsync
     int fork = 0;                                       // FAASBAL_FORK=1: the side stream (measured slower)
     hipEvent_t stage_ev[2] = {nullptr, nullptr};        // copies of half h done (on cp_s)
+    hipEvent_t tick_ev = nullptr;                       // an eagerly committed tick's last kernel done
+    bool tick_ev_set = false;                           // ... signalled by that kernel's launch itself
     hipEvent_t use_ev[2] = {nullptr, nullptr};          // the tick reading device half h done
     bool stage_rec[2] = {false, false}, use_rec[2] = {false, false};
     int stage_half = 1;        // half of the last launch's copies
@@ -359,6 +365,16 @@ size_t arena_skew(int i) {
     return on ? (size_t)(i % 16) * 4352 : 0;
 }
 
+// The host's wait for the context stream: polled (a tick is tens of microseconds; a
+// blocking wait's wake-up was measured at ~20 us per tick, tools/stream_timeline.sh)
+static hipError_t stream_wait(fb_ctx *c) {
+    if (!c->spin) return hipStreamSynchronize(c->stream);
+    for (;;) {
+        const hipError_t e = hipStreamQuery(c->stream);
+        if (e != hipErrorNotReady) return e;
+    }
+}
+
 int arena_commit(fb_ctx *c, ArenaPlan &ap) {
     size_t total = 0;
     int i = 0;
@@ -425,7 +441,7 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
         size_t cap = std::max(need, c->table_cap * 2);
         if (cap > ((size_t)1 << 31))
             return fail(c, FB_ERANGE, "round table of %zu entries (R=%d rows x %d blocks) exceeds the limit", need, R, nbq);
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, stream_wait(c));
         if (c->table_owned) {
             hipFree(c->qcnt);
             hipFree(c->qpre);
@@ -440,7 +456,7 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
         c->table_owned = true;
     }
     if (R > c->R_cap) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, stream_wait(c));
         if (c->A_owned) hipFree(c->A);
         c->A = nullptr;
         int rc;
@@ -452,7 +468,7 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
     // arena holds them for 128 rows; wider sharded tables get their own, grown the same way
     if (c->shard && need > c->seg_cap) {
         const size_t cap = std::max(need, c->seg_cap * 2);
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, stream_wait(c));
         if (c->seg_owned) {
             hipFree(c->segcnt);
             hipFree(c->osegcnt);
@@ -470,7 +486,7 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
         c->seg_owned = true;
     }
     if (c->shard && R > c->oA_cap) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, stream_wait(c));
         if (c->oA_owned) hipFree(c->oA);
         c->oA = nullptr;
         int rc;
@@ -535,7 +551,7 @@ int win_read(fb_ctx *c, std::vector<int32_t> &q, std::vector<int32_t> &f, std::v
 // general tick leaves): for readers of the device view.
 int win_normalize(fb_ctx *c) {
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     std::vector<int32_t> q, f;
     std::vector<double> h;
     int64_t n = 0;
@@ -563,7 +579,7 @@ int win_normalize(fb_ctx *c) {
 int win_alloc(fb_ctx *c) {
     if (c->win_cap) return FB_OK;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     const size_t W = (size_t)c->W_cap, E = (size_t)c->E_cap, Wq = (size_t)c->Wq_cap;
     const size_t qcap = 2 * Wq + 2 * E + 4096;
     auto r256 = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -831,6 +847,7 @@ int enqueue_tick(fb_ctx *c) {
             ea.wlb = c->wlb;
             ea.wlb_n = 2 * (int)cdiv(E, kWinCh) + c->l_nchW;
             ea.wticket = c->wticket;
+            ea.cw = c->cw;
         }
         ea.wcnt = c->wcnt;
         ea.grp = a.grp_on ? a.grp : nullptr;
@@ -1035,7 +1052,7 @@ int enqueue_tick(fb_ctx *c) {
         // synchronises the device
         const size_t need = (size_t)4 * (nbw + nbf + nbq) * 16 + 16;
         if (need > c->dbg_n) {
-            HIPCHK(c, hipStreamSynchronize(c->stream));
+            HIPCHK(c, stream_wait(c));
             hipFree(c->dbg);
             c->dbg = nullptr;
             const size_t cap = std::max(need, 2 * c->dbg_n);
@@ -1064,6 +1081,8 @@ int enqueue_tick(fb_ctx *c) {
         a.nchW = c->l_nchW;
         a.wlb = c->wlb;
         a.wticket = c->wticket;
+        a.cw = c->cw;
+        a.cw_tag = c->link;
         a.wpart = c->wpart;
         a.pos_in = c->pos_of[qc];
         a.tomb = c->tomb;
@@ -1077,7 +1096,10 @@ int enqueue_tick(fb_ctx *c) {
         }
         {
             Timer t(c, "emit");
-            launch_emit_win(a, nch, t.st());
+            // an eager commit follows: the launch's own completion signal is the event the
+            // host waits for (a separate event record between the two kernels cost ~6 us)
+            c->tick_ev_set = !c->timing && c->eager && c->commit_now < 0 && c->reruns == 0;
+            launch_emit_win(a, nch, c->tick_ev_set ? Stream(c->stream, nullptr, c->tick_ev) : t.st());
         }
         HIPCHK(c, hipGetLastError());
         return FB_OK;
@@ -1226,6 +1248,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     ap.add(&c->st, W);
     ap.add(&c->trash, (size_t)kTrashRows * kBS);
     ap.add(&c->dmask, (W + 63) / 64);
+    ap.add(&c->cw, (size_t)8);
     ap.add(&c->bad_min, (size_t)64);
     ap.add(&c->post, W);
     ap.add(&c->ev_status, E);
@@ -1355,6 +1378,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
             hipEventCreateWithFlags(&c->use_ev[h], hipEventDisableTiming) != hipSuccess)
             rc = FB_EHIP;
     if (!rc && hipStreamCreateWithFlags(&c->cp_s, hipStreamNonBlocking) != hipSuccess) rc = FB_EHIP;
+    if (!rc && hipEventCreateWithFlags(&c->tick_ev, hipEventDisableTiming) != hipSuccess) rc = FB_EHIP;
     if (!rc && (hipStreamCreateWithFlags(&c->side_s, hipStreamNonBlocking) != hipSuccess ||
                 hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess))
@@ -1378,6 +1402,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         if (c->tbitsb[p] && hipMemset(c->tbitsb[p], 0, (W + 31) / 32 * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc) c->tbits = c->tbitsb[c->tick & 1];
     if (!rc && getenv("FAASBAL_COMMIT_NOW")) c->commit_now = atoi(getenv("FAASBAL_COMMIT_NOW"));
+    if (!rc && getenv("FAASBAL_WAIT_SPIN")) c->spin = atoi(getenv("FAASBAL_WAIT_SPIN"));
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
@@ -1436,6 +1461,7 @@ int fb_destroy(fb_ctx *c) {
         if (c->stage_ev[h]) hipEventDestroy(c->stage_ev[h]);
         if (c->use_ev[h]) hipEventDestroy(c->use_ev[h]);
     }
+    if (c->tick_ev) hipEventDestroy(c->tick_ev);
     if (c->cp_s) hipStreamDestroy(c->cp_s);
     if (c->side_s) {
         hipStreamSynchronize(c->side_s);
@@ -1488,7 +1514,7 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
         epv[s] = epoch ? epoch[s] : 0u;
     }
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     c->cur = 0;
     c->qcur = 0;
     c->qoff = 0;
@@ -1565,7 +1591,7 @@ int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, doubl
     if (!c) return FB_EINVAL;
     if (int rc_ = flush_commit(c)) return rc_;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     const size_t W = (size_t)c->W;
     if (W) {
         if (registered) HIPCHK(c, hipMemcpy(registered, c->reg, W, hipMemcpyDeviceToHost));
@@ -1638,7 +1664,7 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
         epv[s] = epoch ? epoch[s] : 0u;
     }
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     c->cur = 0;
     c->qcur = 0;
     c->qoff = 0;
@@ -1685,7 +1711,7 @@ int fb_read_inflight(fb_ctx *c, uint32_t *inflight) {
     if (int rc_ = flush_commit(c)) return rc_;
     if (!c->bud) return fail(c, FB_ESTATE, "in-flight counts exist on one-GPU heartbeat contexts only");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     const size_t W = (size_t)c->W;
     if (!W) return FB_OK;
     std::vector<int32_t> bud(W);
@@ -1703,7 +1729,7 @@ int fb_read_shard_log(fb_ctx *c, uint32_t *log_seq, int64_t *log_len, int64_t *l
     if (int rc_ = flush_commit(c)) return rc_;
     if (!c->shard) return fail(c, FB_ESTATE, "fb_read_shard_log on a one-GPU context");
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     if (log_seq && c->head_local)
         HIPCHK(c, hipMemcpy(log_seq, c->lseq, (size_t)c->head_local * 4, hipMemcpyDeviceToHost));
     if (log_len) *log_len = c->head_local;
@@ -1715,7 +1741,7 @@ int fb_bind_exchange(fb_ctx *c, void *device_buffer, int64_t bytes) {
     if (!c) return FB_EINVAL;
     if (!c->shard) return fail(c, FB_ESTATE, "fb_bind_exchange on a one-GPU context");
     if (bytes < 0 || (bytes && !device_buffer)) return fail(c, FB_EINVAL, "exchange buffer");
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     c->xbuf = (uint8_t *)device_buffer;
     c->xcap = bytes;
     return FB_OK;
@@ -1734,7 +1760,7 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
 int fb_set_stream(fb_ctx *c, void *stream) {
     if (!c) return FB_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     c->stream = stream ? (hipStream_t)stream : c->own_s;
     return FB_OK;
 }
@@ -1937,9 +1963,13 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     return FB_OK;
 }
 
+static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid);
+
 int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     if (!c) return FB_EINVAL;
     if (!c->staged) return fail(c, FB_ESTATE, "fb_tick_launch_staged without fb_tick_stage");
+    if (c->launched && c->l_eager)
+        return fail(c, FB_ESTATE, "the last tick was committed eagerly: fb_tick_wait and fb_tick_commit first");
     if (n_pending < 0) return fail(c, FB_EINVAL, "n_pending < 0");
     HIPCHK(c, hipSetDevice(c->device));
     const int E = c->st_E;
@@ -1993,6 +2023,18 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->hout->bad_ev = 0;  // set by k_ev_link when it finds an invalid message
     const int rc = enqueue_tick(c);
     if (rc) return rc;
+    c->l_eager = false;
+    if (c->eager && c->l_win && c->commit_now < 0) {
+        // eager: the window tick's commit right behind it on the stream; it commits only
+        // if the tick finished as a window tick (fb_tick_wait reruns it otherwise)
+        int grid = 0;
+        const CommitArgs a = commit_args(c, true, grid);
+        if (!c->tick_ev_set) HIPCHK(c, hipEventRecord(c->tick_ev, c->stream));  // fb_tick_wait waits for the tick, not its commit
+        Timer t(c, "commit");
+        launch_commit(a, grid, t.st());
+        HIPCHK(c, hipGetLastError());
+        c->l_eager = true;
+    }
     if (E) {
         // the next copy into this device half waits for the tick's reads (a rerun in
         // fb_tick_wait reads it again, but no stage can target this half before then)
@@ -2025,9 +2067,25 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     if (!c->launched) return fail(c, FB_ESTATE, "fb_tick_wait without fb_tick_launch");
     if (c->shard && c->phase != 2) return fail(c, FB_ESTATE, "sharded tick: exchange, then fb_tick_continue");
     HIPCHK(c, hipSetDevice(c->device));
-    for (;;) {
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+    for (bool first = true;; first = false) {
+        if (first && c->l_eager) {
+            // the tick's results are final when its last kernel is: the host goes on while
+            // the eager commit runs (the next launch queues behind it)
+            hipError_t e;
+            while ((e = hipEventQuery(c->tick_ev)) == hipErrorNotReady) {
+                if (!c->spin) {
+                    e = hipEventSynchronize(c->tick_ev);
+                    break;
+                }
+            }
+            HIPCHK(c, e);
+        } else {
+            HIPCHK(c, stream_wait(c));
+        }
+        // any rerun below cancels an eager commit (its kernel found the tick unfinished and
+        // committed nothing); the rerun's commit is the ordinary one
         if (c->l_chk[0] && c->hout->bad_ev) {
+            c->l_eager = false;
             // the batch was left to the device's check: name the first offending event; the
             // tick is not committed (its launch read only committed state)
             c->launched = false;
@@ -2052,6 +2110,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             return fail(c, FB_EINVAL, "invalid message in the batch");
         }
         if (c->l_used_ll && c->hout->resort) {
+            c->l_eager = false;
             // a slot got more messages than k_ev_apply_ll sorts in registers: the same
             // functional tick again, grouped by the radix sort
             if (c->reruns > 4) return fail(c, FB_EHIP, "event regrouping did not converge");
@@ -2063,6 +2122,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             continue;
         }
         if (c->l_win && (c->hout->status == 3 || c->hout->win_ovf)) {
+            c->l_eager = false;
             // the window tick could not finish inside its window (a fill level above 0, an
             // unserved front, a first unserved element past the scanned prefix, no room at
             // the tail): the same functional tick on the general path
@@ -2076,6 +2136,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             continue;
         }
         if (c->hout->status == 0) break;
+        c->l_eager = false;
         if (c->hout->status == 2)
             return fail(c, FB_ENOSPC, "in-flight log full: %lld entries + this tick's dispatches exceed %lld",
                         (long long)c->l_head, (long long)c->log_cap);
@@ -2120,58 +2181,76 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
     return FB_OK;
 }
 
+// The commit of the launched tick.  eager: built at launch, before the tick's results
+// exist -- the window's head and appended positions are read by the kernel from the
+// tick's results, and every orphan tile and appended position gets blocks (grid-stride).
+static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid) {
+    const int64_t n_orph = eager ? 0 : c->last.n_orphans_local;
+    CommitArgs a{};
+    a.W = c->W;
+    a.nbw = (int)cdiv(c->W, kBS);
+    a.tick = c->tick;
+    a.st = c->st;
+    a.touched = c->touched;
+    a.post = c->post;
+    a.tbits = c->tbits;
+    a.E = c->l_E;
+    a.reg = c->reg;
+    a.hb = c->hb;
+    a.epoch = c->epoch;
+    a.n_orph = n_orph;
+    a.orphans = c->orphans;
+    a.log_slot = c->log_slot;
+    a.lseq = c->lseq;
+    a.head_local = c->l_head_local;
+    a.shard = c->shard;
+    a.nbo = (int)cdiv(n_orph, kBS);
+    if (c->l_oseg && (n_orph > 0 || eager)) {  // per-tile segments: a wave per log tile
+        a.oseg = c->fcnt;
+        a.oseg_tiles = c->l_nbf;
+        a.nbo = (int)cdiv(c->l_nbf, kWaves);
+    }
+    a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
+    a.ev_clr = c->ev_clr;
+    a.bud = c->bud;
+    a.bud_next = c->bud_next;
+    if (c->l_win) {
+        // the window moves: positions of slots that left become tombstones, kept slots that
+        // got messages take their post-message counts, appended slots their positions
+        a.win = 1;
+        a.wq_tail = c->l_qoff + c->l_Qn;
+        if (eager) {
+            a.eager = c->cw;
+            a.cw_tag = c->link;
+            a.nbap = (int)std::min<int64_t>(1024, cdiv(2 * (int64_t)c->l_E + c->l_T, kBS) + 1);
+        } else {
+            const HostOut &p = *c->hout;
+            a.wq_head = p.win_head;
+            a.napp = p.win_head + p.new_qlen - a.wq_tail;
+            a.nbap = (int)cdiv(a.napp, kBS);
+        }
+        a.wq_buf = c->queue[c->qcur];
+        a.wqf = c->qfree[c->qcur];
+        a.wqh = c->qhb[c->qcur];
+        a.pos = c->pos_of[c->qcur];
+        a.tomb = c->tomb;
+        a.n_tomb = 2 * c->l_E;
+        a.post_rf = c->post_rf;
+    }
+    grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) : 0);
+    return a;
+}
+
 int fb_tick_commit(fb_ctx *c) {
     if (!c) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "fb_tick_commit without a waited tick");
     HIPCHK(c, hipSetDevice(c->device));
     const int64_t n_orph = c->last.n_orphans_local;
-    if (c->W > 0 || n_orph > 0 || (c->ev_clr && c->l_E > 0)) {
-        CommitArgs a{};
-        a.W = c->W;
-        a.nbw = (int)cdiv(c->W, kBS);
-        a.tick = c->tick;
-        a.st = c->st;
-        a.touched = c->touched;
-        a.post = c->post;
-        a.tbits = c->tbits;
-        a.E = c->l_E;
-        a.reg = c->reg;
-        a.hb = c->hb;
-        a.epoch = c->epoch;
-        a.n_orph = n_orph;
-        a.orphans = c->orphans;
-        a.log_slot = c->log_slot;
-        a.lseq = c->lseq;
-        a.head_local = c->l_head_local;
-        a.shard = c->shard;
-        a.nbo = (int)cdiv(n_orph, kBS);
-        if (c->l_oseg && n_orph > 0) {  // per-tile segments: a wave per log tile
-            a.oseg = c->fcnt;
-            a.oseg_tiles = c->l_nbf;
-            a.nbo = (int)cdiv(c->l_nbf, kWaves);
-        }
-        a.n_clr = c->ev_clr ? c->l_E : 0;  // one-GPU heartbeat: the results' completed entries
-        a.ev_clr = c->ev_clr;
-        a.bud = c->bud;
-        a.bud_next = c->bud_next;
-        if (c->l_win) {
-            // the window moves: positions of slots that left become tombstones, kept slots that
-            // got messages take their post-message counts, appended slots their positions
-            const HostOut &p = *c->hout;
-            a.win = 1;
-            a.wq_head = p.win_head;
-            a.wq_tail = c->l_qoff + c->l_Qn;
-            a.napp = p.win_head + p.new_qlen - a.wq_tail;
-            a.nbap = (int)cdiv(a.napp, kBS);
-            a.wq_buf = c->queue[c->qcur];
-            a.wqf = c->qfree[c->qcur];
-            a.wqh = c->qhb[c->qcur];
-            a.pos = c->pos_of[c->qcur];
-            a.tomb = c->tomb;
-            a.n_tomb = 2 * c->l_E;
-            a.post_rf = c->post_rf;
-        }
-        const int grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) : 0);
+    if (c->l_eager) {
+        // the device committed the tick right behind it (fb_tick_launch_staged)
+    } else if (c->W > 0 || n_orph > 0 || (c->ev_clr && c->l_E > 0)) {
+        int grid = 0;
+        const CommitArgs a = commit_args(c, false, grid);
         if (c->ev_head && c->ev_ll && c->commit_now != 1 && !(c->l_win && c->commit_now < 0)) {  // (by default a window tick's commit runs at once)
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
@@ -2183,6 +2262,7 @@ int fb_tick_commit(fb_ctx *c) {
             HIPCHK(c, hipGetLastError());
         }
     }
+    c->l_eager = false;
     c->cur = 1 - c->cur;
     // sharded: a tick that needed a wide table keeps it for the next one while the fill
     // level stays beyond the narrow table (no relaunch per tick)
@@ -2289,7 +2369,7 @@ static int evict_ready(fb_ctx *c) {
 static int copy_out(fb_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!bytes) return FB_OK;
     if (int rc = d2h(c, dst, src, bytes)) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     return FB_OK;
 }
 
@@ -2307,7 +2387,7 @@ int fb_get_orphans(fb_ctx *c, int64_t n, int64_t *dst) {
     if (n < 0 || n > c->last.n_orphans_local) return fail(c, FB_EINVAL, "orphan count");
     HIPCHK(c, hipSetDevice(c->device));
     if (int rc = orph_out(c, dst, n)) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     return FB_OK;
 }
 
@@ -2340,7 +2420,7 @@ int fb_get_outputs(fb_ctx *c, int32_t *assign, int64_t *orphans, int32_t *evicte
     } else if (evicted && c->last.n_evicted && (rc = d2h(c, evicted, c->evicted, (size_t)c->last.n_evicted * 4))) {
         return rc;
     }
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     return FB_OK;
 }
 
@@ -2354,6 +2434,13 @@ int fb_set_window(fb_ctx *c, int mode) {
         if (int rc = win_alloc(c)) return rc;
     }
     c->win = mode;
+    return FB_OK;
+}
+
+int fb_set_eager_commit(fb_ctx *c, int enable) {
+    if (!c) return FB_EINVAL;
+    if (c->launched && !c->waited) return fail(c, FB_ESTATE, "fb_set_eager_commit with a tick in flight");
+    c->eager = enable ? 1 : 0;
     return FB_OK;
 }
 
@@ -2472,7 +2559,7 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
     launch_copy_multi(m, Stream(c->stream));
     HIPCHK(c, hipGetLastError());
     if (orphans && !orph_done && (rc = orph_out(c, orphans, c->last.n_orphans_local))) return rc;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     return FB_OK;
 }
 
@@ -2622,7 +2709,7 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     v->orphans = orph_dense_dev(c);
     if (c->waited) {
         if (int rc = evict_ready(c)) return rc;
-        HIPCHK(c, hipStreamSynchronize(c->stream));
+        HIPCHK(c, stream_wait(c));
     }
     v->evicted = c->l_cout ? c->cout_ev : c->evicted;
     v->n_workers = c->W;
@@ -2641,7 +2728,7 @@ int fb_timing_read(fb_ctx *c, int32_t max_kernels, const char **names, double *t
                    int32_t *n_kernels) {
     if (!c) return FB_EINVAL;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     std::vector<const char *> nm;
     std::vector<double> ms;
     std::vector<int64_t> cnt;
@@ -2682,7 +2769,7 @@ int fb_selftest(fb_ctx *c, int32_t *errors) {
     for (uint32_t seed = 1; seed <= 8; ++seed) launch_selftest(d, seed * 7919u, c->stream);
     uint32_t h = 0;
     HIPCHK(c, hipMemcpyAsync(&h, d, 4, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     hipFree(d);
     *errors = (int32_t)h;
     return FB_OK;
@@ -2692,7 +2779,7 @@ int fb_selftest(fb_ctx *c, int32_t *errors) {
 int fb_debug_read(fb_ctx *c, unsigned long long *dst, int64_t n, int64_t *n_total) {
     if (!c) return FB_EINVAL;
     if (int rc_ = flush_commit(c)) return rc_;
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     if (n_total) *n_total = (int64_t)c->dbg_n;
     if (dst && n > 0) HIPCHK(c, hipMemcpy(dst, c->dbg, (size_t)std::min<int64_t>(n, c->dbg_n) * 8, hipMemcpyDeviceToHost));
     return FB_OK;
@@ -2702,7 +2789,7 @@ int fb_sync(fb_ctx *c) {
     if (!c) return FB_EINVAL;
     if (int rc_ = flush_commit(c)) return rc_;
     HIPCHK(c, hipSetDevice(c->device));
-    HIPCHK(c, hipStreamSynchronize(c->stream));
+    HIPCHK(c, stream_wait(c));
     return FB_OK;
 }
 

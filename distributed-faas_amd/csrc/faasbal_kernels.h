@@ -153,6 +153,11 @@ struct CommitArgs {
     const int32_t *tomb;       // committed positions of queued slots moved to the front / back
     int n_tomb;                // entries of tomb (-1: nothing to tombstone)
     const uint8_t *post_rf;
+    // non-null: an eager commit (enqueued behind its window tick before the host waited):
+    // it commits only if the tick finished as a window tick, with wq_head / napp from these
+    // results; nbap blocks walk the appended positions grid-stride
+    const int64_t *eager;      // the tick's commit word (TickArgs::cw)
+    int64_t cw_tag;            // its launch's link stamp: cw[0] == cw_tag means the tick failed
 };
 
 struct EvArgs {
@@ -228,6 +233,7 @@ struct EvArgs {
     unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
     int wlb_n;                  // zeroed here
     uint32_t *wticket;
+    int64_t *cw;                // commit word {failed: link stamp, window head, window length} (null: none)
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -321,6 +327,8 @@ struct TickArgs {
     int nchB, nchF, nchW;
     unsigned long long *wlb;     // look-back granules: [0, nchB) the back chain, then the front / window chain
     uint32_t *wticket;           // chunk tickets (zeroed by k_ev_link)
+    int64_t *cw;                 // commit word {failed, window head, window length} (eager commits)
+    int64_t cw_tag;              // failures store this launch's link stamp into cw[0]
     uint32_t *lpart;             // k_logscan: orphans per log workgroup
     int n_lpart;
     uint32_t *wpart;             // evictions / live queued slots, 64 partials (EvArgs::wpart)

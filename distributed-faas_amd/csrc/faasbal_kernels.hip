@@ -786,14 +786,16 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 }
 
 // ------------------------------------------------------------ commit
-__device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
+// wq_head / napp: the window's new head and appended positions (a.wq_head / a.napp, or
+// read from the tick's results by an eager commit)
+__device__ __forceinline__ void commit_body(const CommitArgs &a, int blk, int64_t wq_head, int64_t napp) {
     const int nclr = (a.n_clr + kBS - 1) / kBS;
     if (a.win && blk >= a.nbw + a.nbo + nclr) {
         const int rb = blk - a.nbw - a.nbo - nclr;
         if (rb < a.nbap) {
             // window tick: the slot at each appended position has its position there
-            const int64_t i = (int64_t)rb * kBS + threadIdx.x;
-            if (i < a.napp) a.pos[a.wq_buf[a.wq_tail + i]] = (int32_t)(a.wq_tail + i);
+            for (int64_t i = (int64_t)rb * kBS + threadIdx.x; i < napp; i += (int64_t)a.nbap * kBS)
+                a.pos[a.wq_buf[a.wq_tail + i]] = (int32_t)(a.wq_tail + i);
             return;
         }
         // the committed positions of queued slots a front / back insertion moved (recorded
@@ -801,7 +803,7 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
         const int64_t j = (int64_t)(rb - a.nbap) * kBS + threadIdx.x;
         if (j < a.n_tomb) {
             const int32_t p = a.tomb[j];
-            if (p >= a.wq_head && p < a.wq_tail) a.wqf[p] = kTomb;
+            if (p >= wq_head && p < a.wq_tail) a.wqf[p] = kTomb;
         }
         return;
     }
@@ -849,7 +851,7 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
             const int qs = t ? (a.post_rf[s] >> 2) & 3 : kQsKeep;
             if (!(stt & kStAlive) || qs == kQsOut || qs == kQsKeep) {
                 const int32_t p = a.pos[s];  // exact for a queued slot
-                if (p >= a.wq_head && p < a.wq_tail) {
+                if (p >= wq_head && p < a.wq_tail) {
                     if (!(stt & kStAlive) || qs == kQsOut) {
                         a.wqf[p] = kTomb;
                     } else {
@@ -877,7 +879,19 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk) {
 
 __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
     prefetch_args(a);
-    commit_body(a, blockIdx.x);
+    int64_t wq_head = a.wq_head, napp = a.napp;
+    if (a.eager) {
+        // enqueued behind the window tick before the host waited for it: the tick's commit
+        // word (device memory: {failed, window head, window length}; a failure -- written by
+        // k_ev_link, k_ev_apply_ll or k_emit_win -- stores the launch's link stamp, so the
+        // word is never cleared) says whether it finished as a window tick -- if not,
+        // nothing is committed and the host reruns it -- and where the window moved
+        const int64_t *cw = a.eager;
+        if (cw[0] == a.cw_tag) return;
+        wq_head = cw[1];
+        napp = cw[1] + cw[2] - a.wq_tail;
+    }
+    commit_body(a, blockIdx.x, wq_head, napp);
 }
 
 // ------------------------------------------------------------ event grouping without a sort
@@ -895,7 +909,7 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
     prefetch_args(a);
     const int lb = (int)gridDim.x - a.cm_blocks;  // link blocks; the rest commit the previous tick
     if ((int)blockIdx.x >= lb) {
-        commit_body(a.cm, (int)blockIdx.x - lb);
+        commit_body(a.cm, (int)blockIdx.x - lb, a.cm.wq_head, a.cm.napp);
         return;
     }
     const int t = blockIdx.x * kBS + (int)threadIdx.x, nt = lb * kBS;
@@ -924,6 +938,7 @@ __global__ __launch_bounds__(kBS) void k_ev_link(EvArgs a) {
             const bool bad_sk = s >= (uint32_t)a.W || k > kEvOther;
             if (bad_sk || !(tt <= a.now) || tt < tp) {
                 a.hout->bad_ev = 1;
+                if (a.cw) a.cw[0] = a.link;
                 if (a.bad_min) atomicMin(a.bad_min, t);
             }
             if (bad_sk) {
@@ -1095,6 +1110,7 @@ __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t 
     }
     if (!done) {  // too many messages for the registers: the host reruns through the sort
         a.hout->resort = 1;
+        if (a.cw) a.cw[0] = a.link;
         return false;
     }
     // sort the messages into arrival order (bitonic network, static register indices;
@@ -2963,6 +2979,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 // N - 1 reports where the next window starts and how long it is.  A tick that is not a
 // window tick after all -- an unserved front, or no unserved live element inside the
 // scanned prefix -- is flagged (win_ovf) and the host reruns it on the general path.
+// the tick cannot finish as a window tick: the host's flag and the device word an eager
+// commit reads (device memory; the host-mapped results are too slow to read per block)
+__device__ __forceinline__ void win_fail(const TickArgs &a) {
+    a.hout->win_ovf = 1;
+    a.cw[0] = a.cw_tag;
+}
 constexpr uint64_t kGrA = (1ull << 22) - 1, kGrM = (1ull << 18) - 1;
 __device__ __forceinline__ uint64_t gr_pack(uint32_t st, uint32_t lv, uint32_t g1, uint32_t mx) {
     return ((uint64_t)st << 62) | ((uint64_t)(mx < kGrM ? mx : kGrM) << 44) | ((uint64_t)g1 << 22) | (uint64_t)lv;
@@ -3098,31 +3120,34 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
             xs[2] = eg1;
             xs[3] = LB;
             xs[4] = ok ? 1u : 0u;
-            if (!ok) a.hout->win_ovf = 1;
+            if (!ok) win_fail(a);
             if (ch == 0) {
                 a.hout->O = O;
                 a.hout->n_evicted = nev;
                 a.hout->cap_total = -1;  // beyond the scanned prefix (a window tick never needs it)
                 a.hout->L = 0;
                 a.hout->status = logfull ? 2 : 0;
+                if (logfull) win_fail(a);
                 a.hout->N_eff = logfull ? 0 : N;
                 a.hout->p = N;
             }
             if (ok && reg != 0) {
                 const int64_t inc = (int64_t)elv + tl;  // live fronts / window up to this chunk's end
                 // every front served: the last front chunk's total may not exceed N
-                if (ch == a.nchB + a.nchF - 1 && inc > N) a.hout->win_ovf = 1;
+                if (ch == a.nchB + a.nchF - 1 && inc > N) win_fail(a);
                 if (ci == nfw - 1) {
                     // the first unserved live element must lie in the scanned prefix
-                    if (inc <= N) a.hout->win_ovf = 1;
+                    if (inc <= N) win_fail(a);
                     a.hout->maxc = (int32_t)max(max(emx, bmx), bmax);
                     a.hout->AL = inc + LB;  // at least
                 }
                 if (ci == 0 && N == 0) {
                     a.hout->win_head = a.wq_off;
                     a.hout->new_qlen = a.wq_tail + LB - a.wq_off;
+                    a.cw[1] = a.wq_off;
+                    a.cw[2] = a.wq_tail + LB - a.wq_off;
                     a.hout->win_qlen = nq;
-                    if (a.wq_tail + LB - a.wq_off > a.q_cap) a.hout->win_ovf = 1;
+                    if (a.wq_tail + LB - a.wq_off > a.q_cap) win_fail(a);
                 }
             }
         }
@@ -3166,7 +3191,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
                 a.wqf_buf[pq] = x.raw;
                 a.wqh_buf[pq] = x.hb;
             } else {
-                a.hout->win_ovf = 1;
+                win_fail(a);
             }
             continue;
         }
@@ -3183,16 +3208,18 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
                 a.wqf_buf[pq] = x.raw - 1;
                 a.wqh_buf[pq] = x.hb;
             } else {
-                a.hout->win_ovf = 1;
+                win_fail(a);
             }
         }
         if (k == N - 1) {
             const int64_t head = reg == 2 ? i0 + j * kBS + tid + 1 : a.wq_off;
             a.hout->win_head = head;
             a.hout->new_qlen = a.wq_tail + LB + G - head;
+            a.cw[1] = head;
+            a.cw[2] = a.wq_tail + LB + G - head;
             a.hout->win_qlen = (int64_t)nq - (N - G);
             // the next window, tombstones included, must fit a general tick's position arrays
-            if (a.wq_tail + LB + G - head > a.q_cap) a.hout->win_ovf = 1;
+            if (a.wq_tail + LB + G - head > a.q_cap) win_fail(a);
         }
     }
 }

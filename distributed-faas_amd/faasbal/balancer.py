@@ -254,6 +254,11 @@ class GpuBalancer:
                 None if orphans is None else orphans[: r["n_orphans_local"]],
                 None if evicted is None else evicted[: r["n_evicted"]])
 
+    def set_eager_commit(self, on=True):
+        """Eager commits (fb_set_eager_commit): a window tick commits on the device right
+        behind itself; wait() and commit() are still called before the next launch."""
+        self._chk(self.lib.fb_set_eager_commit(self.h, 1 if on else 0))
+
     def set_window(self, mode=1):
         """Window ticks (fb_set_window): -1 auto (contexts of more than 128K workers), 0 off,
         1 whenever the last tick was at fill level 0.  Results are identical either way."""

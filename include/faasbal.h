@@ -186,6 +186,14 @@ int fb_set_compact(fb_ctx *ctx, int enable);
 int fb_set_window(fb_ctx *ctx, int mode);
 /* Committed window ticks, and launches that fell back to the general path. */
 int fb_window_stats(fb_ctx *ctx, int64_t *window_ticks, int64_t *fallbacks);
+/* Eager commits (a streaming loop that commits every tick it waits for): a window tick's
+ * commit is enqueued right behind it at launch and commits on the device as soon as the
+ * tick finishes -- if the tick finished as a window tick; otherwise it commits nothing and
+ * fb_tick_wait reruns the tick on the general path as usual.  The host still calls
+ * fb_tick_wait and fb_tick_commit (which then only does the host's bookkeeping) before the
+ * next launch; a tick so launched cannot be relaunched uncommitted, and state reads
+ * between its wait and commit see the committed state.  Default off.  Between ticks only. */
+int fb_set_eager_commit(fb_ctx *ctx, int enable);
 int fb_get_outputs_compact(fb_ctx *ctx, int32_t *slot, uint8_t *c, int64_t cap, int64_t *n_pos, int64_t *orphans,
                            int32_t *evicted);
 int fb_expand_compact(fb_ctx *ctx, const int32_t *slot, const uint8_t *c, int64_t n_pos, int32_t *assign);

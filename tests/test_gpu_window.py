@@ -11,16 +11,17 @@ the general path.  Window mode is forced on small contexts (fb_set_window(1)); t
 import numpy as np
 import pytest
 
-from faasbal import GpuBalancer, synth
+from faasbal import GpuBalancer, FaasbalError, synth
 from oracle import Oracle
 
 pytestmark = pytest.mark.gpu
 
 
-def _pair(st, log_cap, max_events, window=1, purge_mode=1):
+def _pair(st, log_cap, max_events, window=1, purge_mode=1, eager=False):
     W = len(st["reg"])
     g = GpuBalancer(W, log_cap, max_events=max_events)
     g.set_window(window)
+    g.set_eager_commit(eager)
     g.load(st)
     o = Oracle(W, log_cap, purge_mode=purge_mode)
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
@@ -47,15 +48,17 @@ def _stream(seed, W, T, dt, n_ticks, hb_frac=0.01, join_frac=0.002):
     return st, ticks
 
 
+@pytest.mark.parametrize("eager", [False, True])
 @pytest.mark.parametrize("seed,W,T,dt", [(0, 8192, 512, 0.5), (1, 8192, 1024, 0.6), (2, 4096, 256, 0.5),
                                          (3, 20000, 2048, 0.05), (4, 8192, 64, 0.3)])
-def test_window_stream_vs_oracle(seed, W, T, dt):
+def test_window_stream_vs_oracle(seed, W, T, dt, eager):
     """configs[4]'s event mix at reduced size: results of in-flight tasks, joins (moved
     to the front), heartbeats (kept in place, refreshed at commit), expiry by the clock
-    (tombstones); most ticks run as window ticks."""
+    (tombstones); most ticks run as window ticks.  eager: each window tick's commit is
+    enqueued behind it at launch (fb_set_eager_commit)."""
     st, ticks = _stream(seed, W, T, dt, n_ticks=10)
     E = max(len(t["ev_kind"]) for t in ticks)
-    g, o = _pair(st, 3 * len(st["log"]) + 20 * T + 16, max_events=E, purge_mode=2)
+    g, o = _pair(st, 3 * len(st["log"]) + 20 * T + 16, max_events=E, purge_mode=2, eager=eager)
     carried = 0
     for t, tk in enumerate(ticks):
         n = carried + tk["n_new"]
@@ -69,7 +72,7 @@ def test_window_stream_vs_oracle(seed, W, T, dt):
 
 
 @pytest.mark.parametrize("seed", range(24))
-def test_window_random_vs_oracle(seed):
+def test_window_random_vs_oracle(seed, eager=False):
     """Every message kind and edge case of the random scenarios (register 0 / -1 of a
     queued worker, reconnects, unknown ids, repeated results, deaths between a slot's
     own messages) with window mode on; task counts vary so ticks alternate between
@@ -80,7 +83,7 @@ def test_window_random_vs_oracle(seed):
                                  max_new=[40, 150, 600, 4000][(seed // 9) % 3 + (seed % 2)])
     st = dict(reg=scen["init_reg"], free=scen["init_free"], hb=scen["init_hb"], epoch=scen["init_epoch"],
               queue=scen["init_queue"], log=scen["init_log"])
-    g, o = _pair(st, 2 * len(scen["init_log"]) + 60000, max_events=4096)
+    g, o = _pair(st, 2 * len(scen["init_log"]) + 60000, max_events=4096, eager=eager)
     carried = 0
     for t, tk in enumerate(scen["ticks"]):
         log = o.export()["log"]
@@ -180,4 +183,38 @@ def test_window_stream_deferred_commits(seed, W, T, dt):
         carried = n + len(b["orphans"]) - len(b["assign"])
     _cmp(g, o, a, b, len(ticks) - 1)
     assert g.window_stats()[0] >= 5
+    g.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 24, 3))
+def test_window_random_eager_vs_oracle(seed):
+    """The random scenarios with eager commits: fallbacks, reruns through the sort and
+    general ticks must leave the eagerly enqueued commit without effect."""
+    test_window_random_vs_oracle(seed, eager=True)
+
+
+def test_eager_tick_cannot_be_relaunched_uncommitted():
+    """An eagerly committed tick must be waited for and committed before the next launch
+    (a tick committed the ordinary way may still be relaunched uncommitted)."""
+    st, ticks = _stream(10, 8192, 512, 0.3, n_ticks=4)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g, o = _pair(st, 2 * len(st["log"]) + 8 * 512 + 16, max_events=E, purge_mode=2, eager=True)
+    carried, raised = 0, 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a = g.tick(*args, commit=False)
+        try:
+            g.launch(*args)
+        except FaasbalError as e:
+            assert "eagerly" in str(e)
+            raised += 1
+        else:
+            a2 = g.wait()
+            assert a2["n_assigned"] == a["result"]["n_assigned"]
+        g.commit()
+        b = o.tick(*args)
+        _cmp(g, o, a, b, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert raised >= 2
     g.close()

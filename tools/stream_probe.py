@@ -6,6 +6,8 @@ import os, sys, time
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "distributed-faas_amd"))
 import numpy as np
+if "--resident" in sys.argv:  # torch before the library (one HIP runtime per process)
+    import torch  # noqa: F401
 from faasbal import GpuBalancer, synth
 
 W, T, K = 1 << 20, 65536, 30
@@ -13,6 +15,8 @@ st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
 ticks = synth.stream_ticks(st, n_ticks=K + 6, seed=2, tasks_per_tick=T, results_per_tick=T)
 g = GpuBalancer(W, len(st["log"]) + (K + 8) * 2 * T, max_events=max(len(t["ev_kind"]) for t in ticks), device=0)
 g.load(st)
+if "--eager" in sys.argv:
+    g.set_eager_commit(True)
 if "--pinned" in sys.argv:  # as bench.py: messages in pinned memory, staging only validates
     for tk in ticks:
         (tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"]) = g.pin_events(

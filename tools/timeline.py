@@ -2,7 +2,7 @@
 streaming probe into a median per-tick timeline: every device event of the tick in
 order with its start relative to the tick's k_ev_link, its duration, the idle gap
 before it, and the host call that enqueued it (start relative to the same origin);
-then the HIP API time per function and tick.  Usage: timeline.py TRACE_DIR"""
+then the HIP API time per function and tick.  Usage: timeline.py TRACE_DIR [ANCHOR_KERNEL]"""
 import csv
 import glob
 import os
@@ -27,7 +27,7 @@ def short(n):
     return n[:28]
 
 
-def main(d):
+def main(d, anchor="k_ev_link"):
     ev = []
     for r in rows(d, "*kernel_trace.csv"):
         ev.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"]), r["Correlation_Id"]))
@@ -37,7 +37,7 @@ def main(d):
     api = rows(d, "*hip_api_trace.csv")
     byc = {r["Correlation_Id"]: r for r in api}
     ev.sort()
-    starts = [i for i, e in enumerate(ev) if e[2].startswith("k_ev_link")]
+    starts = [i for i, e in enumerate(ev) if e[2].startswith(anchor)]
     if len(starts) < 4:
         print("fewer than 4 ticks in the trace")
         return
@@ -93,4 +93,4 @@ def main(d):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], *sys.argv[2:3])
