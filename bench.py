@@ -355,7 +355,7 @@ def host_observed(g, st, T, steps, n_assigned):
     r = g.wait()
     buf = g.pinned(max(n_assigned, 1), np.int32)
     obuf = g.pinned(max(len(st["log"]), 1), np.int64)  # room for every in-flight entry (fb_set_compact_out)
-    ebuf = g.pinned(max(int(r["n_evicted"]), 1), np.int32)
+    ebuf = g.pinned(max(len(st["reg"]), 1), np.int32)  # room for every worker (fb_set_compact_out)
     cap = Q + 16
     sbuf, cbuf = g.pinned(cap, np.int32), g.pinned(cap, np.uint8)
 

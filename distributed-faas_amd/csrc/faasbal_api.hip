@@ -818,6 +818,9 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_head = c->ev_head;
         ea.ev_next = c->ev_next;
         ea.check_ev = c->l_chk[0] != nullptr;
+#ifdef FAASBAL_STAMPS
+        ea.dbg = c->dbg;
+#endif
         ea.bad_min = c->bad_min;
         if (++c->link == 0) c->link = 1;  // a fresh stamp per launch, reruns included
         ea.link = c->link;
@@ -2035,7 +2038,7 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
         HIPCHK(c, hipGetLastError());
         c->l_eager = true;
     }
-    if (E) {
+    if (E && !c->l_res) {  // (a device-resident batch used no half)
         // the next copy into this device half waits for the tick's reads (a rerun in
         // fb_tick_wait reads it again, but no stage can target this half before then)
         HIPCHK(c, hipEventRecord(c->use_ev[half], c->stream));

@@ -234,6 +234,7 @@ struct EvArgs {
     int wlb_n;                  // zeroed here
     uint32_t *wticket;
     int64_t *cw;                // commit word {failed: link stamp, window head, window length} (null: none)
+    unsigned long long *dbg;    // diagnostic stamps (FAASBAL_STAMPS builds; null until the first tick allocated them)
 };
 
 // one argument block for k_scan / k_plan / k_emit

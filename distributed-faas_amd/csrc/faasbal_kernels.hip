@@ -1016,8 +1016,27 @@ __device__ __forceinline__ bool SlotRun::purge(const EvArgs &a, uint32_t s, int 
 __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t s, int e, int hidx, int kind0,
                                           int32_t val0, double ts0, int64_t seq0, int reg0, bool &ev);
 
+#ifdef FAASBAL_STAMPS
+// entry: thread 0's stamps; exit: the block's last thread (realtime, atomicMax into slot 14)
+#define APPLY_STAMP(slot)                                   \
+    do {                                                    \
+        if (a.dbg) STAMP(a, 0, slot);                       \
+    } while (0)
+#define APPLY_EXIT()                                                                                  \
+    do {                                                                                              \
+        if (a.dbg) atomicMax(&a.dbg[blockIdx.x * 16 + 14], (unsigned long long)__builtin_amdgcn_s_memrealtime()); \
+    } while (0)
+#else
+#define APPLY_STAMP(slot) \
+    do {                  \
+    } while (0)
+#define APPLY_EXIT() \
+    do {             \
+    } while (0)
+#endif
 __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     prefetch_args(a);
+    APPLY_STAMP(0);
     const int nba = (int)gridDim.x - a.nbw;  // apply blocks; the rest purge untouched slots
     if ((int)blockIdx.x >= nba) {
         const int blk = (int)blockIdx.x - nba;
@@ -1048,10 +1067,14 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
             count_orphans(a, blk, nw);
             if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
         }
+        APPLY_EXIT();
         return;
     }
     const int e = blockIdx.x * kBS + threadIdx.x;
-    if (e >= a.E) return;
+    if (e >= a.E) {
+        APPLY_EXIT();
+        return;
+    }
     // slot, link and payload of this message in one load round
     const uint32_t s = (uint32_t)a.ev_slot[e];
     const int32_t nx = a.ev_next[e];
@@ -1059,7 +1082,10 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     const int32_t val0 = a.ev_val[e];
     const double ts0 = a.ev_ts[e];
     const int64_t seq0 = a.ev_seq[e];
-    if (nx >= 0) return;  // another message of this slot owns it
+    if (nx >= 0) {  // another message of this slot owns it
+        APPLY_EXIT();
+        return;
+    }
     // second round: the slot's head, its record and this message's log entry together
     const int hidx = (int)(uint32_t)a.ev_head[s];
     const int32_t logv0 = log_peek(a, seq0);
@@ -1080,6 +1106,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
         const uint32_t ne = (uint32_t)__popcll(__ballot(ev)), nq = (uint32_t)__popcll(__ballot(qd));
         if (lane_id() == (int)__builtin_ctzll(act)) count_wpart(a, (int)blockIdx.x * kWaves + wave_id(), ne, nq);
     }
+    APPLY_EXIT();
 }
 
 // A slot with several messages (k_ev_apply_ll): walk head -> ... -> e, restore arrival

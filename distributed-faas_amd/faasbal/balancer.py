@@ -273,15 +273,19 @@ class GpuBalancer:
     def set_compact_out(self, slot, c, orphans, evicted):
         """Register pinned arrays (``pinned()``) that fused ticks fill with their compact
         outputs while they run (fb_set_compact_out); ``outputs_compact`` into the same
-        arrays then copies nothing.  ``slot=None`` unregisters."""
+        arrays then copies nothing.  A tick uses them only if they fit its worst case --
+        slot / c: the queue + 2 x messages positions, orphans: the whole in-flight log,
+        evicted: every worker -- and copies otherwise.  ``slot=None`` unregisters."""
         if slot is None:
             self._chk(self.lib.fb_set_compact_out(self.h, None, None, 0, None, 0, None, 0))
+            self._cout = self._cout_args = None
             return
         if slot.dtype != np.int32 or c.dtype != np.uint8 or orphans.dtype != np.int64 or evicted.dtype != np.int32:
             raise ValueError("slot int32, c uint8, orphans int64, evicted int32")
         self._chk(self.lib.fb_set_compact_out(self.h, _p(slot), _p(c), min(len(slot), len(c)), _p(orphans),
                                               len(orphans), _p(evicted), len(evicted)))
         self._cout = (slot, c, orphans, evicted)  # keep them alive while registered
+        self._cout_args = (_p(slot), _p(c), min(len(slot), len(c)), _p(orphans), _p(evicted))
 
     def set_compact(self, on=True):
         """Ticks launched afterwards also write the compact assignment form (slot and
@@ -294,6 +298,13 @@ class GpuBalancer:
         plus orphans and evicted slots, one synchronisation; returns the filled views
         (slot, c, orphans, evicted).  ``expand(slot, c)`` gives the per-task slots."""
         r = self.last
+        cout = getattr(self, "_cout", None)
+        if cout is not None and slot is cout[0] and c is cout[1] and orphans is cout[2] and evicted is cout[3]:
+            # the registered arrays (the tick wrote them): one call, pointers made at registration
+            p0, p1, cap, p2, p3 = self._cout_args
+            n = C.c_int64()
+            self._chk(self.lib.fb_get_outputs_compact(self.h, p0, p1, cap, C.byref(n), p2, p3))
+            return slot[: n.value], c[: n.value], orphans[: r["n_orphans_local"]], evicted[: r["n_evicted"]]
         for a, n, dt in ((orphans, r["n_orphans_local"], np.int64), (evicted, r["n_evicted"], np.int32)):
             if a is not None and (len(a) < n or a.dtype != dt):
                 raise ValueError("output array too small or of the wrong type")

@@ -15,7 +15,7 @@ g.launch(1000.0, 10.0, n_pending=T)
 r = g.wait()
 Q = len(st["queue"])
 obuf = g.pinned(max(len(st["log"]), 1), np.int64)
-ebuf = g.pinned(max(int(r["n_evicted"]), 1), np.int32)
+ebuf = g.pinned(W, np.int32)
 sbuf, cbuf = g.pinned(Q + 16, np.int32), g.pinned(Q + 16, np.uint8)
 g.set_compact_out(sbuf, cbuf, obuf, ebuf)
 pc = time.perf_counter
