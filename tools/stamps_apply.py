@@ -16,7 +16,8 @@ st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
 ticks = synth.stream_ticks(st, n_ticks=K + 5, seed=2, tasks_per_tick=T, results_per_tick=T)
 E = max(len(t["ev_kind"]) for t in ticks)
 g = GpuBalancer(W, len(st["log"]) + (K + 8) * 2 * T, max_events=E,
-                lib_path=os.path.join(REPO, "distributed-faas_amd", "faasbal", "libfaasbal_stamps.so"))
+                lib_path=os.environ.get("FAASBAL_STAMPS_LIB") or
+                os.path.join(REPO, "distributed-faas_amd", "faasbal", "libfaasbal_stamps.so"))
 g.load(st)
 carried = 0
 res = []
