@@ -124,8 +124,11 @@ int fb_tick_launch(fb_ctx *ctx, double now, double tte, int32_t n_events, const 
  * Events already in pinned memory (fb_host_alloc) are copied as they are and, on
  * one-GPU heartbeat contexts, checked by the tick's first kernel instead of the
  * host: an invalid message (slot, kind, timestamp) then fails fb_tick_wait with
- * FB_EINVAL naming it, and nothing is committed.  Pinned arrays must stay
- * unchanged until their tick was waited for. */
+ * FB_EINVAL naming it, and nothing is committed.  Arrays in this GPU's memory (all of
+ * them; seq may be NULL) are not copied at all: the tick reads them in place and its
+ * first kernel checks them the same way (overwriting an invalid message with a harmless
+ * one); arrays mixing device and host memory are refused.  Pinned or device arrays
+ * must stay unchanged until their tick was waited for. */
 int fb_tick_stage(fb_ctx *ctx, double now, int32_t n_events, const uint8_t *kind, const int32_t *slot,
                   const int32_t *val, const double *ts, const int64_t *seq);
 int fb_tick_launch_staged(fb_ctx *ctx, double tte, int64_t n_pending);
