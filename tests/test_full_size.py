@@ -69,13 +69,16 @@ def _cmp(a, b, t):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("window", [-1, 0], ids=["auto", "general"])
-def test_gpu_stream_1m_workers_matches_oracle(window):
+@pytest.mark.parametrize("window,eager,resident", [(-1, False, False), (0, False, False), (-1, True, True)],
+                         ids=["auto", "general", "eager-resident"])
+def test_gpu_stream_1m_workers_matches_oracle(window, eager, resident):
     """configs[4] per GPU: 1M workers, 64K new tasks + 64K results + joins +
     heartbeats per tick, the clock advancing so silent workers expire; committed
     ticks, every output and the post-state compared with the oracle (heap purge).
     auto: level-0 ticks after the first run as window ticks; general:
-    every tick on the general path (fb_set_window(0))."""
+    every tick on the general path (fb_set_window(0)); eager-resident: as bench.py's
+    stream value runs it -- message batches in HBM, window commits enqueued behind
+    their ticks (fb_set_eager_commit)."""
     from faasbal import GpuBalancer
     from oracle import Oracle
     W, T = 1 << 20, 65536
@@ -86,6 +89,7 @@ def test_gpu_stream_1m_workers_matches_oracle(window):
     E = max(len(t["ev_kind"]) for t in ticks)
     g = GpuBalancer(W, cap, max_events=E, device=0)
     g.set_window(window)
+    g.set_eager_commit(eager)
     g.load(st)
     o = Oracle(W, cap, purge_mode=2)  # heap purge: per-event clocks over 1M slots
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
@@ -93,7 +97,19 @@ def test_gpu_stream_1m_workers_matches_oracle(window):
     for t, tk in enumerate(ticks):
         n = carried + tk["n_new"]
         args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
-        a = g.tick(*args)
+        if resident:
+            import torch
+            dev = [torch.from_numpy(np.ascontiguousarray(tk[k])).to("cuda:0")
+                   for k in ("ev_kind", "ev_slot", "ev_val", "ev_ts", "ev_seq")]
+            g.stage_device(tk["now"], *dev)
+            g.launch_staged(10.0, n)
+            r = g.wait()
+            a = dict(result=r, reconnect=g.event_status(), assign=g.assignments(), orphans=g.orphans(),
+                     evicted=g.evicted())
+            g.commit()
+            del dev
+        else:
+            a = g.tick(*args)
         b = o.tick(*args)
         _cmp(a, b, t)
         assert len(b["assign"]) > 0, "the stream must dispatch"
