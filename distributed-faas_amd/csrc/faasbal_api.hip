@@ -177,6 +177,8 @@ struct fb_ctx {
     int eager = 0;             // fb_set_eager_commit: window ticks commit on the device right behind the tick
     bool l_eager = false;      // the launched tick's eager commit is enqueued (until a rerun cancels it)
     int spin = 1;              // FAASBAL_WAIT_SPIN=0: waits block in hipStreamSynchronize instead of polling
+    int sparse_commit = 0;     // FAASBAL_SPARSE_COMMIT=1: window commits from the message owners (A/B knob; slower)
+    int slot_apply = 0;        // FAASBAL_SLOT_APPLY=1: touched slots applied in slot order by the slot blocks (A/B knob)
     PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
     uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
@@ -818,6 +820,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_head = c->ev_head;
         ea.ev_next = c->ev_next;
         ea.check_ev = c->l_chk[0] != nullptr;
+        ea.slot_apply = c->slot_apply;
 #ifdef FAASBAL_STAMPS
         ea.dbg = c->dbg;
 #endif
@@ -1406,6 +1409,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc) c->tbits = c->tbitsb[c->tick & 1];
     if (!rc && getenv("FAASBAL_COMMIT_NOW")) c->commit_now = atoi(getenv("FAASBAL_COMMIT_NOW"));
     if (!rc && getenv("FAASBAL_WAIT_SPIN")) c->spin = atoi(getenv("FAASBAL_WAIT_SPIN"));
+    if (!rc && getenv("FAASBAL_SPARSE_COMMIT")) c->sparse_commit = atoi(getenv("FAASBAL_SPARSE_COMMIT"));
+    if (!rc && getenv("FAASBAL_SLOT_APPLY")) c->slot_apply = atoi(getenv("FAASBAL_SLOT_APPLY"));
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
@@ -1966,7 +1971,7 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     return FB_OK;
 }
 
-static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid);
+static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid, bool at_once);
 
 int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     if (!c) return FB_EINVAL;
@@ -2031,7 +2036,7 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
         // eager: the window tick's commit right behind it on the stream; it commits only
         // if the tick finished as a window tick (fb_tick_wait reruns it otherwise)
         int grid = 0;
-        const CommitArgs a = commit_args(c, true, grid);
+        const CommitArgs a = commit_args(c, true, grid, true);
         if (!c->tick_ev_set) HIPCHK(c, hipEventRecord(c->tick_ev, c->stream));  // fb_tick_wait waits for the tick, not its commit
         Timer t(c, "commit");
         launch_commit(a, grid, t.st());
@@ -2187,7 +2192,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
 // The commit of the launched tick.  eager: built at launch, before the tick's results
 // exist -- the window's head and appended positions are read by the kernel from the
 // tick's results, and every orphan tile and appended position gets blocks (grid-stride).
-static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid) {
+static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid, bool at_once) {
     const int64_t n_orph = eager ? 0 : c->last.n_orphans_local;
     CommitArgs a{};
     a.W = c->W;
@@ -2239,8 +2244,16 @@ static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid) {
         a.tomb = c->tomb;
         a.n_tomb = 2 * c->l_E;
         a.post_rf = c->post_rf;
+        // a commit that runs before the next launch (not inside it): the tick's message
+        // lists are intact, so its touched slots come from their owners, not a 1M-slot sweep
+        if (at_once && c->l_used_ll && !c->l_resort && c->sparse_commit) {
+            a.owners = c->ev_next;
+            a.own_slot = c->ev_slot;
+            a.wcnt = c->wcnt;
+        }
     }
-    grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) + (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) : 0);
+    grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) +
+           (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) + (a.owners ? (int)cdiv(a.E, kBS) : 0) : 0);
     return a;
 }
 
@@ -2253,8 +2266,9 @@ int fb_tick_commit(fb_ctx *c) {
         // the device committed the tick right behind it (fb_tick_launch_staged)
     } else if (c->W > 0 || n_orph > 0 || (c->ev_clr && c->l_E > 0)) {
         int grid = 0;
-        const CommitArgs a = commit_args(c, false, grid);
-        if (c->ev_head && c->ev_ll && c->commit_now != 1 && !(c->l_win && c->commit_now < 0)) {  // (by default a window tick's commit runs at once)
+        const bool defer = c->ev_head && c->ev_ll && c->commit_now != 1 && !(c->l_win && c->commit_now < 0);
+        const CommitArgs a = commit_args(c, false, grid, !defer);
+        if (defer) {  // (by default a window tick's commit runs at once)
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
             c->cm_grid = grid;

@@ -156,6 +156,11 @@ struct CommitArgs {
     // non-null: an eager commit (enqueued behind its window tick before the host waited):
     // it commits only if the tick finished as a window tick, with wq_head / napp from these
     // results; nbap blocks walk the appended positions grid-stride
+    // sparse window commits (non-null owners): blocks after the tomb ones commit the slot
+    // of every message with owners[e] < 0 (k_ev_link's list heads: one per touched slot);
+    // the slot blocks then commit only untouched slots of tiles with evictions (wcnt)
+    const int32_t *owners, *own_slot;
+    const uint32_t *wcnt;
     const int64_t *eager;      // the tick's commit word (TickArgs::cw)
     int64_t cw_tag;            // its launch's link stamp: cw[0] == cw_tag means the tick failed
 };
@@ -229,6 +234,7 @@ struct EvArgs {
     // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
     uint32_t *wpart;
     int check_ev;               // k_ev_link checks the messages (host-unchecked pinned batches)
+    int slot_apply;             // k_ev_apply_ll: touched slots applied by the slot blocks, in slot order
     int32_t *bad_min;           // k_ev_link: the first invalid message's index (atomicMin; reset by the host)
     unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
     int wlb_n;                  // zeroed here

@@ -786,6 +786,46 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 }
 
 // ------------------------------------------------------------ commit
+// One slot's commit: t = the slot got messages this tick.
+__device__ __forceinline__ void commit_slot(const CommitArgs &a, int s, bool t, int64_t wq_head) {
+    const uint8_t stt = a.st[s];
+    if (a.win) {
+        // window tick: the committed position of a slot queued at tick start that the tick
+        // did not serve -- tombstoned when the slot died or its messages took it out of the
+        // queue, refreshed with its post-message free count and heartbeat when they kept it
+        // there (a queued slot that lives on untouched keeps its position as it is).  Slots
+        // moved to the front or the back were recorded by k_emit_win (the tomb list above):
+        // they may also be appended, so their pos is rewritten in this launch.
+        if ((stt & kStQ0) && (t || !(stt & kStAlive))) {
+            const int qs = t ? (a.post_rf[s] >> 2) & 3 : kQsKeep;
+            if (!(stt & kStAlive) || qs == kQsOut || qs == kQsKeep) {
+                const int32_t p = a.pos[s];  // exact for a queued slot
+                if (p >= wq_head && p < a.wq_tail) {
+                    if (!(stt & kStAlive) || qs == kQsOut) {
+                        a.wqf[p] = kTomb;
+                    } else {
+                        const PostRec pr = a.post[s];
+                        a.wqf[p] = pr.free;
+                        a.wqh[p] = pr.hb;
+                    }
+                }
+            }
+        }
+    }
+    // committed hb is NaN for slots without a record (k_scan's log role relies on it)
+    if (t) {
+        const bool alive = (stt & kStAlive) != 0;
+        const PostRec pr = a.post[s];
+        a.reg[s] = alive ? 1 : 0;
+        a.hb[s] = alive ? pr.hb : __builtin_nan("");
+        a.epoch[s] = pr.epoch;
+        if (a.bud) a.bud[s] = a.bud_next[s];
+    } else if (stt & kStEvicted) {
+        a.reg[s] = 0;
+        a.hb[s] = __builtin_nan("");
+    }
+}
+
 // wq_head / napp: the window's new head and appended positions (a.wq_head / a.napp, or
 // read from the tick's results by an eager commit)
 __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk, int64_t wq_head, int64_t napp) {
@@ -800,11 +840,19 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk, int64_
         }
         // the committed positions of queued slots a front / back insertion moved (recorded
         // by k_emit_win per list entry, before any position changed) become tombstones
-        const int64_t j = (int64_t)(rb - a.nbap) * kBS + threadIdx.x;
-        if (j < a.n_tomb) {
-            const int32_t p = a.tomb[j];
-            if (p >= wq_head && p < a.wq_tail) a.wqf[p] = kTomb;
+        const int ntb = (a.n_tomb + kBS - 1) / kBS;
+        if (rb < a.nbap + ntb) {
+            const int64_t j = (int64_t)(rb - a.nbap) * kBS + threadIdx.x;
+            if (j < a.n_tomb) {
+                const int32_t p = a.tomb[j];
+                if (p >= wq_head && p < a.wq_tail) a.wqf[p] = kTomb;
+            }
+            return;
         }
+        // sparse window commit: each slot that got messages, once -- by the message whose
+        // thread owned it in k_ev_apply_ll (the first in its linked list)
+        const int64_t e = (int64_t)(rb - a.nbap - ntb) * kBS + threadIdx.x;
+        if (a.owners && e < a.E && a.owners[e] < 0) commit_slot(a, a.own_slot[e], true, wq_head);
         return;
     }
     if (blk >= a.nbw + a.nbo) {
@@ -838,43 +886,15 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk, int64_
     }
     const int s = blk * kBS + threadIdx.x;
     if (s >= a.W) return;
-    const uint8_t stt = a.st[s];
-    if (a.win) {
-        // window tick: the committed position of a slot queued at tick start that the tick
-        // did not serve -- tombstoned when the slot died or its messages took it out of the
-        // queue, refreshed with its post-message free count and heartbeat when they kept it
-        // there (a queued slot that lives on untouched keeps its position as it is).  Slots
-        // moved to the front or the back were recorded by k_emit_win (the tomb list above):
-        // they may also be appended, so their pos is rewritten in this launch.
-        const bool t = a.E > 0 && got_msg(a, s);
-        if ((stt & kStQ0) && (t || !(stt & kStAlive))) {
-            const int qs = t ? (a.post_rf[s] >> 2) & 3 : kQsKeep;
-            if (!(stt & kStAlive) || qs == kQsOut || qs == kQsKeep) {
-                const int32_t p = a.pos[s];  // exact for a queued slot
-                if (p >= wq_head && p < a.wq_tail) {
-                    if (!(stt & kStAlive) || qs == kQsOut) {
-                        a.wqf[p] = kTomb;
-                    } else {
-                        const PostRec pr = a.post[s];
-                        a.wqf[p] = pr.free;
-                        a.wqh[p] = pr.hb;
-                    }
-                }
-            }
-        }
+    if (a.owners) {
+        // sparse window commit: the touched slots are the owners' (blocks above); a tile
+        // without evictions has nothing else to commit
+        if (a.wcnt[blk] == 0) return;
+        if (got_msg(a, s)) return;
+        commit_slot(a, s, false, wq_head);
+        return;
     }
-    // committed hb is NaN for slots without a record (k_scan's log role relies on it)
-    if (a.E > 0 && got_msg(a, s)) {
-        const bool alive = (stt & kStAlive) != 0;
-        const PostRec pr = a.post[s];
-        a.reg[s] = alive ? 1 : 0;
-        a.hb[s] = alive ? pr.hb : __builtin_nan("");
-        a.epoch[s] = pr.epoch;
-        if (a.bud) a.bud[s] = a.bud_next[s];
-    } else if (stt & kStEvicted) {
-        a.reg[s] = 0;
-        a.hb[s] = __builtin_nan("");
-    }
+    commit_slot(a, s, a.E > 0 && got_msg(a, s), wq_head);
 }
 
 __global__ __launch_bounds__(kBS) void k_commit(CommitArgs a) {
@@ -1015,6 +1035,47 @@ __device__ __forceinline__ bool SlotRun::purge(const EvArgs &a, uint32_t s, int 
 
 __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t s, int e, int hidx, int kind0,
                                           int32_t val0, double ts0, int64_t seq0, int reg0, bool &ev);
+__device__ __forceinline__ bool apply_touched(const EvArgs &a, uint32_t s, int hidx, bool &ev);
+
+// k_ev_apply_ll's slot blocks: the purge of untouched slots and (slot_apply) the
+// application of touched ones, one slot per thread, block blk = slots [256 blk, +256)
+__device__ __forceinline__ void apply_slot_block(const EvArgs &a, int blk) {
+    const int s = blk * kBS + (int)threadIdx.x;
+    bool died = false, evicted = false, queued = false;
+    bool qt = false, evt = false;  // a touched slot applied here: queued / evicted after its purge
+    uint32_t no = 0;
+    if (s < a.W) {
+        // the link stamp says whether the slot got messages (its owner purges it); the
+        // committed record loaded with it (no dependent round)
+        const bool t = (uint32_t)(a.ev_head[s] >> 32) == a.link;
+        const int reg0 = a.reg[s];
+        const double hb0 = a.hb[s];
+        const int2 fq0 = a.free_in[s];
+        const int32_t b0 = a.bud ? a.bud[s] : 0;
+        const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(b0 - fq0.x) : 0u;
+        bool alive;
+        if (!t) {
+            no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, fq0.y, in0, died, evicted, alive,
+                            queued);
+        } else if (a.slot_apply) {
+            // the slot's messages, applied by its thread in slot order: the records of
+            // the touched slots are read and written a wave's 64 slots at a time
+            // instead of in message order (SlotRun::purge counts its own eviction)
+            qt = apply_touched(a, (uint32_t)s, (int)(uint32_t)a.ev_head[s], evt);
+        }
+    }
+    const uint64_t dm = __ballot(died);
+    const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
+    const uint32_t nq = (uint32_t)__popcll(__ballot(queued || qt));
+    const uint32_t nea = ne + (uint32_t)__popcll(__ballot(evt));
+    const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
+    if (lane_id() == 0) {
+        if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
+        if (ne) count_evicted(a, blk, ne);
+        count_orphans(a, blk, nw);
+        if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), nea, nq);
+    }
+}
 
 #ifdef FAASBAL_STAMPS
 // entry: thread 0's stamps; exit: the block's last thread (realtime, atomicMax into slot 14)
@@ -1039,34 +1100,7 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     APPLY_STAMP(0);
     const int nba = (int)gridDim.x - a.nbw;  // apply blocks; the rest purge untouched slots
     if ((int)blockIdx.x >= nba) {
-        const int blk = (int)blockIdx.x - nba;
-        const int s = blk * kBS + (int)threadIdx.x;
-        bool died = false, evicted = false, queued = false;
-        uint32_t no = 0;
-        if (s < a.W) {
-            // the link stamp says whether the slot got messages (its owner purges it); the
-            // committed record loaded with it (no dependent round)
-            const bool t = (uint32_t)(a.ev_head[s] >> 32) == a.link;
-            const int reg0 = a.reg[s];
-            const double hb0 = a.hb[s];
-            const int2 fq0 = a.free_in[s];
-            const int32_t b0 = a.bud ? a.bud[s] : 0;
-            const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(b0 - fq0.x) : 0u;
-            bool alive;
-            if (!t)
-                no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, fq0.y, in0, died, evicted, alive,
-                                queued);
-        }
-        const uint64_t dm = __ballot(died);
-        const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
-        const uint32_t nq = (uint32_t)__popcll(__ballot(queued));
-        const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
-        if (lane_id() == 0) {
-            if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
-            if (ne) count_evicted(a, blk, ne);
-            count_orphans(a, blk, nw);
-            if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
-        }
+        apply_slot_block(a, (int)blockIdx.x - nba);
         APPLY_EXIT();
         return;
     }
@@ -1106,6 +1140,15 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
         const uint32_t ne = (uint32_t)__popcll(__ballot(ev)), nq = (uint32_t)__popcll(__ballot(qd));
         if (lane_id() == (int)__builtin_ctzll(act)) count_wpart(a, (int)blockIdx.x * kWaves + wave_id(), ne, nq);
     }
+    APPLY_EXIT();
+}
+
+// slot_apply: the slot blocks alone (touched slots applied in slot order), compiled
+// without k_ev_apply_ll's message-order path and its register budget
+__global__ __launch_bounds__(kBS) void k_ev_apply_slots(EvArgs a) {
+    prefetch_args(a);
+    APPLY_STAMP(0);
+    apply_slot_block(a, (int)blockIdx.x);
     APPLY_EXIT();
 }
 
@@ -1195,6 +1238,80 @@ __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t 
     return a.nbw ? r.purge(a, s, reg0, ev) : false;
 }
 
+
+// Slot-ordered application (k_ev_apply_ll's slot blocks, EvArgs::slot_apply): the thread
+// of touched slot s walks k_ev_link's list from its head (hidx) to the first message
+// (next < 0).  A single message (most slots) is applied with its payload loaded together
+// with its link; longer runs collect up to kLinkMax indices (a dependent load each),
+// sort them into arrival order and apply them, each payload loaded as it is applied.
+// Beyond kLinkMax the host reruns the tick through the sort.  Returns whether the slot
+// is queued after its purge; ev: evicted.
+__device__ __forceinline__ bool apply_touched(const EvArgs &a, uint32_t s, int hidx, bool &ev) {
+    SlotRun r;
+    r.init(a, s);
+    const int reg0 = r.reg;
+    const int32_t nx0 = a.ev_next[hidx];
+    const int kind0 = a.ev_kind[hidx];
+    const int32_t val0 = a.ev_val[hidx];
+    const double ts0 = a.ev_ts[hidx];
+    const int64_t seq0 = a.ev_seq[hidx];
+    if (nx0 < 0) {
+        r.step<true>(a, s, hidx, kind0, val0, ts0, seq0, log_peek(a, seq0));
+        r.finish(a, s, s);
+        return r.purge(a, s, reg0, ev);
+    }
+    int ix[kLinkMax];
+    int n = 1, cur = nx0;
+    bool done = false;
+#pragma unroll
+    for (int k = 0; k < kLinkMax; ++k) {
+        if (k == 0) {
+            ix[0] = hidx;
+            continue;
+        }
+        ix[k] = done ? INT32_MAX : cur;
+        if (!done) {
+            ++n;
+            const int32_t nx = a.ev_next[cur];
+            if (nx < 0) done = true;
+            else cur = nx;
+        }
+    }
+    if (!done) {  // too many messages for the registers: the host reruns through the sort
+        a.hout->resort = 1;
+        if (a.cw) a.cw[0] = a.link;
+        return false;
+    }
+#pragma unroll
+    for (int k = 2; k <= kLinkMax; k <<= 1)
+#pragma unroll
+        for (int j = k >> 1; j > 0; j >>= 1)
+#pragma unroll
+            for (int i = 0; i < kLinkMax; ++i)
+                if ((i ^ j) > i) {
+                    const int l = i ^ j;
+                    const bool sw = (i & k) == 0 ? (ix[i] > ix[l]) : (ix[i] < ix[l]);
+                    const int t = ix[i];
+                    ix[i] = sw ? ix[l] : t;
+                    ix[l] = sw ? t : ix[l];
+                }
+    uint32_t clr = 0;  // bit m: message m completed its entry
+#pragma unroll
+    for (int m = 0; m < kLinkMax; ++m) {
+        if (m < n) {
+            const int i = ix[m];
+            const int64_t q = a.ev_seq[i];
+            bool dup = false;
+#pragma unroll
+            for (int k = 0; k < m; ++k)
+                if ((clr >> k) & 1u) dup = dup || a.ev_seq[ix[k]] == q;
+            const bool cl = r.step<true>(a, s, i, a.ev_kind[i], a.ev_val[i], a.ev_ts[i], q, log_peek(a, q), dup);
+            clr |= cl ? (1u << m) : 0u;
+        }
+    }
+    r.finish(a, s, s);
+    return r.purge(a, s, reg0, ev);
+}
 
 // ------------------------------------------------------------ slot state
 
@@ -3780,7 +3897,11 @@ void launch_ev_link(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_link, dim3(grid + a.cm_blocks), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    // slot_apply: the slot blocks apply the touched slots too (no message blocks)
+    if (a.slot_apply && a.nbw)
+        hipExtLaunchKernelGGL(k_ev_apply_slots, dim3(a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    else
+        hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_copy_multi(const CopyMulti &m, Stream st) {
     if (m.n <= 0 && m.otiles <= 0) return;

@@ -197,7 +197,7 @@ class GpuBalancer:
         device: uint8 / int32 / int32 / float64 / int64): the tick reads it in place and
         its first kernel checks it (an invalid message is overwritten with a harmless one
         and wait() raises naming it).  The tensors must stay unchanged until that tick
-        was waited for."""
+        was committed."""
         import torch
         want = ((ev_kind, torch.uint8), (ev_slot, torch.int32), (ev_val, torch.int32), (ev_ts, torch.float64),
                 (ev_seq, torch.int64))

@@ -127,8 +127,9 @@ int fb_tick_launch(fb_ctx *ctx, double now, double tte, int32_t n_events, const 
  * FB_EINVAL naming it, and nothing is committed.  Arrays in this GPU's memory (all of
  * them; seq may be NULL) are not copied at all: the tick reads them in place and its
  * first kernel checks them the same way (overwriting an invalid message with a harmless
- * one); arrays mixing device and host memory are refused.  Pinned or device arrays
- * must stay unchanged until their tick was waited for. */
+ * one); arrays mixing device and host memory are refused.  Pinned arrays must stay
+ * unchanged until their tick was waited for, device arrays until it was committed (a
+ * window tick's commit reads the slots of its messages). */
 int fb_tick_stage(fb_ctx *ctx, double now, int32_t n_events, const uint8_t *kind, const int32_t *slot,
                   const int32_t *val, const double *ts, const int64_t *seq);
 int fb_tick_launch_staged(fb_ctx *ctx, double tte, int64_t n_pending);
