@@ -218,3 +218,21 @@ def test_eager_tick_cannot_be_relaunched_uncommitted():
         carried = n + len(b["orphans"]) - len(b["assign"])
     assert raised >= 2
     g.close()
+
+
+@pytest.fixture
+def slot_apply(monkeypatch):
+    """Touched slots applied in slot order by k_ev_apply_slots (FAASBAL_SLOT_APPLY=1)."""
+    monkeypatch.setenv("FAASBAL_SLOT_APPLY", "1")
+
+
+@pytest.mark.parametrize("seed,W,T,dt", [(0, 8192, 512, 0.5), (3, 20000, 2048, 0.05)])
+def test_window_stream_slot_apply(slot_apply, seed, W, T, dt):
+    test_window_stream_vs_oracle(seed, W, T, dt, eager=True)
+
+
+@pytest.mark.parametrize("seed", range(0, 24, 2))
+def test_window_random_slot_apply(slot_apply, seed):
+    """Every message kind, runs of several messages per slot (sorted into arrival order by
+    the slot's thread), repeated results, deaths between a slot's own messages."""
+    test_window_random_vs_oracle(seed)
