@@ -175,18 +175,27 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
             else:
                 g.stage(tk["now"], tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"])
 
-        def run(i):
-            # launch tick i on its staged messages, stage tick i+1's while the device runs
-            # tick i (double-buffered), then wait + commit
-            tk = ticks[i]
-            n = carried[0] + tk["n_new"]
+        def loop(i0, i1):
+            # ticks [i0, i1), tick i0's messages staged: launch tick i on its staged messages,
+            # stage tick i+1's while the device runs tick i (double-buffered), wait, commit,
+            # launch tick i+1 at once -- the bookkeeping of tick i comes after (off the path
+            # between one tick's end and the next one's first kernel)
+            out = []
+            n = carried[0] + ticks[i0]["n_new"]
             g.launch_staged(10.0, n)
-            if i + 1 < len(ticks):
-                stage(ticks[i + 1])
-            r = g.wait()
-            g.commit()
-            carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
-            return r
+            if i0 + 1 < len(ticks):
+                stage(ticks[i0 + 1])
+            for i in range(i0, i1):
+                r = g.wait()
+                g.commit()
+                carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
+                if i + 1 < i1:
+                    n = carried[0] + ticks[i + 1]["n_new"]
+                    g.launch_staged(10.0, n)
+                    if i + 2 < len(ticks):
+                        stage(ticks[i + 2])
+                out.append(r)
+            return out
 
         def start():
             g.load(st)
@@ -202,15 +211,13 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
             mode = "pinned"
             prep(mode)
             start()
-            for i in range(Wu):
-                run(i)
+            loop(0, Wu)
             g.sync()
             t0 = time.perf_counter()
-            na = 0
-            for i in range(Wu, Wu + K):
-                na += int(run(i)["n_assigned"])
+            rs = loop(Wu, Wu + K)
             g.sync()
             dtp = time.perf_counter() - t0
+            na = sum(int(r["n_assigned"]) for r in rs)
             pcie = {"value": na / dtp, "ms_per_step": dtp * 1e3 / K, "events_in": "pinned host memory, H2D copies "
                     "inside the timed region (tick i+1's overlapping tick i)"}
             for tk in ticks:
@@ -237,36 +244,36 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
             carried[0] = n + int(r["n_orphans"]) - int(r["n_assigned"])
             return r
 
+        def loop(i0, i1):
+            return [run(i) for i in range(i0, i1)]
+
     def barrier():
         if dist is not None:
             t = torch.zeros(1, device="cuda")
             dist.all_reduce(t)
             torch.cuda.synchronize()
 
-    for i in range(Wu):
-        run(i)
+    loop(0, Wu)
     g.sync()
     barrier()
     g.sync()
     t0 = time.perf_counter()
-    for i in range(Wu, Wu + K):
-        tk = ticks[i]
-        r = run(i)
-        stats["assigned"] += int(r["n_assigned"])
-        stats["orphans"] += int(r["n_orphans"])
-        stats["evicted"] += int(r["n_evicted"])  # sharded: this rank's evictions (summed below)
-        stats["events"] += len(tk["ev_kind"])
+    rs = loop(Wu, Wu + K)
     g.sync()
     barrier()
     dt = time.perf_counter() - t0
+    for i, r in zip(range(Wu, Wu + K), rs):
+        stats["assigned"] += int(r["n_assigned"])
+        stats["orphans"] += int(r["n_orphans"])
+        stats["evicted"] += int(r["n_evicted"])  # sharded: this rank's evictions (summed below)
+        stats["events"] += len(ticks[i]["ev_kind"])
     if dist is not None:
         t = torch.tensor([dt, float(stats["evicted"])], device="cuda", dtype=torch.float64)
         dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
         dist.all_reduce(t[1:])
         dt, stats["evicted"] = float(t[0].item()), int(t[1].item())
     g.timing_enable(True)
-    for i in range(Wu + K, len(ticks)):
-        run(i)
+    loop(Wu + K, len(ticks))
     kt = g.timing_read()
     g.timing_enable(False)
     wstats = g.window_stats() if world == 1 else (0, 0)
