@@ -1056,7 +1056,8 @@ int enqueue_tick(fb_ctx *c) {
     {
         // diagnostic stamp rows (stamps builds only); grown geometrically -- hipFree
         // synchronises the device
-        const size_t need = (size_t)4 * (nbw + nbf + nbq) * 16 + 16;
+        // (k_emit_win stamps rows from 8192 on, one per chunk)
+        const size_t need = std::max((size_t)4 * (nbw + nbf + nbq) * 16 + 16, (size_t)(8192 + kWinMaxCh) * 16);
         if (need > c->dbg_n) {
             HIPCHK(c, stream_wait(c));
             hipFree(c->dbg);

@@ -3130,6 +3130,7 @@ __device__ __forceinline__ void win_fail(const TickArgs &a) {
     a.cw[0] = a.cw_tag;
 }
 constexpr uint64_t kGrA = (1ull << 22) - 1, kGrM = (1ull << 18) - 1;
+constexpr int kWinStampRow = 8192;  // k_emit_win's diagnostic stamp rows (after k_ev_apply_ll's)
 __device__ __forceinline__ uint64_t gr_pack(uint32_t st, uint32_t lv, uint32_t g1, uint32_t mx) {
     return ((uint64_t)st << 62) | ((uint64_t)(mx < kGrM ? mx : kGrM) << 44) | ((uint64_t)g1 << 22) | (uint64_t)lv;
 }
@@ -3198,6 +3199,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
     __shared__ uint32_t wt[4][kWaves][2];
     __shared__ uint32_t xs[8];
     const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
+    STAMP(a, kWinStampRow, 0);
     if (tid == 0) xs[0] = atomicAdd(a.wticket, 1u);  // chunk = ticket: predecessors already run
     // the orphan partials of the log workgroups and the purge's eviction / queued partials
     const uint32_t op = tid < a.n_lpart ? a.lpart[tid] : 0u;
@@ -3226,6 +3228,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
             wt[j][w][1] = (uint32_t)__popcll(mg[j]);
         }
     }
+    STAMP(a, kWinStampRow, 1);
     {
         const uint32_t x0 = wave_sum_u32(op), x1 = wave_sum_u32(e0), x2 = wave_sum_u32(q0), x3 = wave_max_u32(cmx);
         if (lane == 0) {
@@ -3297,7 +3300,11 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
         }
     }
     lds_barrier();
-    if (!xs[4] || logfull) return;
+    STAMP(a, kWinStampRow, 2);
+    if (!xs[4] || logfull) {
+        STAMP(a, kWinStampRow, 15);
+        return;
+    }
     if (reg < 2) {
         // a queued slot moved to the front or the back: its committed position (read-only
         // during the tick) is tombstoned by the commit; one entry per list position
@@ -3309,7 +3316,10 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
     }
     const uint32_t lvx = xs[1], g1x = xs[2], LB = xs[3];
     const uint32_t blx = lvx;  // back chunks: their chain counts live backs
-    if (reg != 0 && (int64_t)lvx >= N) return;  // every element of the chunk stays put
+    if (reg != 0 && (int64_t)lvx >= N) {  // every element of the chunk stays put
+        STAMP(a, kWinStampRow, 15);
+        return;
+    }
     uint32_t bl = 0, bg = 0;  // elements of the earlier sub-rounds / waves
     int32_t *const q = a.wq_buf;
 #pragma unroll
@@ -3366,6 +3376,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
             if (a.wq_tail + LB + G - head > a.q_cap) win_fail(a);
         }
     }
+    STAMP(a, kWinStampRow, 15);
 }
 
 // ------------------------------------------------------------ k_emit_shard
