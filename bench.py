@@ -424,6 +424,52 @@ def host_observed(g, st, T, steps, n_assigned):
                     "the compact form into one slot per task"}
 
 
+def committed_tick(st, T, reps=10):
+    """The configs[2] tick with its commit.  A committed one-GPU tick defers its commit
+    (the evicted records' deletion, task_dispatcher.py:246-247, and its orphans' log
+    entries) into the next launch's first kernel; after an idle tick that is k_scan, so a
+    stream of committed configs[2]-shaped ticks is two launches per tick.  Measured on the
+    tick after a committed configs[2] tick (same state both times): its k_scan with the
+    folded commit, then relaunched uncommitted without it -- the difference is the commit's
+    device cost inside the step.  The commit as its own kernel (what a state read in
+    between forces) is timed beside it.  Packet-event device times, averages of `reps`."""
+    from faasbal import GpuBalancer
+    g = GpuBalancer(len(st["reg"]), 2 * len(st["log"]) + 2 * T + 16, max_events=1, device=0)
+    d_fold, d_plain, d_sep, d_emit = [], [], [], []
+    for _ in range(reps):
+        g.load(st)
+        g.launch(1000.0, 10.0, n_pending=T)
+        g.wait()
+        g.commit()  # deferred: the next launch's k_scan runs it
+        g.timing_enable(True)
+        g.launch(1000.0, 10.0, n_pending=T)
+        g.wait()
+        k1 = g.timing_read()
+        g.launch(1000.0, 10.0, n_pending=T)  # same tick, nothing left to fold
+        g.wait()
+        k2 = g.timing_read()
+        g.timing_enable(False)
+        if set(k1) != {"scan", "emit"}:
+            raise SystemExit("committed_tick: the folded commit did not ride in k_scan (%s)" % sorted(k1))
+        d_fold.append(k1["scan"][0])
+        d_plain.append(k2["scan"][0])
+        d_emit.append(k1["emit"][0])
+        # the same commit as its own launch
+        g.load(st)
+        g.launch(1000.0, 10.0, n_pending=T)
+        g.wait()
+        g.commit()
+        g.timing_enable(True)
+        g.sync()  # flushes the deferred commit as its own kernel
+        k3 = g.timing_read()
+        g.timing_enable(False)
+        d_sep.append(k3["commit"][0])
+    g.close()
+    return dict(scan_with_commit_ms=float(np.mean(d_fold)), scan_ms=float(np.mean(d_plain)),
+                emit_ms=float(np.mean(d_emit)), commit_in_scan_ms=float(np.mean(d_fold) - np.mean(d_plain)),
+                commit_kernel_ms=float(np.mean(d_sep)), launches_per_committed_tick=2)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -440,8 +486,9 @@ def main():
     ap.add_argument("--backend", default="nccl", help="torch.distributed backend for N > 1 (nccl = RCCL)")
     ap.add_argument("--mode", default="heartbeat", choices=("heartbeat", "deque"),
                     help="deque: the loop without heartbeats (PushDispatcher.start), one GPU")
-    ap.add_argument("--workload", default="tick", choices=("tick", "cfg3", "stream"),
-                    help="tick: configs[2] (N GPUs: weak scaling, N x 64K workers, N x 1M tasks); cfg3: configs[3], "
+    ap.add_argument("--workload", default="tick", choices=("tick", "weak", "cfg3", "stream"),
+                    help="tick: configs[2], 1M tasks x 64K workers (N GPUs: the same global table sharded N ways, "
+                         "strong scaling); weak: N x 64K workers and N x 1M tasks sharded N ways; cfg3: configs[3], "
                          "16M tasks x 1M workers (N GPUs: the same global table sharded, strong scaling); stream: "
                          "configs[4], committed ticks with churn and 64K results each against 1M workers")
     ap.add_argument("--events", choices=("hbm", "pinned", "pageable"), default="hbm",
@@ -496,16 +543,18 @@ def main():
 
     from faasbal import GpuBalancer, synth
 
-    # weak scaling: the pool grows with the GPUs.  N = 1 runs configs[2] on one
-    # table; N > 1 shards ONE global table of N x 64K workers / N x 1M tasks by
-    # worker-id range and runs the two-phase tick with the RCCL exchange
-    # all-reduce every step.
+    # configs[2] (the metric's config): ONE global table of 64K workers and 1M pending
+    # tasks, sharded by worker-id range over the N GPUs (strong scaling), the two-phase
+    # tick with the RCCL exchange all-reduce every step; --workload weak:
+    # N x 64K workers / N x 1M tasks (the pool grows with the GPUs)
     if args.workload == "cfg3":
         # configs[3]: one global table of 1M workers and 16M pending tasks, whatever N
         W = args.workers if args.workers != 65536 else 1 << 20
         T = args.tasks if args.tasks != 1_000_000 else 16_000_000
-    else:
+    elif args.workload == "weak":
         W, T = args.workers * world, args.tasks * world
+    else:
+        W, T = args.workers, args.tasks
     deque = args.mode == "deque"
     if deque and world > 1:
         raise SystemExit("--mode deque runs on one GPU (the start() loop has no sharded form)")
@@ -592,8 +641,7 @@ def main():
     kern = {k: (ms / n, n) for k, (ms, n) in kt.items()}
     # fused one-GPU heartbeat ticks (scan + emit only, W <= 128K slots): the emit's log
     # workgroups read the in-flight log and flag the orphans, k_scan has no log role
-    log_in_emit = (world == 1 and not deque and set(kern) == {"scan", "emit"} and W <= 1 << 17
-                   and os.environ.get("FAASBAL_F_EMIT", "1") != "0")
+    log_in_emit = world == 1 and not deque and set(kern) == {"scan", "emit"} and W <= 1 << 17
     dom = max((k for k in kern if k != "exchange_allreduce"), key=lambda k: kern[k][0])
     dom_ms = kern[dom][0]
     tick_dev_ms = sum(v[0] for k, v in kern.items() if k != "exchange_allreduce")
@@ -633,7 +681,7 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": dt * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "strong" if args.workload == "cfg3" else "weak",
+        "scaling": "weak" if args.workload == "weak" else "strong",
         "vs_baseline": None,
         "dtype": "int32",
         "data": "synthetic (faasbal.synth.%s, seed=0)" % ("uniform_state" if args.loads == "uniform" else "zipf_state"),
@@ -650,10 +698,10 @@ def main():
                                 "256, busy ~U[0,128)), %d orphans redistributed" % (T, W, O)) if args.loads == "uniform" else
                                ("configs[2]: one tick, %d pending tasks x %d workers, Zipf(1.5) loads cap 32, "
                                 "5%% dead -> %d orphans redistributed" % (T, W, O)) if world == 1 else
-                               ("configs[2] per GPU, weak: one global tick of %d tasks x %d workers sharded by "
-                                "worker-id range over %d GPUs, exchange all-reduce of %d B per tick (%s), "
-                                "%d orphans redistributed" % (T, W, world, kt_x_bytes,
-                                                              "RCCL" if args.backend == "nccl" else args.backend, O)),
+                               ("configs[2]%s: one global tick of %d tasks x %d workers sharded by worker-id range "
+                                "over %d GPUs, exchange all-reduce of %d B per tick (%s), %d orphans redistributed"
+                                % (" per GPU (weak)" if args.workload == "weak" else "", T, W, world, kt_x_bytes,
+                                   "RCCL" if args.backend == "nccl" else args.backend, O)),
                    "tasks_per_tick": T, "workers": W, "in_flight": F, "queue": Q,
                    "assigned_per_tick": n_assigned, "evicted": n_evicted,
                    "fill_level": int(res["fill_level"]),
@@ -679,6 +727,15 @@ def main():
             cpu_baseline(st, T, args.cpu_budget)
         if not deque:
             line["reference_python_value"] = REFERENCE_PYTHON
+    if world == 1 and not deque:
+        cm = committed_tick(st, T)
+        cm["device_ms_with_commit"] = tick_dev_ms + cm["commit_in_scan_ms"]
+        cm["ms_per_step_with_commit"] = dt * 1e3 / args.steps + cm["commit_in_scan_ms"]
+        cm["value_with_commit"] = n_assigned / (cm["ms_per_step_with_commit"] * 1e-3)
+        cm["note"] = ("the tick's commit folded into the next tick's k_scan (W role + orphan-clearing blocks): "
+                      "commit_in_scan_ms = k_scan with it - k_scan without it on the same state; "
+                      "ms_per_step_with_commit = ms_per_step + that")
+        line["committed"] = cm
     if world == 1 and not args.no_host_observed:
         line["host_observed"] = host_observed(g, st, T, min(args.steps, 50), n_assigned)
     if rank == 0:

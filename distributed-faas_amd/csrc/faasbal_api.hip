@@ -115,7 +115,6 @@ struct fb_ctx {
     int32_t *ev_clr = nullptr;
     uint32_t *ctag = nullptr;
     uint32_t lstamp = 0;               // per enqueued launch, reruns included (never 0)
-    int f_emit = 1;                    // FAASBAL_F_EMIT=0: fused ticks keep k_scan's log blocks (A/B knob)
     // f_emit ticks leave their orphans in per-tile segments (orphans[t*2048 + i], i < fcnt[t]);
     // the dense list is gathered into orph_dense when something reads it
     bool l_oseg = false, dense_ok = false;
@@ -142,7 +141,7 @@ struct fb_ctx {
     int qcur = 0;
     int64_t qoff = 0, qcap = 0, Qtrue = 0;  // Qtrue: the LRU queue's length (tombstones excluded)
     bool win_cap = false;      // the context can run window ticks (buffers allocated)
-    int win = -1;              // fb_set_window / FAASBAL_WINDOW: -1 auto (large tables), 0 off, 1 on
+    int win = -1;              // fb_set_window: -1 auto (large tables), 0 off, 1 on
     bool l_win = false;        // the last launch is a window tick
     int l_nchW = 0;            // ... and the window chunks it scans
     int64_t l_qoff = 0;
@@ -173,12 +172,8 @@ struct fb_ctx {
     bool cm_pending = false;
     CommitArgs cm{};
     int cm_grid = 0;
-    int commit_now = -1;       // FAASBAL_COMMIT_NOW: 1 never defer, 0 always, -1 window ticks' at once (A/B knob)
     int eager = 0;             // fb_set_eager_commit: window ticks commit on the device right behind the tick
     bool l_eager = false;      // the launched tick's eager commit is enqueued (until a rerun cancels it)
-    int spin = 1;              // FAASBAL_WAIT_SPIN=0: waits block in hipStreamSynchronize instead of polling
-    int sparse_commit = 0;     // FAASBAL_SPARSE_COMMIT=1: window commits from the message owners (A/B knob; slower)
-    int slot_apply = 0;        // FAASBAL_SLOT_APPLY=1: touched slots applied in slot order by the slot blocks (A/B knob)
     PostRec *post = nullptr;       // post-message records {hb, free, epoch} of touched slots
     uint8_t *post_rf = nullptr, *st = nullptr;
     unsigned long long *dmask = nullptr;
@@ -194,14 +189,9 @@ struct fb_ctx {
     unsigned long long *ev_head = nullptr;  // per slot {link stamp, last linked message}
     int32_t *ev_next = nullptr;             // per message
     uint32_t link = 0;                      // stamp of the last k_ev_link launch
-    int ev_ll = 1;                          // FAASBAL_EV_LL=0: always the radix sort (A/B knob)
+    int ev_ll = 1;                          // fb_set_path("ev_ll", 0): always the radix sort (test paths)
     bool l_resort = false;                  // this tick reruns through the sort (a slot had > kLinkMax messages)
     bool l_used_ll = false;                 // the last enqueue grouped by linked lists
-    int purge_apply = 1;
-    int cq_direct = 1;                      // FAASBAL_CQ_DIRECT=0: idle ticks copy c / hb through k_scan (A/B knob)
-    // A/B knobs read once at creation (not per launch): FAASBAL_SCAN_FFIRST,
-    // FAASBAL_POST_EAGER, FAASBAL_NO_ARENA32
-    int scan_ffirst = 0, post_eager = 0, no_arena32 = 0;                    // FAASBAL_PURGE_APPLY=0: the slot purge stays in k_scan (A/B knob)
     void *h_stage = nullptr;  // two pinned halves of E_cap events each (fb_tick_stage)
     // device event arrays, double-buffered like the pinned halves: fb_tick_stage copies
     // half h on its own stream (overlapping a running tick), the launch waits for it
@@ -210,12 +200,6 @@ struct fb_ctx {
     double *evt[2] = {nullptr, nullptr};
     int64_t *evq[2] = {nullptr, nullptr};
     hipStream_t cp_s = nullptr;                         // H2D copies of staged events
-    // k_logscan beside k_scan: both read only what k_ev_apply_ll's launch wrote (the
-    // died bitmap, the post-message records), k_plan2 waits for both
-    hipStream_t side_s = nullptr;
-    hipEvent_t fork_ev = nullptr, join_ev = nullptr;
-    int d2h_kernel = 1;                                 // FAASBAL_D2H_KERNEL=0: readbacks by hipMemcpyAsync
-    int fork = 0;                                       // FAASBAL_FORK=1: the side stream (measured slower)
     hipEvent_t stage_ev[2] = {nullptr, nullptr};        // copies of half h done (on cp_s)
     hipEvent_t tick_ev = nullptr;                       // an eagerly committed tick's last kernel done
     bool tick_ev_set = false;                           // ... signalled by that kernel's launch itself
@@ -233,9 +217,6 @@ struct fb_ctx {
     // device-resident batches (fb_tick_stage of arrays in this GPU's memory): read in place
     bool st_res = false, l_res = false;
     const void *st_dev[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
-    int stage_prof = 0;        // FAASBAL_STAGE_PROF=1: fb_tick_stage's time split to stderr
-    double sprof[4] = {0, 0, 0, 0};
-    int sprof_n = 0;
     // scan / plan / emit
     int32_t *c_arr = nullptr, *qbmax = nullptr, *qbm_raw = nullptr;
     unsigned long long *csum = nullptr;
@@ -250,7 +231,6 @@ struct fb_ctx {
     int64_t *qpre = nullptr, *A = nullptr;
     int64_t *A_rep = nullptr;     // k_plan2 path: per-group copies of A and the totals
     DevTotals *P_rep = nullptr;
-    int repl = 1;                 // FAASBAL_REPL=0: one shared copy (A/B knob)
     size_t table_cap = 0;  // entries of qcnt / qpre
     int R_cap = 0;         // entries of A
     int64_t *orphans = nullptr;
@@ -259,15 +239,13 @@ struct fb_ctx {
     HostOut *hout = nullptr, *hout_dev = nullptr;  // host-mapped results written by k_emit
     unsigned long long *dbg = nullptr;             // diagnostic stamps
     size_t dbg_n = 0;
-    int force_plan = 0;
-    int emit_cfirst = 0;  // FAASBAL_EMIT_CFIRST: k_emit2 grid order (A/B knob)
-    int rs_wide = 1;       // FAASBAL_RS_WIDE=0: 8-bit sort digits only (A/B knob)
-    int gplan = 1;         // FAASBAL_GPLAN=0: large k_emit2 tables through k_plan, not k_plan2 (A/B knob)
-    int rs_fuse = 0;       // FAASBAL_RS_FUSE=1: next-pass histograms from the scatters' atomics (A/B knob)
-    int logscan = -1;      // -1: auto (k_logscan for large tables when the bitmap fits in LDS)
+    // fb_set_path: the launch sequences of other table sizes on small (oracle-checkable)
+    // inputs (test paths)
+    int force_plan = 0;    // "plan": 1 the k_plan2 + k_emit2 path, 2 the chunked k_emit (R > 128)
+    int rs_wide = 1;       // "rs_wide": 0 8-bit sort digits only (the path past kRsWideMaxBlocks tiles)
+    int logscan = -1;      // "logscan": -1 auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
-    int split_slots = -1;  // -1: auto (separate k_slots launch once the records outgrow L2)
-    int dbg_stop = 0;      // FAASBAL_DBG_STOP=n: timing probe (results invalid)
+    int split_slots = -1;  // "split_slots": -1 auto (separate k_slots launch once the records outgrow L2)
     // deque contexts (fb_create_deque): PushDispatcher.start, task_dispatcher.py:251-322
     int deque = 0;
     int32_t *tokcnt[2] = {nullptr, nullptr}, *xw[2] = {nullptr, nullptr}, *kl[2] = {nullptr, nullptr};
@@ -333,10 +311,6 @@ int fail(fb_ctx *c, int code, const char *fmt, ...) {
     } while (0)
 
 inline int64_t cdiv(int64_t a, int64_t b) { return (a + b - 1) / b; }
-inline int getenv_int(const char *name) {
-    const char *v = getenv(name);
-    return v ? atoi(v) : 0;
-}
 inline int round_up(int v, int m) { return (v + m - 1) / m * m; }
 
 template <typename T>
@@ -358,19 +332,14 @@ struct ArenaPlan {
     }
 };
 
-// FAASBAL_ARENA_SKEW (default 1): buffer i starts (i mod 16) x 4.25 KB after the end of
-// buffer i - 1, so arrays read by position side by side (c_arr, c_hb, queue, qfree,
-// qhb: power-of-two sizes at 1 M workers) do not start at the same offset modulo the
-// memory channel interleave (diagnostic A/B knob)
-size_t arena_skew(int i) {
-    static const int on = getenv("FAASBAL_ARENA_SKEW") ? atoi(getenv("FAASBAL_ARENA_SKEW")) : 1;
-    return on ? (size_t)(i % 16) * 4352 : 0;
-}
+// Buffer i starts (i mod 16) x 4.25 KB after the end of buffer i - 1, so arrays read by
+// position side by side (c_arr, c_hb, queue, qfree, qhb: power-of-two sizes at 1 M
+// workers) do not start at the same offset modulo the memory channel interleave
+size_t arena_skew(int i) { return (size_t)(i % 16) * 4352; }
 
 // The host's wait for the context stream: polled (a tick is tens of microseconds; a
 // blocking wait's wake-up was measured at ~20 us per tick, tools/stream_timeline.sh)
 static hipError_t stream_wait(fb_ctx *c) {
-    if (!c->spin) return hipStreamSynchronize(c->stream);
     for (;;) {
         const hipError_t e = hipStreamQuery(c->stream);
         if (e != hipErrorNotReady) return e;
@@ -387,13 +356,10 @@ int arena_commit(fb_ctx *c, ArenaPlan &ap) {
     c->arena_bytes = total;
     // Every byte written once: some kernels load words no tick has written yet (a
     // round table's rows past the fill level, tail padding) and discard them; zeroing
-    // makes those loads deterministic (FAASBAL_ARENA_ZERO=0: off).  It did not change
-    // the streaming emit's two timing modes (profiles/NOTES_r02.md).
-    if (!getenv("FAASBAL_ARENA_ZERO") || atoi(getenv("FAASBAL_ARENA_ZERO"))) {
-        e = hipMemset(c->arena, 0, total);
-        if (e == hipSuccess) e = hipDeviceSynchronize();
-        if (e != hipSuccess) return fail(c, FB_EHIP, "hipMemset(arena) failed: %s", hipGetErrorString(e));
-    }
+    // makes those loads deterministic.
+    e = hipMemset(c->arena, 0, total);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) return fail(c, FB_EHIP, "hipMemset(arena) failed: %s", hipGetErrorString(e));
     char *p = (char *)c->arena;
     i = 0;
     for (auto &r : ap.req) {
@@ -634,6 +600,15 @@ int win_alloc(fb_ctx *c) {
     return FB_OK;
 }
 
+// A launched window tick moves the committed window (its commit may already have run on
+// the device, eager) while the host's view of it changes only at fb_tick_commit: state
+// reads wait for that commit.
+int win_uncommitted(fb_ctx *c, const char *what) {
+    if (c->launched && c->l_win)
+        return fail(c, FB_ESTATE, "%s between the launch and the commit of a window tick: fb_tick_commit first", what);
+    return FB_OK;
+}
+
 // The deferred commit of the last tick as its own launch (when no k_ev_link takes it).
 int flush_commit(fb_ctx *c) {
     if (!c->cm_pending) return FB_OK;
@@ -652,7 +627,7 @@ int flush_commit(fb_ctx *c) {
 // messages (the purge rides in k_ev_apply_ll's launch), on the linked-list path.
 bool win_plan(fb_ctx *c) {
     const int mode = c->win;
-    if (!c->win_cap || mode == 0 || c->l_E <= 0 || !c->ev_head || !c->ev_ll || !c->purge_apply || c->compact ||
+    if (!c->win_cap || mode == 0 || c->l_E <= 0 || !c->ev_head || !c->ev_ll || c->compact ||
         c->l_purge_only || c->deque || c->shard)
         return false;
     if (mode < 0 && c->last_L != 0) return false;  // auto: after a level-0 tick
@@ -727,9 +702,8 @@ int enqueue_tick(fb_ctx *c) {
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
     // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
     a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
-    a.cfirst = c->emit_cfirst;
-    // large tables for k_emit2: group rows too, scanned by k_plan2 (FAASBAL_GPLAN=0: k_plan)
-    const bool gplan = !a.fused && a.segw && !c->shard && c->gplan;
+    // large tables for k_emit2: group rows too, scanned by k_plan2
+    const bool gplan = !a.fused && a.segw && !c->shard;
     if ((a.fused || gplan) && !c->l_win) {  // (a window tick uses no group rows)
         // group rows: fused, about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads
         // both); k_plan2, the smallest groups that make at most 64 rows (one workgroup each)
@@ -776,7 +750,7 @@ int enqueue_tick(fb_ctx *c) {
     // log role was asked to run as k_logscan (FAASBAL_LOGSCAN=1)
     const int nbfe = (int)cdiv(nbf, 4);
     const size_t bm16 = (size_t)(((W + 63) / 64 + 1) / 2) * 16;
-    a.f_emit = (defer && a.fused && !a.f_sep && c->f_emit && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
+    a.f_emit = (defer && a.fused && !a.f_sep && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
                 bm16 <= (size_t)c->max_lds && !c->l_win) ? 1 : 0;
     c->l_oseg = a.f_emit != 0 || c->l_win;
     c->l_nbf = nbf;
@@ -790,7 +764,10 @@ int enqueue_tick(fb_ctx *c) {
         launch_pos_rebuild(c->pos_of[c->qcur], c->queue[c->qcur], c->qfree[c->qcur], c->qoff, Qn, Stream(c->stream));
         c->pos_ok = true;
     }
-    if (!ll && (rc = flush_commit(c))) return rc;
+    // the last tick's deferred commit: into this launch's first kernel (k_ev_link below, or
+    // k_scan for an idle tick after an idle tick), else as its own launch now
+    const bool cm_idle = c->cm_pending && c->cm.E == 0 && !c->cm.win && c->cm.n_clr == 0 && !c->cm.shard;
+    if (!ll && !(E == 0 && cm_idle) && (rc = flush_commit(c))) return rc;
     if (ll) {
         // group the messages per slot by linked lists (no sort): two launches
         EvArgs ea{};
@@ -820,7 +797,6 @@ int enqueue_tick(fb_ctx *c) {
         ea.ev_head = c->ev_head;
         ea.ev_next = c->ev_next;
         ea.check_ev = c->l_chk[0] != nullptr;
-        ea.slot_apply = c->slot_apply;
 #ifdef FAASBAL_STAMPS
         ea.dbg = c->dbg;
 #endif
@@ -835,7 +811,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.bud = c->bud;
         ea.post_infl = c->post_infl;
         ea.bud_next = c->bud_next;
-        ea.orph_grp = (a.f_emit && c->purge_apply) ? 1 : 0;
+        ea.orph_grp = a.f_emit ? 1 : 0;
         if (c->cm_pending) {  // the previous tick's commit rides in this launch
             ea.cm = c->cm;
             ea.cm_blocks = c->cm_grid;
@@ -843,11 +819,11 @@ int enqueue_tick(fb_ctx *c) {
         }
         // the slot purge (k_scan's W role) runs in k_ev_apply_ll's launch: extra blocks for
         // the untouched slots, each owner thread for its touched slot
-        ea.nbw = c->purge_apply ? nbw : 0;
+        ea.nbw = nbw;
         ea.now = c->l_now;
         ea.st = c->st;
         ea.free_out = c->free_[nxt];
-        ea.dmask = (c->purge_apply && (!a.slots_in_scan || a.f_sep || a.f_emit || c->l_win)) ? c->dmask : nullptr;
+        ea.dmask = (!a.slots_in_scan || a.f_sep || a.f_emit || c->l_win) ? c->dmask : nullptr;
         ea.wpart = c->l_win ? c->wpart : nullptr;
         if (c->l_win) {  // k_emit_win's look-back granules and ticket start from zero
             ea.wlb = c->wlb;
@@ -892,25 +868,15 @@ int enqueue_tick(fb_ctx *c) {
             p.shift = db * ps;
             p.db = db;
             p.nblk = nb;
-            // FAASBAL_RS_FUSE=1: each scatter adds the next pass's histogram with one global
-            // atomic per key instead of a histogram launch per pass -- measured slower at
-            // configs[4] (77 K messages: scatter 10.8 -> 14.0 us, the launch saved 4.7 us)
-            const bool fuse = c->rs_fuse != 0;
-            p.hist = c->rs_hist[fuse ? ps : 0];
-            p.hnext = fuse && ps + 1 < passes ? c->rs_hist[ps + 1] : nullptr;
-            p.first = (ps == 0 || !fuse) ? 1 : 0;
+            p.hist = c->rs_hist[0];
             p.identity_vals = ps == 0 ? 1 : 0;
-            if (ps == 0) {
+            if (ps == 0 && !c->shard) {
                 // pass 0 also clears the one-GPU front / back lists (sharded: zeroed with the
-                // exchange buffer), the touched bitmap and the later passes' count tables
-                if (!c->shard) {
-                    p.zero0 = front;
-                    p.zero1 = back;
-                    p.zbits = c->tbits;
-                    p.zwords = c->tbits ? (int)cdiv(W, 32) : 0;
-                }
-                for (int q = 1; q < 4; ++q) p.zhist[q - 1] = fuse && passes > q ? c->rs_hist[q] : nullptr;
-                p.zhwords = fuse && passes > 1 ? nb * NBw : 0;
+                // exchange buffer) and the touched bitmap
+                p.zero0 = front;
+                p.zero1 = back;
+                p.zbits = c->tbits;
+                p.zwords = c->tbits ? (int)cdiv(W, 32) : 0;
             }
             launch_rs_pass(p, t.first(), t.last());
             kin = p.kout;
@@ -961,8 +927,7 @@ int enqueue_tick(fb_ctx *c) {
         Timer t(c, "ev_apply");
         launch_ev_apply(a, t.st());
     }
-    a.slots_in_apply = (c->l_used_ll && c->purge_apply) ? 1 : 0;
-    a.dbg_stop = c->dbg_stop;
+    a.slots_in_apply = c->l_used_ll ? 1 : 0;
     a.tick = c->tick;
     a.now = c->l_now;
     a.tte = c->l_tte;
@@ -978,7 +943,7 @@ int enqueue_tick(fb_ctx *c) {
     const int qc = c->qcur, qn = c->qcur ^ 1;
     a.queue_in = c->queue[qc] + c->qoff;
     a.qaos = (!c->shard && c->qaos) ? 1 : 0;
-    a.cq_direct = (c->cq_direct && E == 0 && a.qaos && a.segw && !c->deque) ? 1 : 0;
+    a.cq_direct = (E == 0 && a.qaos && a.segw && !c->deque) ? 1 : 0;
     a.qfree_in = c->qfree[qc] ? c->qfree[qc] + c->qoff : nullptr;
     a.qhb_in = c->qhb[qc] ? c->qhb[qc] + c->qoff : nullptr;
     a.touched = c->touched;
@@ -986,8 +951,7 @@ int enqueue_tick(fb_ctx *c) {
     a.post = c->post;
     a.post_rf = c->post_rf;
     // past the L2-resident sizes the purge is bandwidth-bound: skip untouched post records
-    a.ffirst = c->scan_ffirst;
-    a.post_lazy = (W > kLdsBitmapSlots && !c->post_eager) ? 1 : 0;
+    a.post_lazy = W > kLdsBitmapSlots ? 1 : 0;
     a.front_list = front;
     a.back_list = back;
     a.st = c->st;
@@ -1008,7 +972,7 @@ int enqueue_tick(fb_ctx *c) {
     a.P = c->P;
     a.A_rep = c->A_rep;
     a.P_rep = c->P_rep;
-    a.repl = (gplan && c->repl) ? 1 : 0;  // k_plan2 writes a copy per group
+    a.repl = gplan ? 1 : 0;  // k_plan2 writes a copy per group
     a.trash = c->trash;
     c->l_compact = c->compact && !c->shard;
     if (c->l_compact) {
@@ -1025,7 +989,7 @@ int enqueue_tick(fb_ctx *c) {
         a.evicted = c->cout_ev;
     }
     a.arena = (char *)c->arena;
-    a.arena32 = (c->arena_bytes < ((size_t)1 << 32) && !c->no_arena32) ? 1 : 0;
+    a.arena32 = c->arena_bytes < ((size_t)1 << 32) ? 1 : 0;
     a.log_slot = c->log_slot;
     a.free_out = c->free_[nxt];
     a.queue_out = c->queue[qn];
@@ -1105,7 +1069,7 @@ int enqueue_tick(fb_ctx *c) {
             Timer t(c, "emit");
             // an eager commit follows: the launch's own completion signal is the event the
             // host waits for (a separate event record between the two kernels cost ~6 us)
-            c->tick_ev_set = !c->timing && c->eager && c->commit_now < 0 && c->reruns == 0;
+            c->tick_ev_set = !c->timing && c->eager && c->reruns == 0;
             launch_emit_win(a, nch, c->tick_ev_set ? Stream(c->stream, nullptr, c->tick_ev) : t.st());
         }
         HIPCHK(c, hipGetLastError());
@@ -1143,27 +1107,28 @@ int enqueue_tick(fb_ctx *c) {
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
+    if (c->cm_pending) {
+        // an idle tick's commit (evicted records, orphaned log entries) rides in k_scan when
+        // k_scan purges the slots and reads no log entry itself
+        if (a.slots_in_scan && !a.slots_in_apply && (a.f_emit || a.f_sep) && !c->deque) {
+            a.cm_fold = 1;
+            a.cm_tiles = c->cm.oseg ? c->cm.oseg_tiles : 0;
+            a.cm_n_orph = c->cm.n_orph;
+            a.cm_blocks = std::max(1, c->cm.oseg ? (int)cdiv(c->cm.oseg_tiles, kWaves) : (int)cdiv(c->cm.n_orph, kBS));
+            c->cm_pending = false;
+        } else if ((rc = flush_commit(c))) {
+            return rc;
+        }
+    }
     if (!a.slots_in_scan && !a.slots_in_apply) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
-    }
-    // the died bitmap is complete before k_scan when the purge ran in the apply launch:
-    // the log scan then runs beside the queue scan on a second stream
-    const bool fork = a.f_sep && a.slots_in_apply && c->fork;
-    if (fork) {
-        HIPCHK(c, hipEventRecord(c->fork_ev, c->stream));
-        HIPCHK(c, hipStreamWaitEvent(c->side_s, c->fork_ev, 0));
-        Timer t(c, "logscan");
-        launch_logscan(a, ls_grid, Stream(c->side_s, t.a, t.b));
-        HIPCHK(c, hipEventRecord(c->join_ev, c->side_s));
     }
     {
         Timer t(c, "scan");
         launch_scan(a, t.st());
     }
-    if (fork) {
-        HIPCHK(c, hipStreamWaitEvent(c->stream, c->join_ev, 0));
-    } else if (a.f_sep) {
+    if (a.f_sep) {
         Timer t(c, "logscan");
         launch_logscan(a, ls_grid, t.st());
     }
@@ -1221,9 +1186,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     const size_t Qlog = Wq + 2 * E;
     // window-capable contexts (one GPU, heartbeat loop): each queue buffer holds a window
     // that slides right by the served prefix and grows at its tail (<= 2 E + tasks per tick)
-    // (large tables, or FAASBAL_WINDOW=1; fb_set_window allocates them later for others)
-    const char *wenv = getenv("FAASBAL_WINDOW");
-    c->win_cap = !shard && !c->deque && (wenv ? atoi(wenv) > 0 : W > (size_t)kLdsBitmapSlots);
+    // (large tables; fb_set_window allocates them later for others)
+    c->win_cap = !shard && !c->deque && W > (size_t)kLdsBitmapSlots;
     c->qcap = c->win_cap ? (int64_t)(2 * Wq + 2 * E + 4096) : (int64_t)Wq;
     const size_t Wqb = (size_t)c->qcap;
     ArenaPlan ap;
@@ -1270,11 +1234,8 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->keys[i], E);
         ap.add(&c->vals[i], E);
     }
-    // 8-bit passes: 256 x blocks; wide passes (a tick of <= kRsWideMaxBlocks blocks): 2048 x blocks;
-    // one table per pass only with FAASBAL_RS_FUSE (read here: the arena is planned before the knobs)
-    c->rs_fuse = getenv_int("FAASBAL_RS_FUSE");
-    for (int i = 0; i < (c->rs_fuse ? 4 : 1); ++i)
-        ap.add(&c->rs_hist[i], std::max((size_t)256 * (cdiv(E, kRsTile) + 1),
+    // 8-bit passes: 256 x blocks; wide passes (a tick of <= kRsWideMaxBlocks blocks): 2048 x blocks
+    ap.add(&c->rs_hist[0], std::max((size_t)256 * (cdiv(E, kRsTile) + 1),
                                         (size_t)2048 * (size_t)(std::min<int64_t>((int64_t)cdiv(E, kRsTile), kRsWideMaxBlocks) + 1)));
     ap.add(&c->front_list, E);
     ap.add(&c->back_list, E);
@@ -1345,8 +1306,6 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     }
     int rc = arena_commit(c, ap);
     if (!rc && hipMemset(c->bad_min, 0x7f, 4) != hipSuccess) rc = fail(c, FB_EHIP, "hipMemset(bad_min) failed");
-    if (!rc && getenv_int("FAASBAL_PRINT_ARENA"))  // diagnostics: placement of the arena
-        fprintf(stderr, "faasbal arena %p, %zu bytes\n", c->arena, c->arena_bytes);
     if (!rc) {
         c->table_cap = tab;
         c->R_cap = 128;
@@ -1357,28 +1316,9 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         rc = FB_ENOMEM;
     if (!rc && hipHostGetDevicePointer((void **)&c->hout_dev, c->hout, 0) != hipSuccess) rc = FB_EHIP;
     if (!rc) memset(c->hout, 0, sizeof(HostOut));
-    if (!rc && getenv("FAASBAL_FORCE_PLAN")) c->force_plan = atoi(getenv("FAASBAL_FORCE_PLAN"));
-    if (!rc && getenv("FAASBAL_EMIT_CFIRST")) c->emit_cfirst = atoi(getenv("FAASBAL_EMIT_CFIRST"));
-    if (!rc && getenv("FAASBAL_LOGSCAN")) c->logscan = atoi(getenv("FAASBAL_LOGSCAN"));
-    if (!rc && getenv("FAASBAL_RS_WIDE")) c->rs_wide = atoi(getenv("FAASBAL_RS_WIDE"));
-    if (!rc && getenv("FAASBAL_GPLAN")) c->gplan = atoi(getenv("FAASBAL_GPLAN"));
-    if (!rc && getenv("FAASBAL_EV_LL")) c->ev_ll = atoi(getenv("FAASBAL_EV_LL"));
-    if (!rc && getenv("FAASBAL_REPL")) c->repl = atoi(getenv("FAASBAL_REPL"));
-    if (!rc && getenv("FAASBAL_PURGE_APPLY")) c->purge_apply = atoi(getenv("FAASBAL_PURGE_APPLY"));
-    if (!rc && getenv("FAASBAL_CQ_DIRECT")) c->cq_direct = atoi(getenv("FAASBAL_CQ_DIRECT"));
-    if (!rc && getenv("FAASBAL_F_EMIT")) c->f_emit = atoi(getenv("FAASBAL_F_EMIT"));
-    if (!rc && getenv("FAASBAL_WINDOW")) c->win = atoi(getenv("FAASBAL_WINDOW"));
-    if (!rc) c->stage_prof = getenv_int("FAASBAL_STAGE_PROF");
-    if (!rc) {
-        c->scan_ffirst = getenv_int("FAASBAL_SCAN_FFIRST");
-        c->post_eager = getenv_int("FAASBAL_POST_EAGER");
-        c->no_arena32 = getenv_int("FAASBAL_NO_ARENA32");
-    }
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;
-    if (!rc && getenv("FAASBAL_SPLIT_SLOTS")) c->split_slots = atoi(getenv("FAASBAL_SPLIT_SLOTS"));
-    if (!rc && getenv("FAASBAL_DBG_STOP")) c->dbg_stop = atoi(getenv("FAASBAL_DBG_STOP"));
     if (!rc && hipHostMalloc(&c->h_stage, (size_t)E * 32 * 2, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
     for (int h = 0; h < 2 && !rc; ++h)
         if (hipEventCreateWithFlags(&c->stage_ev[h], hipEventDisableTiming) != hipSuccess ||
@@ -1386,12 +1326,6 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
             rc = FB_EHIP;
     if (!rc && hipStreamCreateWithFlags(&c->cp_s, hipStreamNonBlocking) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipEventCreateWithFlags(&c->tick_ev, hipEventDisableTiming) != hipSuccess) rc = FB_EHIP;
-    if (!rc && (hipStreamCreateWithFlags(&c->side_s, hipStreamNonBlocking) != hipSuccess ||
-                hipEventCreateWithFlags(&c->fork_ev, hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming) != hipSuccess))
-        rc = FB_EHIP;
-    if (!rc && getenv("FAASBAL_FORK")) c->fork = atoi(getenv("FAASBAL_FORK"));
-    if (!rc && getenv("FAASBAL_D2H_KERNEL")) c->d2h_kernel = atoi(getenv("FAASBAL_D2H_KERNEL"));
     if (!rc) {
         int nt = getenv("FAASBAL_STAGE_THREADS") ? atoi(getenv("FAASBAL_STAGE_THREADS")) : 8;
         nt = std::max(1, std::min(nt, 16));
@@ -1408,10 +1342,6 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     for (int p = 0; p < 2 && !rc; ++p)
         if (c->tbitsb[p] && hipMemset(c->tbitsb[p], 0, (W + 31) / 32 * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc) c->tbits = c->tbitsb[c->tick & 1];
-    if (!rc && getenv("FAASBAL_COMMIT_NOW")) c->commit_now = atoi(getenv("FAASBAL_COMMIT_NOW"));
-    if (!rc && getenv("FAASBAL_WAIT_SPIN")) c->spin = atoi(getenv("FAASBAL_WAIT_SPIN"));
-    if (!rc && getenv("FAASBAL_SPARSE_COMMIT")) c->sparse_commit = atoi(getenv("FAASBAL_SPARSE_COMMIT"));
-    if (!rc && getenv("FAASBAL_SLOT_APPLY")) c->slot_apply = atoi(getenv("FAASBAL_SLOT_APPLY"));
     for (int p = 0; p < 2 && !rc; ++p)
         if (hipMemset(c->grp[p], 0, kGrpWords * 4) != hipSuccess) rc = FB_EHIP;
     if (!rc && hipMemset(c->reg, 0, W) != hipSuccess) rc = FB_EHIP;
@@ -1472,12 +1402,6 @@ int fb_destroy(fb_ctx *c) {
     }
     if (c->tick_ev) hipEventDestroy(c->tick_ev);
     if (c->cp_s) hipStreamDestroy(c->cp_s);
-    if (c->side_s) {
-        hipStreamSynchronize(c->side_s);
-        hipStreamDestroy(c->side_s);
-    }
-    if (c->fork_ev) hipEventDestroy(c->fork_ev);
-    if (c->join_ev) hipEventDestroy(c->join_ev);
     for (auto &t : c->tl) {
         hipEventDestroy(t.a);
         hipEventDestroy(t.b);
@@ -1598,6 +1522,7 @@ int fb_load_state(fb_ctx *c, int32_t n_workers, const uint8_t *registered, const
 int fb_read_state(fb_ctx *c, uint8_t *registered, int32_t *free_processes, double *last_heartbeat, uint32_t *epoch,
                   int32_t *queue, int64_t *queue_len, int32_t *log_slot, int64_t *log_len) {
     if (!c) return FB_EINVAL;
+    if (int rc_ = win_uncommitted(c, "fb_read_state")) return rc_;
     if (int rc_ = flush_commit(c)) return rc_;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, stream_wait(c));
@@ -1717,6 +1642,7 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
 
 int fb_read_inflight(fb_ctx *c, uint32_t *inflight) {
     if (!c || !inflight) return FB_EINVAL;
+    if (int rc_ = win_uncommitted(c, "fb_read_inflight")) return rc_;
     if (int rc_ = flush_commit(c)) return rc_;
     if (!c->bud) return fail(c, FB_ESTATE, "in-flight counts exist on one-GPU heartbeat contexts only");
     HIPCHK(c, hipSetDevice(c->device));
@@ -1822,8 +1748,6 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     // dispatcher that parses messages straight into them) the pass only validates, and
     // the H2D copies read the caller's arrays; they must stay unchanged until the tick
     // that uses them has been waited for.
-    using clk = std::chrono::steady_clock;
-    const auto tp0 = clk::now();
     bool direct = E > 0, resident = E > 0;
     if (direct) {
         const void *ptrs[5] = {kind, slot, val, ts, seq};
@@ -1836,7 +1760,10 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
                 (void)hipGetLastError();
             } else if (at.type == hipMemoryTypeHost) {
                 ++nhost;
-            } else if (at.type == hipMemoryTypeDevice && at.device == c->device) {
+            } else if (at.type == hipMemoryTypeDevice) {
+                if (at.device != c->device)
+                    return fail(c, FB_EINVAL, "event array %d is in the memory of GPU %d, the context's is GPU %d", j,
+                                at.device, c->device);
                 ++ndev;
             }
         }
@@ -1867,12 +1794,10 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     // pinned inputs: their H2D copies go out first and overlap the validation below (a
     // batch that fails validation is never launched, so copying it first is harmless)
     bool copied = false;
-    const auto tp1 = clk::now();
     if (E && direct) {
         if (int rc = stage_copies(c, half, kind, slot, val, ts, seq, E)) return rc;
         copied = true;
     }
-    const auto tp2 = clk::now();
     if (E) {
         const size_t ecap = (size_t)c->E_cap;
         char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
@@ -1945,25 +1870,10 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
             c->st_chk[0] = nullptr;
         }
     }
-    const auto tp3 = clk::now();
     if (E && !copied) {
         const size_t ecap = (size_t)c->E_cap;
         char *h = (char *)c->h_stage + (size_t)half * ecap * 32;
         if (int rc = stage_copies(c, half, h, h + ecap, h + ecap * 5, h + ecap * 9, h + ecap * 17, E)) return rc;
-    }
-    if (c->stage_prof) {  // FAASBAL_STAGE_PROF=1: where fb_tick_stage's time goes (diagnostics)
-        const auto tp4 = clk::now();
-        auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-        c->sprof[0] += us(tp0, tp1);
-        c->sprof[1] += us(tp1, tp2);
-        c->sprof[2] += us(tp2, tp3);
-        c->sprof[3] += us(tp3, tp4);
-        if (++c->sprof_n == 16) {
-            fprintf(stderr, "fb_tick_stage us: pointer checks %.1f, copies %.1f, validation %.1f, copies (staged) %.1f\n",
-                    c->sprof[0] / 16, c->sprof[1] / 16, c->sprof[2] / 16, c->sprof[3] / 16);
-            c->sprof[0] = c->sprof[1] = c->sprof[2] = c->sprof[3] = 0;
-            c->sprof_n = 0;
-        }
     }
     c->staged = true;
     c->st_E = E;
@@ -1972,7 +1882,7 @@ int fb_tick_stage(fb_ctx *c, double now, int32_t n_events, const uint8_t *kind, 
     return FB_OK;
 }
 
-static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid, bool at_once);
+static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid);
 
 int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     if (!c) return FB_EINVAL;
@@ -2033,11 +1943,11 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     const int rc = enqueue_tick(c);
     if (rc) return rc;
     c->l_eager = false;
-    if (c->eager && c->l_win && c->commit_now < 0) {
+    if (c->eager && c->l_win) {
         // eager: the window tick's commit right behind it on the stream; it commits only
         // if the tick finished as a window tick (fb_tick_wait reruns it otherwise)
         int grid = 0;
-        const CommitArgs a = commit_args(c, true, grid, true);
+        const CommitArgs a = commit_args(c, true, grid);
         if (!c->tick_ev_set) HIPCHK(c, hipEventRecord(c->tick_ev, c->stream));  // fb_tick_wait waits for the tick, not its commit
         Timer t(c, "commit");
         launch_commit(a, grid, t.st());
@@ -2082,10 +1992,6 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             // the eager commit runs (the next launch queues behind it)
             hipError_t e;
             while ((e = hipEventQuery(c->tick_ev)) == hipErrorNotReady) {
-                if (!c->spin) {
-                    e = hipEventSynchronize(c->tick_ev);
-                    break;
-                }
             }
             HIPCHK(c, e);
         } else {
@@ -2098,12 +2004,14 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
             // the batch was left to the device's check: name the first offending event; the
             // tick is not committed (its launch read only committed state)
             c->launched = false;
+            // the first offending message's index (k_ev_link atomicMins it for every checked
+            // batch): read, and reset for the next checked batch whatever its kind
+            int32_t bi = 0x7f7f7f7f;
+            const int32_t none = 0x7f7f7f7f;
+            HIPCHK(c, hipMemcpy(&bi, c->bad_min, 4, hipMemcpyDeviceToHost));
+            HIPCHK(c, hipMemcpy(c->bad_min, &none, 4, hipMemcpyHostToDevice));
             if (c->l_res) {
-                // a device-resident batch: the first offending message's index from the device
-                int32_t bi = 0x7f7f7f7f;
-                const int32_t none = 0x7f7f7f7f;
-                HIPCHK(c, hipMemcpy(&bi, c->bad_min, 4, hipMemcpyDeviceToHost));
-                HIPCHK(c, hipMemcpy(c->bad_min, &none, 4, hipMemcpyHostToDevice));
+                // a device-resident batch: the index from the device
                 return fail(c, FB_EINVAL, "event %d: invalid message (slot outside [0, %d), unknown kind, or a "
                             "timestamp decreasing or past now)", bi, c->W);
             }
@@ -2193,7 +2101,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
 // The commit of the launched tick.  eager: built at launch, before the tick's results
 // exist -- the window's head and appended positions are read by the kernel from the
 // tick's results, and every orphan tile and appended position gets blocks (grid-stride).
-static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid, bool at_once) {
+static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid) {
     const int64_t n_orph = eager ? 0 : c->last.n_orphans_local;
     CommitArgs a{};
     a.W = c->W;
@@ -2245,16 +2153,9 @@ static CommitArgs commit_args(fb_ctx *c, bool eager, int &grid, bool at_once) {
         a.tomb = c->tomb;
         a.n_tomb = 2 * c->l_E;
         a.post_rf = c->post_rf;
-        // a commit that runs before the next launch (not inside it): the tick's message
-        // lists are intact, so its touched slots come from their owners, not a 1M-slot sweep
-        if (at_once && c->l_used_ll && !c->l_resort && c->sparse_commit) {
-            a.owners = c->ev_next;
-            a.own_slot = c->ev_slot;
-            a.wcnt = c->wcnt;
-        }
     }
     grid = a.nbw + a.nbo + (int)cdiv(a.n_clr, kBS) +
-           (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) + (a.owners ? (int)cdiv(a.E, kBS) : 0) : 0);
+           (a.win ? a.nbap + (int)cdiv(a.n_tomb, kBS) : 0);
     return a;
 }
 
@@ -2267,8 +2168,8 @@ int fb_tick_commit(fb_ctx *c) {
         // the device committed the tick right behind it (fb_tick_launch_staged)
     } else if (c->W > 0 || n_orph > 0 || (c->ev_clr && c->l_E > 0)) {
         int grid = 0;
-        const bool defer = c->ev_head && c->ev_ll && c->commit_now != 1 && !(c->l_win && c->commit_now < 0);
-        const CommitArgs a = commit_args(c, false, grid, !defer);
+        const bool defer = c->ev_head && c->ev_ll && !c->l_win;
+        const CommitArgs a = commit_args(c, false, grid);
         if (defer) {  // (by default a window tick's commit runs at once)
             // deferred: the next launch's k_ev_link runs it (or flush_commit)
             c->cm = a;
@@ -2338,7 +2239,7 @@ int fb_get_local_assignments(fb_ctx *c, int64_t first, int64_t n, int64_t *task,
 // hipMemcpyAsync.  (FAASBAL_D2H_KERNEL=0: always hipMemcpyAsync.)
 static int d2h(fb_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!bytes) return FB_OK;
-    if (c->d2h_kernel && (bytes & 3) == 0) {
+    if ((bytes & 3) == 0) {
         hipPointerAttribute_t at;
         if (hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
             launch_copy_words((uint32_t *)at.devicePointer, (const uint32_t *)src, (int64_t)(bytes / 4), Stream(c->stream));
@@ -2364,7 +2265,7 @@ static int64_t *orph_dense_dev(fb_ctx *c) {
 // pinned host memory by the gather kernel
 static int orph_out(fb_ctx *c, int64_t *dst, int64_t n) {
     if (!n) return FB_OK;
-    if (c->l_oseg && c->d2h_kernel && n == c->last.n_orphans_local) {
+    if (c->l_oseg && n == c->last.n_orphans_local) {
         hipPointerAttribute_t at;
         if (hipPointerGetAttributes(&at, dst) == hipSuccess && at.type == hipMemoryTypeHost && at.devicePointer) {
             launch_orph_gather((int64_t *)at.devicePointer, c->orphans, c->fcnt, c->l_nbf, Stream(c->stream));
@@ -2536,7 +2437,7 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
         return nullptr;
     };
     auto add = [&](void *dst, const void *src, int64_t bytes) -> bool {
-        uint32_t *d = c->d2h_kernel && (bytes & 3) == 0 ? mapped(dst) : nullptr;
+        uint32_t *d = (bytes & 3) == 0 ? mapped(dst) : nullptr;
         if (!d) return false;
         const int b0 = m.n ? m.blk0[m.n - 1] + (int)std::min<int64_t>(
                                                        std::max<int64_t>(1, (m.words[m.n - 1] + 4 * kBS - 1) / (4 * kBS)), 512)
@@ -2565,7 +2466,7 @@ int fb_get_outputs_compact(fb_ctx *c, int32_t *slot, uint8_t *cnt, int64_t cap, 
     }
     // the orphans' segments gathered by the same launch when they go to pinned memory
     bool orph_done = false;
-    if (orphans && c->l_oseg && c->d2h_kernel && c->last.n_orphans_local) {
+    if (orphans && c->l_oseg && c->last.n_orphans_local) {
         if (int64_t *od = (int64_t *)mapped(orphans)) {
             m.odst = od;
             m.osrc = c->orphans;
@@ -2711,9 +2612,9 @@ int fb_tick(fb_ctx *c, double now, double tte, int32_t n_events, const uint8_t *
 }
 
 int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
-    if (!c) return FB_EINVAL;
-    if (int rc_ = flush_commit(c)) return rc_;
     if (!c || !v) return FB_EINVAL;
+    if (int rc_ = win_uncommitted(c, "fb_device_view_get")) return rc_;
+    if (int rc_ = flush_commit(c)) return rc_;
     v->free_processes = &c->free_[c->cur]->x;
     v->free_processes_stride = (int32_t)sizeof(int2);
     v->last_heartbeat = c->hb;
@@ -2733,6 +2634,20 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     v->n_workers = c->W;
     v->queue_len = c->Qn;
     v->log_head = c->head;
+    return FB_OK;
+}
+
+int fb_set_path(fb_ctx *c, const char *name, int value) {
+    if (!c || !name) return FB_EINVAL;
+    if (c->launched) return fail(c, FB_ESTATE, "fb_set_path between ticks only");
+    if (int rc_ = flush_commit(c)) return rc_;
+    const std::string n(name);
+    if (n == "plan" && value >= 0 && value <= 2) c->force_plan = value;
+    else if (n == "logscan" && value >= -1 && value <= 1) c->logscan = value;
+    else if (n == "split_slots" && value >= -1 && value <= 1) c->split_slots = value;
+    else if (n == "ev_ll" && (value == 0 || value == 1)) c->ev_ll = value;
+    else if (n == "rs_wide" && (value == 0 || value == 1)) c->rs_wide = value;
+    else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }
 

@@ -156,11 +156,6 @@ struct CommitArgs {
     // non-null: an eager commit (enqueued behind its window tick before the host waited):
     // it commits only if the tick finished as a window tick, with wq_head / napp from these
     // results; nbap blocks walk the appended positions grid-stride
-    // sparse window commits (non-null owners): blocks after the tomb ones commit the slot
-    // of every message with owners[e] < 0 (k_ev_link's list heads: one per touched slot);
-    // the slot blocks then commit only untouched slots of tiles with evictions (wcnt)
-    const int32_t *owners, *own_slot;
-    const uint32_t *wcnt;
     const int64_t *eager;      // the tick's commit word (TickArgs::cw)
     int64_t cw_tag;            // its launch's link stamp: cw[0] == cw_tag means the tick failed
 };
@@ -234,7 +229,6 @@ struct EvArgs {
     // word 1 of each), zeroed by k_ev_link; k_emit_win sums them
     uint32_t *wpart;
     int check_ev;               // k_ev_link checks the messages (host-unchecked pinned batches)
-    int slot_apply;             // k_ev_apply_ll: touched slots applied by the slot blocks, in slot order
     int32_t *bad_min;           // k_ev_link: the first invalid message's index (atomicMin; reset by the host)
     unsigned long long *wlb;    // k_emit_win's look-back granules (wlb_n of them) and ticket,
     int wlb_n;                  // zeroed here
@@ -248,7 +242,6 @@ struct TickArgs {
     int W, E, R, nbw, nbf, nbq;
     int fused;       // 1: k_emit derives the cross-block prefixes itself (no k_plan launch)
     int segw;        // 1: k_scan stores per-64-position segment counts (k_emit2, fused or after k_plan)
-    int cfirst;      // 1: k_emit2's compaction blocks come first in the grid
     int lds_bitmap;  // 1: F-blocks stage the died-registration bitmap in LDS
     int slots_in_scan;
     int deque;        // 1: PushDispatcher.start semantics (see EvArgs)
@@ -279,7 +272,6 @@ struct TickArgs {
     // k_emit2's log workgroups flag the orphans against the died bitmap in LDS and write
     // them into per-tile segments (orphans[t*2048 + i], i < fcnt[t])
     int f_emit;
-    int dbg_stop;     // timing probes only (FAASBAL_DBG_STOP)  // 1: no k_slots launch; k_scan's W-role purges and its F-role reads records
     uint32_t tick;
     double now, tte;
     int64_t Qn, Qlog, head_in, T, log_cap;
@@ -298,7 +290,6 @@ struct TickArgs {
     const uint32_t *tbits;  // one GPU, message ticks: touched as a bitmap (L2-resident: 128 KB per 1M slots)
     const PostRec *post;
     const uint8_t *post_rf;
-    int ffirst;     // k_scan: log blocks before queue blocks in the grid (A/B knob FAASBAL_SCAN_FFIRST)
     int slots_in_apply;
     int cq_direct;  // idle one-GPU tick on k_emit2: the emit recomputes each position's raw free count
                     // and heartbeat from the committed per-position arrays; k_scan stores neither  // the slot purge ran in k_ev_apply_ll's launch: k_scan has no W blocks
@@ -344,6 +335,14 @@ struct TickArgs {
                                  // it moved (-1: none), 2 E entries
     int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
 
+    // the previous tick's commit folded into this k_scan (one-GPU heartbeat contexts, an
+    // idle tick after an idle tick): the W role deletes the records that tick evicted
+    // (st & kStEvicted, read before it writes this tick's st) and the last cm_blocks
+    // blocks clear its orphaned log entries -- per-tile segments (cm_tiles tiles of
+    // orphans / fcnt) or a dense list of cm_n_orph -- before this tick's log role runs
+    int cm_fold, cm_blocks, cm_tiles;
+    int64_t cm_n_orph;
+
     int32_t *trash;     // kTrashRows x kBS words: k_emit2's round stores of inactive lanes land here
     int32_t *rb_slot;   // compact assignments (null: off): slot per LRU position, -1 none
     uint8_t *rb_c;      // ... and min(c, L + 1) (clamped to 255)
@@ -387,23 +386,16 @@ struct Stream {
 // One LSD pass (histogram + scatter launches) over `db`-bit digits at `shift`;
 // hist holds (1 << db rounded up to 256 / 1024 / 2048) x (nblk + 1) counts (the
 // extra row: digit totals when nblk > kRsScanMin).
-// Only the first pass launches a histogram kernel: every scatter adds the next
-// pass's [tile][digit] counts (hnext) while it places the keys, so a pass after the
-// first is one launch (plus k_rs_scan past kRsScanMin tiles).  The first pass's
-// histogram launch clears zero0 / zero1 (n words each), zbits (zwords) and the later
-// passes' tables zhist[0..2] (zhwords each).
+// The first pass's histogram launch clears zero0 / zero1 (n words each) and zbits (zwords).
 struct RsPass {
     const uint32_t *kin, *vin;
     uint32_t *kout, *vout;
     int n, shift, db, nblk;
-    uint32_t *hist;   // this pass's counts (filled by the histogram launch or the previous scatter)
-    uint32_t *hnext;  // the next pass's counts, or null on the last pass
-    int first, identity_vals;
+    uint32_t *hist;   // this pass's [tile][digit] counts (its histogram launch)
+    int identity_vals;
     int32_t *zero0, *zero1;
     uint32_t *zbits;
     int zwords;
-    uint32_t *zhist[3];
-    int zhwords;
 };
 void launch_rs_pass(const RsPass &p, Stream h, Stream s);
 #ifndef FAASBAL_RS_SCAN_MIN

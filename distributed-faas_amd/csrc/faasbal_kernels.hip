@@ -360,9 +360,7 @@ __device__ __forceinline__ void prefetch_args(const A &a) {
 template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ keys, int n, int shift, int db,
                                                  uint32_t *__restrict__ hist, int nblk, int32_t *__restrict__ zero0,
-                                                 int32_t *__restrict__ zero1, uint32_t *__restrict__ zbits, int zwords,
-                                                 uint32_t *__restrict__ zh0, uint32_t *__restrict__ zh1,
-                                                 uint32_t *__restrict__ zh2, int zhwords) {
+                                                 int32_t *__restrict__ zero1, uint32_t *__restrict__ zbits, int zwords) {
     constexpr int DPT = NB / kBS;
     __shared__ uint32_t cnt[NB];
 #pragma unroll
@@ -370,12 +368,6 @@ __global__ __launch_bounds__(kBS) void k_rs_hist(const uint32_t *__restrict__ ke
     __syncthreads();
     const int base = blockIdx.x * kRsTile;
     for (int i = blockIdx.x * kBS + (int)threadIdx.x; i < zwords; i += nblk * kBS) zbits[i] = 0;
-    // the later passes' count tables, filled by atomics in the scatters before them
-    for (int i = blockIdx.x * kBS + (int)threadIdx.x; i < zhwords; i += nblk * kBS) {
-        if (zh0) zh0[i] = 0;
-        if (zh1) zh1[i] = 0;
-        if (zh2) zh2[i] = 0;
-    }
     if (zero0) {
 #pragma unroll
         for (int j = 0; j < kRsItems; ++j) {
@@ -447,8 +439,7 @@ template <int NB>
 __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__ kin, const uint32_t *__restrict__ vin,
                                                     uint32_t *__restrict__ kout, uint32_t *__restrict__ vout, int n,
                                                     int shift, int db, const uint32_t *__restrict__ hist, int nblk,
-                                                    int identity_vals, const uint32_t *__restrict__ scanned,
-                                                    uint32_t *__restrict__ hnext) {
+                                                    int identity_vals, const uint32_t *__restrict__ scanned) {
     constexpr int DPT = NB / kBS;       // digits per thread
     constexpr int CH = 64 / DPT;        // blocks per batch of 64 loads in flight
     __shared__ uint32_t base[NB];
@@ -554,8 +545,6 @@ __global__ __launch_bounds__(kBS) void k_rs_scatter(const uint32_t *__restrict__
             for (int q = 0; q < w; ++q) off += wcnt[q][d];
             kout[off] = key;
             vout[off] = val;
-            // the next pass's histogram: this key's next digit in its destination tile
-            if (hnext) atomicAdd(&hnext[(size_t)(off / kRsTile) * NB + ((key >> (shift + db)) & mask)], 1u);
         }
         __syncthreads();
         if constexpr (NB == 256) {
@@ -847,12 +836,7 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk, int64_
                 const int32_t p = a.tomb[j];
                 if (p >= wq_head && p < a.wq_tail) a.wqf[p] = kTomb;
             }
-            return;
         }
-        // sparse window commit: each slot that got messages, once -- by the message whose
-        // thread owned it in k_ev_apply_ll (the first in its linked list)
-        const int64_t e = (int64_t)(rb - a.nbap - ntb) * kBS + threadIdx.x;
-        if (a.owners && e < a.E && a.owners[e] < 0) commit_slot(a, a.own_slot[e], true, wq_head);
         return;
     }
     if (blk >= a.nbw + a.nbo) {
@@ -886,14 +870,6 @@ __device__ __forceinline__ void commit_body(const CommitArgs &a, int blk, int64_
     }
     const int s = blk * kBS + threadIdx.x;
     if (s >= a.W) return;
-    if (a.owners) {
-        // sparse window commit: the touched slots are the owners' (blocks above); a tile
-        // without evictions has nothing else to commit
-        if (a.wcnt[blk] == 0) return;
-        if (got_msg(a, s)) return;
-        commit_slot(a, s, false, wq_head);
-        return;
-    }
     commit_slot(a, s, a.E > 0 && got_msg(a, s), wq_head);
 }
 
@@ -1035,14 +1011,12 @@ __device__ __forceinline__ bool SlotRun::purge(const EvArgs &a, uint32_t s, int 
 
 __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t s, int e, int hidx, int kind0,
                                           int32_t val0, double ts0, int64_t seq0, int reg0, bool &ev);
-__device__ __forceinline__ bool apply_touched(const EvArgs &a, uint32_t s, int hidx, bool &ev);
 
-// k_ev_apply_ll's slot blocks: the purge of untouched slots and (slot_apply) the
-// application of touched ones, one slot per thread, block blk = slots [256 blk, +256)
+// k_ev_apply_ll's slot blocks: the purge of untouched slots, one slot per thread, block
+// blk = slots [256 blk, +256)
 __device__ __forceinline__ void apply_slot_block(const EvArgs &a, int blk) {
     const int s = blk * kBS + (int)threadIdx.x;
     bool died = false, evicted = false, queued = false;
-    bool qt = false, evt = false;  // a touched slot applied here: queued / evicted after its purge
     uint32_t no = 0;
     if (s < a.W) {
         // the link stamp says whether the slot got messages (its owner purges it); the
@@ -1054,26 +1028,19 @@ __device__ __forceinline__ void apply_slot_block(const EvArgs &a, int blk) {
         const int32_t b0 = a.bud ? a.bud[s] : 0;
         const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(b0 - fq0.x) : 0u;
         bool alive;
-        if (!t) {
+        if (!t)
             no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, fq0.y, in0, died, evicted, alive,
                             queued);
-        } else if (a.slot_apply) {
-            // the slot's messages, applied by its thread in slot order: the records of
-            // the touched slots are read and written a wave's 64 slots at a time
-            // instead of in message order (SlotRun::purge counts its own eviction)
-            qt = apply_touched(a, (uint32_t)s, (int)(uint32_t)a.ev_head[s], evt);
-        }
     }
     const uint64_t dm = __ballot(died);
     const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
-    const uint32_t nq = (uint32_t)__popcll(__ballot(queued || qt));
-    const uint32_t nea = ne + (uint32_t)__popcll(__ballot(evt));
+    const uint32_t nq = (uint32_t)__popcll(__ballot(queued));
     const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
     if (lane_id() == 0) {
         if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
         if (ne) count_evicted(a, blk, ne);
         count_orphans(a, blk, nw);
-        if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), nea, nq);
+        if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
     }
 }
 
@@ -1140,15 +1107,6 @@ __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
         const uint32_t ne = (uint32_t)__popcll(__ballot(ev)), nq = (uint32_t)__popcll(__ballot(qd));
         if (lane_id() == (int)__builtin_ctzll(act)) count_wpart(a, (int)blockIdx.x * kWaves + wave_id(), ne, nq);
     }
-    APPLY_EXIT();
-}
-
-// slot_apply: the slot blocks alone (touched slots applied in slot order), compiled
-// without k_ev_apply_ll's message-order path and its register budget
-__global__ __launch_bounds__(kBS) void k_ev_apply_slots(EvArgs a) {
-    prefetch_args(a);
-    APPLY_STAMP(0);
-    apply_slot_block(a, (int)blockIdx.x);
     APPLY_EXIT();
 }
 
@@ -1238,80 +1196,6 @@ __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t 
     return a.nbw ? r.purge(a, s, reg0, ev) : false;
 }
 
-
-// Slot-ordered application (k_ev_apply_ll's slot blocks, EvArgs::slot_apply): the thread
-// of touched slot s walks k_ev_link's list from its head (hidx) to the first message
-// (next < 0).  A single message (most slots) is applied with its payload loaded together
-// with its link; longer runs collect up to kLinkMax indices (a dependent load each),
-// sort them into arrival order and apply them, each payload loaded as it is applied.
-// Beyond kLinkMax the host reruns the tick through the sort.  Returns whether the slot
-// is queued after its purge; ev: evicted.
-__device__ __forceinline__ bool apply_touched(const EvArgs &a, uint32_t s, int hidx, bool &ev) {
-    SlotRun r;
-    r.init(a, s);
-    const int reg0 = r.reg;
-    const int32_t nx0 = a.ev_next[hidx];
-    const int kind0 = a.ev_kind[hidx];
-    const int32_t val0 = a.ev_val[hidx];
-    const double ts0 = a.ev_ts[hidx];
-    const int64_t seq0 = a.ev_seq[hidx];
-    if (nx0 < 0) {
-        r.step<true>(a, s, hidx, kind0, val0, ts0, seq0, log_peek(a, seq0));
-        r.finish(a, s, s);
-        return r.purge(a, s, reg0, ev);
-    }
-    int ix[kLinkMax];
-    int n = 1, cur = nx0;
-    bool done = false;
-#pragma unroll
-    for (int k = 0; k < kLinkMax; ++k) {
-        if (k == 0) {
-            ix[0] = hidx;
-            continue;
-        }
-        ix[k] = done ? INT32_MAX : cur;
-        if (!done) {
-            ++n;
-            const int32_t nx = a.ev_next[cur];
-            if (nx < 0) done = true;
-            else cur = nx;
-        }
-    }
-    if (!done) {  // too many messages for the registers: the host reruns through the sort
-        a.hout->resort = 1;
-        if (a.cw) a.cw[0] = a.link;
-        return false;
-    }
-#pragma unroll
-    for (int k = 2; k <= kLinkMax; k <<= 1)
-#pragma unroll
-        for (int j = k >> 1; j > 0; j >>= 1)
-#pragma unroll
-            for (int i = 0; i < kLinkMax; ++i)
-                if ((i ^ j) > i) {
-                    const int l = i ^ j;
-                    const bool sw = (i & k) == 0 ? (ix[i] > ix[l]) : (ix[i] < ix[l]);
-                    const int t = ix[i];
-                    ix[i] = sw ? ix[l] : t;
-                    ix[l] = sw ? t : ix[l];
-                }
-    uint32_t clr = 0;  // bit m: message m completed its entry
-#pragma unroll
-    for (int m = 0; m < kLinkMax; ++m) {
-        if (m < n) {
-            const int i = ix[m];
-            const int64_t q = a.ev_seq[i];
-            bool dup = false;
-#pragma unroll
-            for (int k = 0; k < m; ++k)
-                if ((clr >> k) & 1u) dup = dup || a.ev_seq[ix[k]] == q;
-            const bool cl = r.step<true>(a, s, i, a.ev_kind[i], a.ev_val[i], a.ev_ts[i], q, log_peek(a, q), dup);
-            clr |= cl ? (1u << m) : 0u;
-        }
-    }
-    r.finish(a, s, s);
-    return r.purge(a, s, reg0, ev);
-}
 
 // ------------------------------------------------------------ slot state
 
@@ -1486,7 +1370,15 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
     bool died_start = false, evicted = false;
     uint32_t no = 0;  // orphans: in-flight entries of this slot's dead registration
     if (s < a.W) {
-        const Cur c = cur_slot(a, s);
+        Cur c = cur_slot(a, s);
+        if (a.cm_fold && (a.st[s] & kStEvicted)) {
+            // the previous tick deleted this record (its commit, folded in here):
+            // del self.workers[remove_id] (task_dispatcher.py:246-247)
+            c.reg0 = c.reg = 0;
+            c.hb = __builtin_nan("");
+            const_cast<uint8_t *>(a.reg)[s] = 0;  // (the committed record arrays: read-only elsewhere in a tick)
+            const_cast<double *>(a.hb)[s] = c.hb;
+        }
         // in-flight entries after the messages (loaded with the record, selected after)
         const int32_t b0 = a.bud ? a.bud[s] : 0;
         const uint32_t ip = (a.bud && a.E > 0) ? a.post_infl[s] : 0u;
@@ -1598,9 +1490,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     __shared__ unsigned long long s4[kWaves];
     __shared__ uint32_t wc[kWaves][kBS];
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
-    // a.ffirst: log blocks first in hardware order (logical ids unchanged)
-    int bid = blockIdx.x;
-    if (a.ffirst) bid = bid < nbf ? bid + a.nbq : (bid < nbf + a.nbq ? bid - nbf : bid);
+    const int bid = blockIdx.x;
     const int SO = a.nbw;
     STAMP(a, SO, 0);
     // grid: queue blocks first (the critical path: their loads go out before the log
@@ -1686,6 +1576,19 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)n);
         }
         STAMP(a, SO, 15);
+        return;
+    }
+    if (a.cm_fold && bid >= (int)gridDim.x - a.cm_blocks) {
+        // ---- the previous tick's orphaned log entries leave the log (its folded commit)
+        const int cb = bid - ((int)gridDim.x - a.cm_blocks);
+        if (a.cm_tiles > 0) {  // per-tile segments: a wave per tile
+            const int t = cb * kWaves + wave_id();
+            const uint32_t n = t < a.cm_tiles ? a.fcnt[t] : 0u;
+            for (uint32_t i = lane_id(); i < n; i += 64) a.log_slot[a.orphans[(int64_t)t * kFTile + i]] = -1;
+        } else {
+            const int64_t i = (int64_t)cb * kBS + threadIdx.x;
+            if (i < a.cm_n_orph) a.log_slot[a.orphans[i]] = -1;
+        }
         return;
     }
     if (bid >= a.nbq) {
@@ -2444,7 +2347,7 @@ __global__ __launch_bounds__(kBS) void k_emit(TickArgs a_) {
         }
         int status = 0;
         if (maxc > a.R && L >= a.R - 1) status = 1;   // rows beyond the table needed: rerun wider
-        if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log
+        else if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log (N_eff exact once R is)
         const int64_t p = N_eff - S_L;
         auto getA = [&](int r) -> int64_t { return r < rlim ? a.A[r] : (int64_t)0; };
         const int64_t AL = (L < maxc && L < rlim) ? getA(L) : 0;
@@ -2721,11 +2624,10 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     const int lane = lane_id(), w = wave_id();
     // the other parity's group rows, for the next launch's k_scan atomics
     for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
-    // grid: queue blocks then compaction blocks, or (a.cfirst) compaction first
-    // log workgroups: 4 tiles each (f_emit: one tile each), then the slot tiles 4 per workgroup
-    const int nbf4 = a.f_emit ? a.nbf : (a.nbf + 3) >> 2, nbw4 = (a.nbw + 3) >> 2;
-    const int qb0 = a.cfirst ? nbf4 + nbw4 : 0;  // first queue block
-    const int cb0 = a.cfirst ? 0 : a.nbq;        // first compaction block
+    // grid: queue blocks, then compaction blocks -- log workgroups: 4 tiles each (f_emit:
+    // one tile each), then the slot tiles 4 per workgroup
+    const int nbf4 = a.f_emit ? a.nbf : (a.nbf + 3) >> 2;
+    const int qb0 = 0, cb0 = a.nbq;
     if (bid >= qb0 && bid < qb0 + a.nbq) {
         const int b = xcd_block(bid - qb0, a.nbq);
         const int64_t pos = (int64_t)b * kBS + threadIdx.x;
@@ -2929,7 +2831,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(Sv, Lc), Ll);
         int status = 0;
         if (maxc > R && L >= R - 1) status = 1;   // rows beyond the table needed: rerun wider
-        if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log
+        else if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log (N_eff exact once R is)
         const int64_t pL = N_eff - S_L;
         const int64_t AL =
             (L < maxc && L < rlim) ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(totv, Lc), Ll) : 0;
@@ -3464,9 +3366,12 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Sv[0] : (Lc == 1 ? Sv[1] : Sv[2])), Ll);
         const int64_t oSL =
             (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Sov[0] : (Lc == 1 ? Sov[1] : Sov[2])), Ll);
+        // status 1 (the table is too narrow: every rank sees it, all relaunch) before
+        // status 2 (this rank's log shard is full), whose N_eff is exact only once the
+        // table is wide enough -- so the ranks never split between a relaunch and a failure
         int status = 0;
         if (maxc > R && L >= R - 1) status = 1;
-        if (a.head_local + N_eff > a.log_cap) status = 2;
+        else if (a.head_local + N_eff > a.log_cap) status = 2;
         const int64_t p = N_eff - S_L;
         const int64_t AL = (L < maxc && L < rlim) ? a.A[L] : 0;
         if (b == 0 && threadIdx.x == 0) {
@@ -3658,9 +3563,9 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
         }
     }
     lds_barrier();
-    int status = 0;
+    int status = 0;  // (precedence as in k_emit_shard)
     if (maxc > R && L >= R - 1) status = 1;  // R <= 64 * kWideMaxCh (the host caps it)
-    if (a.head_local + N_eff > a.log_cap) status = 2;
+    else if (a.head_local + N_eff > a.log_cap) status = 2;
     const int64_t p = N_eff - S_L;
     const int64_t AL = (L < maxc && L < rlim) ? a.A[L] : 0;
     if (b == 0 && threadIdx.x == 0) {
@@ -3875,12 +3780,9 @@ namespace fb {
 static inline int cdiv(int64_t a, int64_t b) { return (int)((a + b - 1) / b); }
 template <int NB>
 static void rs_pass(const RsPass &p, Stream h, Stream s) {
-    if (p.first)
-        hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(p.nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, p.kin, p.n, p.shift,
-                              p.db, p.hist, p.nblk, p.zero0, p.zero1, p.zbits, p.zwords, p.zhist[0], p.zhist[1],
-                              p.zhist[2], p.zhwords);
-    // timing: the pass starts with its first launch (histogram, scan or scatter)
-    hipEvent_t start = p.first ? nullptr : h.e0;
+    hipExtLaunchKernelGGL(k_rs_hist<NB>, dim3(p.nblk), dim3(kBS), 0, h.s, h.e0, h.e1, 0, p.kin, p.n, p.shift, p.db,
+                          p.hist, p.nblk, p.zero0, p.zero1, p.zbits, p.zwords);
+    hipEvent_t start = nullptr;
     const uint32_t *tot = nullptr;
     if (p.nblk > kRsScanMin) {
         uint32_t *t = p.hist + (size_t)p.nblk * NB;
@@ -3890,7 +3792,7 @@ static void rs_pass(const RsPass &p, Stream h, Stream s) {
         tot = t;
     }
     hipExtLaunchKernelGGL(k_rs_scatter<NB>, dim3(p.nblk), dim3(kBS), 0, s.s, start, s.e1, 0, p.kin, p.vin, p.kout,
-                          p.vout, p.n, p.shift, p.db, p.hist, p.nblk, p.identity_vals, tot, p.hnext);
+                          p.vout, p.n, p.shift, p.db, p.hist, p.nblk, p.identity_vals, tot);
 }
 void launch_rs_pass(const RsPass &p, Stream h, Stream s) {
     if (p.db <= 8)
@@ -3908,11 +3810,7 @@ void launch_ev_link(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_link, dim3(grid + a.cm_blocks), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
-    // slot_apply: the slot blocks apply the touched slots too (no message blocks)
-    if (a.slot_apply && a.nbw)
-        hipExtLaunchKernelGGL(k_ev_apply_slots, dim3(a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
-    else
-        hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_copy_multi(const CopyMulti &m, Stream st) {
     if (m.n <= 0 && m.otiles <= 0) return;
@@ -3947,7 +3845,7 @@ void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
     const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : a.nbw;
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;
-    FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq), nbf ? lds : 0, st, a);
+    FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq + (a.cm_fold ? a.cm_blocks : 0)), nbf ? lds : 0, st, a);
 }
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
     const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot

@@ -18,6 +18,11 @@ from ._lib import FaasbalError, TickResult
 
 _NONE = None
 
+# Test paths (fb_set_path) applied to every context created in this process: the
+# launch sequences of other table sizes on small, oracle-checkable inputs.  Test
+# fixtures set them (tests/test_gpu_parity.py); production code leaves this empty.
+TEST_PATHS = {}
+
 
 def _p(a):
     return a.ctypes.data_as(C.c_void_p) if a is not None and a.size else None
@@ -59,6 +64,12 @@ class GpuBalancer:
         self.max_events = int(max_events)
         self.n_workers = 0
         self._E = 0
+        for name, value in TEST_PATHS.items():
+            self.set_path(name, value)
+
+    def set_path(self, name, value):
+        """fb_set_path: run another table size's launch sequence (results are identical)."""
+        self._chk(self.lib.fb_set_path(self.h, name.encode(), int(value)))
 
     def _create(self, max_workers, max_log, max_events, device):
         rc = self.lib.fb_create(C.byref(self.h), int(max_workers), int(max_log), int(max_events), int(device))
@@ -209,6 +220,9 @@ class GpuBalancer:
                 continue
             if t.dtype != dt or not t.is_cuda or not t.is_contiguous() or t.numel() != E:
                 raise ValueError("device batch: contiguous %s tensors of %d elements on the GPU expected" % (dt, E))
+            dev = t.device.index if t.device.index is not None else torch.cuda.current_device()
+            if dev != self.device:
+                raise ValueError("device batch on cuda:%d, the context's GPU is cuda:%d" % (dev, self.device))
             ptrs.append(C.c_void_p(t.data_ptr()) if E else None)
         self._chk(self.lib.fb_tick_stage(self.h, float(now), E, *ptrs))
         self._staged_E = E

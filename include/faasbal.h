@@ -258,6 +258,17 @@ int fb_selftest(fb_ctx *ctx, int32_t *errors);
  * builds compiled with -DFAASBAL_STAMPS); *n_total = buffer length in words. */
 int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_total);
 
+/* Test paths: run the launch sequence another table size would take on small
+ * (oracle-checkable) inputs.  Results are identical on every path.  name / value:
+ *   "plan"        0 auto, 1 the k_plan2 + k_emit2 sequence of large tables, 2 the
+ *                 chunked k_emit of round tables wider than 128 rows;
+ *   "logscan"     -1 auto, 0 never, 1 the log role as its own k_logscan launch;
+ *   "split_slots" -1 auto, 0 never, 1 the slot purge as its own k_slots launch;
+ *   "ev_ll"       1 per-slot linked lists (one GPU), 0 the radix sort of messages;
+ *   "rs_wide"     1 digits up to 11 bits while a batch has <= 4096 sort tiles, 0 8-bit.
+ * Between ticks only; FB_EINVAL for an unknown name or value. */
+int fb_set_path(fb_ctx *ctx, const char *name, int value);
+
 /* Synchronise the context stream (for wall-clock benchmarking). */
 int fb_sync(fb_ctx *ctx);
 

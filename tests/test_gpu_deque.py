@@ -13,6 +13,7 @@ import numpy as np
 import pytest
 
 from faasbal import FaasbalError, GpuBalancer, synth
+from faasbal.balancer import TEST_PATHS
 from oracle import DequeOracle, fixture_expect, fixture_ticks
 
 pytestmark = pytest.mark.gpu
@@ -141,7 +142,7 @@ def test_deque_relaunch_without_commit_is_identical():
 
 @pytest.fixture
 def force_plan(monkeypatch):
-    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "1")
+    monkeypatch.setitem(TEST_PATHS, "plan", 1)
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -155,5 +156,5 @@ def test_deque_config3_plan_path(force_plan):
 
 @pytest.mark.parametrize("seed", range(3))
 def test_deque_random_chunked_emit(monkeypatch, seed):
-    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "2")
+    monkeypatch.setitem(TEST_PATHS, "plan", 2)
     test_deque_random_multitick_vs_oracle(seed + 20)

@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 
 from faasbal import GpuBalancer, FaasbalError, synth
+from faasbal.balancer import TEST_PATHS
 from oracle import Oracle, fixture_expect, fixture_ticks
 
 pytestmark = pytest.mark.gpu
@@ -391,7 +392,7 @@ def test_invalid_messages_in_pinned_batches(bad):
 @pytest.fixture
 def force_plan(monkeypatch):
     """Route ticks through the 3-launch path (k_plan), used for large grids."""
-    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "1")
+    monkeypatch.setitem(TEST_PATHS, "plan", 1)
 
 
 @pytest.mark.parametrize("seed", range(8))
@@ -409,27 +410,10 @@ def test_golden_plan_path(force_plan):
 
 
 @pytest.fixture
-def column_plan(monkeypatch):
-    """The 3-launch path with k_plan's per-round column scans instead of k_plan2's
-    group rows (FAASBAL_GPLAN=0)."""
-    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "1")
-    monkeypatch.setenv("FAASBAL_GPLAN", "0")
-
-
-@pytest.mark.parametrize("seed", range(4))
-def test_random_multitick_column_plan(column_plan, seed):
-    test_random_multitick_vs_oracle(seed + 40)
-
-
-def test_config3_column_plan(column_plan):
-    test_config3_full_size()
-
-
-@pytest.fixture
 def force_chunked_emit(monkeypatch):
     """The 3-launch path with the chunked k_emit (used when R > 128) instead of
     k_emit2 after k_plan."""
-    monkeypatch.setenv("FAASBAL_FORCE_PLAN", "2")
+    monkeypatch.setitem(TEST_PATHS, "plan", 2)
 
 
 @pytest.mark.parametrize("seed", range(4))
@@ -449,14 +433,14 @@ def test_device_primitives_selftest():
 @pytest.fixture
 def logscan(monkeypatch):
     """Route the log role through k_logscan (died bitmap in LDS), the default past 128K slots."""
-    monkeypatch.setenv("FAASBAL_LOGSCAN", "1")
+    monkeypatch.setitem(TEST_PATHS, "logscan", 1)
 
 
 @pytest.fixture
 def split_slots(monkeypatch):
     """Separate k_slots launch + global died bitmap (tables too large for k_logscan's LDS)."""
-    monkeypatch.setenv("FAASBAL_LOGSCAN", "0")
-    monkeypatch.setenv("FAASBAL_SPLIT_SLOTS", "1")
+    monkeypatch.setitem(TEST_PATHS, "logscan", 0)
+    monkeypatch.setitem(TEST_PATHS, "split_slots", 1)
 
 
 @pytest.mark.parametrize("seed", range(12))
@@ -597,22 +581,22 @@ def _sort_tick(W, E, hot_frac, seed, purge_mode=1, hot_n=5, expect_reruns=None):
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
     _cmp_state(g, o, 0)
-    if expect_reruns is not None and os.environ.get("FAASBAL_EV_LL", "1") != "0":  # reruns: linked-list path only
+    if expect_reruns is not None and TEST_PATHS.get("ev_ll", 1) != 0:  # reruns: linked-list path only
         assert (a["result"]["reruns"] > 0) == expect_reruns, a["result"]["reruns"]
 
 
 @pytest.fixture
 def radix(monkeypatch):
-    """FAASBAL_EV_LL=0: every message tick groups its events by the radix sort."""
-    monkeypatch.setenv("FAASBAL_EV_LL", "0")
+    """fb_set_path("ev_ll", 0): every message tick groups its events by the radix sort."""
+    monkeypatch.setitem(TEST_PATHS, "ev_ll", 0)
 
 
 @pytest.mark.parametrize("W,E,wide", [((1 << 17) + 5, 12000, "1"), (1 << 20, 2000, "1"), (1 << 21, 1000, "1"),
                                       ((1 << 17) + 5, 12000, "0"), (1 << 20, 2000, "0")])
 def test_event_sort_wide_digits(radix, monkeypatch, W, E, wide):
     """Slot spaces of 17-22 bits: the event sort runs two passes of 9-11-bit
-    digits (FAASBAL_RS_WIDE=0: three of 8 bits); identical to the oracle."""
-    monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
+    digits (fb_set_path("rs_wide", 0): three of 8 bits); identical to the oracle."""
+    monkeypatch.setitem(TEST_PATHS, "rs_wide", int(wide))
     _sort_tick(W, E, 0.0, W + E)
 
 
@@ -653,7 +637,7 @@ def test_event_link_limit(n_hot):
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
     _cmp_state(g, o, 0)
-    if os.environ.get("FAASBAL_EV_LL", "1") != "0":
+    if TEST_PATHS.get("ev_ll", 1) != 0:
         assert (a["result"]["reruns"] > 0) == (n_hot > 16)
 
 
@@ -663,37 +647,30 @@ def test_event_sort_large_batches(radix, monkeypatch, W, E, wide):
     """Batches of more than kRsScanMin sort tiles (E > 128 K): the column prefixes
     of the [tile][digit] counts come from their own launch (k_rs_scan) before each
     scatter; identical to the oracle (heap purge) up to 2 M messages in one tick."""
-    monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
+    monkeypatch.setitem(TEST_PATHS, "rs_wide", int(wide))
     _sort_tick(W, E, 0.3, W + E, purge_mode=2)
 
 
-@pytest.mark.parametrize("W,E,wide", [(1 << 20, 2000, "1"), ((1 << 17) + 5, 12000, "0"), (1 << 20, 300_000, "1")])
-def test_event_sort_fused_histograms(radix, monkeypatch, W, E, wide):
-    """FAASBAL_RS_FUSE=1: every pass after the first takes its histogram from the
-    previous scatter's atomics (no histogram launch); identical to the oracle with
-    two and three passes, and past the column-prefix launch's threshold."""
-    monkeypatch.setenv("FAASBAL_RS_FUSE", "1")
-    monkeypatch.setenv("FAASBAL_RS_WIDE", wide)
-    _sort_tick(W, E, 0.3, W + E + 1, purge_mode=2)
-
-@pytest.fixture
-def purge_in_scan(monkeypatch):
-    """FAASBAL_PURGE_APPLY=0: message ticks purge the slots in k_scan's W role (as
-    before the purge moved into k_ev_apply_ll's launch)."""
-    monkeypatch.setenv("FAASBAL_PURGE_APPLY", "0")
-
-
-@pytest.mark.parametrize("seed", range(3))
-def test_random_multitick_purge_in_scan(purge_in_scan, seed):
-    test_random_multitick_vs_oracle(seed)
-
-
-def test_churn_stream_purge_in_scan(purge_in_scan):
-    test_churn_stream_vs_oracle()
-
-
-def test_churn_stream_side_stream(monkeypatch):
-    """FAASBAL_FORK=1: k_logscan beside k_scan on a second stream (joined before k_plan2)."""
-    monkeypatch.setenv("FAASBAL_FORK", "1")
-    monkeypatch.setenv("FAASBAL_LOGSCAN", "1")
-    test_churn_stream_vs_oracle()
+@pytest.mark.parametrize("W,dead", [(8192, 0.05), (65536, 0.05)])
+def test_idle_ticks_commit_folded_into_scan(W, dead):
+    """Committed idle ticks back to back (the configs[2] shape: no messages, a clock that
+    advances so workers keep expiring): each tick's commit -- the evicted records'
+    deletion (task_dispatcher.py:246-247) and its orphaned log entries -- rides in the
+    next tick's k_scan (W role and extra blocks); outputs, state and in-flight counts
+    equal the oracle's every tick, also when a state read flushes the commit first."""
+    st = synth.zipf_state(W=W, seed=5, dead_frac=dead)
+    T = 4 * W
+    g, o = _pair(st, len(st["log"]) + 12 * T + 16)
+    carried = 0
+    for t in range(6):
+        now = 1000.0 + 1.5 * t
+        n = carried + T
+        args = (now, 10.0, [], [], [], [], [], n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp_out(a, b, t)
+        assert t > 0 or len(b["evicted"]) > 0
+        if t % 2:  # a state read flushes the pending commit as its own launch
+            _cmp_state(g, o, t)
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    _cmp_state(g, o, 6)
+    g.close()

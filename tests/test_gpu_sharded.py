@@ -10,6 +10,7 @@ import numpy as np
 import pytest
 
 from faasbal import synth
+from faasbal.balancer import TEST_PATHS
 from oracle import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -164,7 +165,7 @@ def test_sharded_world1_equals_one_gpu():
 @pytest.fixture
 def logscan(monkeypatch):
     """Phase 1's log role through k_logscan (the default past 128K local slots)."""
-    monkeypatch.setenv("FAASBAL_LOGSCAN", "1")
+    monkeypatch.setitem(TEST_PATHS, "logscan", 1)
 
 
 @pytest.mark.parametrize("seed", range(6))
@@ -262,3 +263,38 @@ def test_sharded_fill_level_beyond_128(world):
         carried = n + len(b["orphans"]) - len(b["assign"])
     assert max(levels) > 128, levels
     assert relaunches, "the first wide tick must ask for a relaunch"
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_wide_table_with_tight_log_shards(world):
+    """A narrow first launch cannot know N_eff (free counts beyond its round table), so
+    its log check would see the whole backlog: more pending tasks (1.5 M) than the
+    ranks' capacity (~0.9 M) and log shards sized for the capacity, not the backlog.
+    Every rank must ask for the relaunch (FB_ERERUN before FB_ENOSPC), and
+    the wide relaunch fits and matches the oracle."""
+    import torch  # noqa: F401
+    from faasbal.sharded import ShardedBalancer
+    rng = np.random.default_rng(90 + world)
+    W, now = 600, 1000.0
+    reg = np.ones(W, np.uint8)
+    free = rng.integers(0, 3001, W).astype(np.int32)
+    hb = now - rng.random(W) * 9.9
+    queue = rng.permutation(np.nonzero(free > 0)[0]).astype(np.int32)
+    log = rng.integers(-1, W, 20_000).astype(np.int32)
+    st = dict(reg=reg, free=free, hb=hb, epoch=np.zeros(W, np.uint32), queue=queue, log=log)
+    T = 1_500_000
+    cap_sum = int(free[queue].sum())
+    assert cap_sum < 1_000_000 < T
+    rank_cap = len(log) + 1_100_000  # > the capacity any rank can take, < the backlog
+    bals = [ShardedBalancer(r, world, W, rank_cap, max_events=16) for r in range(world)]
+    for b in bals:
+        b.load(st)
+    o = Oracle(W, len(log) + T + 16, purge_mode=1)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    relaunches = []
+    a, r = _group_tick(bals, now, 10.0, [], [], [], [], [], T, relaunches=relaunches)
+    b = o.tick(now, 10.0, [], [], [], [], [], T)
+    assert relaunches and r["n_assigned"] == cap_sum and r["fill_level"] > 128
+    _cmp(bals, o, a, b, 0)
+    for x in bals:
+        x.close()

@@ -11,7 +11,7 @@ the general path.  Window mode is forced on small contexts (fb_set_window(1)); t
 import numpy as np
 import pytest
 
-from faasbal import GpuBalancer, FaasbalError, synth
+from faasbal import GpuBalancer, FaasbalError, _lib, synth
 from oracle import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -220,19 +220,36 @@ def test_eager_tick_cannot_be_relaunched_uncommitted():
     g.close()
 
 
-@pytest.fixture
-def slot_apply(monkeypatch):
-    """Touched slots applied in slot order by k_ev_apply_slots (FAASBAL_SLOT_APPLY=1)."""
-    monkeypatch.setenv("FAASBAL_SLOT_APPLY", "1")
-
-
-@pytest.mark.parametrize("seed,W,T,dt", [(0, 8192, 512, 0.5), (3, 20000, 2048, 0.05)])
-def test_window_stream_slot_apply(slot_apply, seed, W, T, dt):
-    test_window_stream_vs_oracle(seed, W, T, dt, eager=True)
-
-
-@pytest.mark.parametrize("seed", range(0, 24, 2))
-def test_window_random_slot_apply(slot_apply, seed):
-    """Every message kind, runs of several messages per slot (sorted into arrival order by
-    the slot's thread), repeated results, deaths between a slot's own messages."""
-    test_window_random_vs_oracle(seed)
+@pytest.mark.parametrize("eager", [False, True], ids=["deferred", "eager"])
+def test_window_state_reads_refused_until_commit(eager):
+    """fb_read_state / fb_device_view_get / fb_read_inflight between the launch and the
+    commit of a window tick fail with FB_ESTATE (the window moves at the commit, on the
+    device already with eager commits); after the commit they read the new state and the
+    stream continues identical to the oracle."""
+    st, ticks = _stream(5, 4096, 256, 0.3, n_ticks=4)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g, o = _pair(st, 2 * len(st["log"]) + 8 * 256 + 16, max_events=E, purge_mode=2)
+    g.set_eager_commit(eager)
+    carried, refused = 0, 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        g.launch(*args)
+        res = g.wait()
+        a = dict(result=res, reconnect=g.event_status(), assign=g.assignments(), orphans=g.orphans(),
+                 evicted=g.evicted())
+        win, r_t = g.window_stats()[0], 0
+        for read in (g.read_state, g.device_view, g.inflight):
+            try:
+                read()
+            except FaasbalError as e:
+                assert e.code == _lib.FB_ESTATE
+                r_t += 1
+        g.commit()
+        b = o.tick(*args)
+        _cmp(g, o, a, b, t)
+        assert r_t == (3 if g.window_stats()[0] > win else 0), (t, r_t)
+        refused += r_t
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    assert refused >= 3
+    g.close()

@@ -1,0 +1,16 @@
+#!/bin/bash
+# Round-4 check pass on one box: the GPU suite (per-test timeout), smoke, the default bench
+# line.  Each step has its own time limit; the chain stops at the first failure.
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
+TAG=${1:-chk}
+SEL=${2:-}
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread $SEL \
+    > gpurun_out/${TAG}_pytest.log 2>&1 || { tail -40 gpurun_out/${TAG}_pytest.log; exit 1; }
+tail -2 gpurun_out/${TAG}_pytest.log
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/${TAG}_smoke.log 2>&1 \
+    || { tail -20 gpurun_out/${TAG}_smoke.log; exit 2; }
+tail -1 gpurun_out/${TAG}_smoke.log
+timeout -k 10 300 python -u bench.py > gpurun_out/${TAG}_bench.json 2> gpurun_out/${TAG}_bench.err \
+    || { tail -20 gpurun_out/${TAG}_bench.err; exit 3; }
+cat gpurun_out/${TAG}_bench.json

@@ -1,8 +1,10 @@
 """Probe: per-rank device time of the sharded tick at world N,
 all N rank contexts on ONE GPU (exchange summed on-device, no RCCL): what one
-rank of the N-GPU weak-scaling bench computes per tick, minus the all-reduce.
+rank of the N-GPU bench computes per tick, minus the all-reduce.  strong (default,
+bench.py --gpus N): the configs[2] table of 64K workers / 1M tasks split N ways;
+weak: N x 64K workers / N x 1M tasks.  Reports rank 0 and the slowest rank.
 
-    python tools/shard_probe.py [--world 2 4 8 --reps 50]
+    python tools/shard_probe.py [--world 2 4 8 --reps 50 --scaling strong]
 """
 import argparse
 import os
@@ -22,9 +24,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--world", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--reps", type=int, default=50)
+    ap.add_argument("--scaling", default="strong", choices=("strong", "weak"))
     args = ap.parse_args()
     for world in args.world:
-        W, T = 65536 * world, 1_000_000 * world
+        k = world if args.scaling == "weak" else 1
+        W, T = 65536 * k, 1_000_000 * k
         st = synth.zipf_state(W=W, seed=0)
         F = len(st["log"])
         bals = [ShardedBalancer(r, world, W, 2 * F // world + T + 16, max_events=1) for r in range(world)]
@@ -54,10 +58,14 @@ def main():
         for _ in range(args.reps):
             tick()
         dt = (time.perf_counter() - t0) / args.reps
-        kt = bals[0].timing_read()
-        per = {k: round(ms / args.reps * 1e3, 2) for k, (ms, n) in kt.items()}
-        print("world %d: rank-0 device us per tick %s (sum %.1f), exchange %d B, serial wall %.0f us"
-              % (world, per, sum(per.values()), bals[0].exchange().numel(), dt * 1e6), flush=True)
+        pers = []
+        for b in bals:
+            kt = b.timing_read()
+            pers.append({k: round(ms / args.reps * 1e3, 2) for k, (ms, n) in kt.items()})
+        slow = max(range(world), key=lambda r: sum(pers[r].values()))
+        print("%s world %d: rank-0 device us per tick %s (sum %.1f); slowest rank %d: sum %.1f; exchange %d B, "
+              "serial wall %.0f us" % (args.scaling, world, pers[0], sum(pers[0].values()), slow,
+                                       sum(pers[slow].values()), bals[0].exchange().numel(), dt * 1e6), flush=True)
         for b in bals:
             b.timing_enable(False)
             b.close()
