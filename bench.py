@@ -348,57 +348,31 @@ def self_launch(args):
 
 
 def host_observed(g, st, T, steps, n_assigned):
-    """Decisions the Python host can act on: per tick launch, wait and the readback of
-    the tick's decisions into pinned host memory, in the compact form (slot and
-    min(c, L + 1) per LRU position: every task's slot in closed form, 5 B per queued
-    worker) and, for comparison, as the per-task slot array (4 B per task), each with
-    the orphans and evicted slots.  The tick is relaunched uncommitted (same workload
-    every step); the commit (one kernel, then the host's bookkeeping) is timed once at
-    the end and added per tick.  The host-side expansion of the compact form into the
-    per-task array (fb_expand_compact, threads) is timed separately."""
+    """Decisions the Python host can act on, on the path the drop-in dispatcher uses
+    (GpuPushDispatcher._run -> GpuBalancer.tick(pinned=True), dispatcher.py:307-391): per
+    tick launch, wait, the per-message status bytes and one readback of the per-task
+    slots, orphans and evicted slots into reusable pinned arrays.  The tick is relaunched
+    uncommitted (same workload every step); the commit (one kernel, then the host's
+    bookkeeping) is timed separately and added per tick.  Beside it, the compact form
+    (slot and min(c, L + 1) per LRU position, 5 B per queued worker, written into
+    registered pinned arrays by the tick itself) and its host expansion into the per-task
+    array -- a consumer that can walk rounds instead of tasks."""
     Q = len(st["queue"])
-    g.set_compact(True)
-    g.launch(1000.0, 10.0, n_pending=T)
-    r = g.wait()
-    buf = g.pinned(max(n_assigned, 1), np.int32)
-    obuf = g.pinned(max(len(st["log"]), 1), np.int64)  # room for every in-flight entry (fb_set_compact_out)
-    ebuf = g.pinned(max(len(st["reg"]), 1), np.int32)  # room for every worker (fb_set_compact_out)
-    cap = Q + 16
-    sbuf, cbuf = g.pinned(cap, np.int32), g.pinned(cap, np.uint8)
 
-    def timed(read):
+    def timed(step):
         for _ in range(3):
-            g.launch(1000.0, 10.0, n_pending=T)
-            g.wait()
-            read()
+            step()
         g.sync()
         t0 = time.perf_counter()
         for _ in range(steps):
-            g.launch(1000.0, 10.0, n_pending=T)
-            g.wait()
-            read()
+            step()
         return (time.perf_counter() - t0) / steps
 
-    # the ticks write the compact form, orphans and evicted slots into these pinned arrays
-    # while they run (fb_set_compact_out): the readback call copies nothing
-    g.set_compact_out(sbuf, cbuf, obuf, ebuf)
-    dt_c = timed(lambda: g.outputs_compact(sbuf, cbuf, obuf, ebuf))
-    g.set_compact_out(None, None, None, None)
-    dt_f = timed(lambda: g.outputs(buf, obuf, ebuf))
-    # the expansion on the host (same tick), checked against the per-task readback
-    g.launch(1000.0, 10.0, n_pending=T)
-    g.wait()
-    sl, cc, _, _ = g.outputs_compact(sbuf, cbuf, obuf, ebuf)
-    out = np.zeros(max(n_assigned, 1), np.int32)
-    g.expand(sl, cc, out)
-    te = time.perf_counter()
-    for _ in range(5):
-        g.expand(sl, cc, out)
-    t_exp = (time.perf_counter() - te) / 5
-    g.outputs(buf, obuf, ebuf)
-    if not np.array_equal(out[:n_assigned], buf[:n_assigned]):
-        raise SystemExit("host_observed: the expanded compact form differs from the per-task readback")
-    g.set_compact(False)
+    def tick_path():
+        out = g.tick(1000.0, 10.0, n_pending=T, commit=False, pinned=True)
+        assert len(out["assign"]) == n_assigned
+
+    dt_t = timed(tick_path)
     # the commit (one kernel + host bookkeeping), averaged over a few ticks, the
     # state reloaded (untimed) after each so every commit is the same tick's
     tc, nc = 0.0, 5
@@ -411,17 +385,45 @@ def host_observed(g, st, T, steps, n_assigned):
         tc += time.perf_counter() - t1
         g.load(st)
     tc /= nc
-    return {"value": n_assigned / (dt_c + tc), "unit": "assignments/s", "ms_per_tick": (dt_c + tc) * 1e3,
-            "readback_ms_per_tick": dt_c * 1e3, "commit_ms": tc * 1e3, "readback_bytes": 5 * len(sl),
-            "readback_form": "compact: slot + min(c, L+1) per LRU position, written into registered pinned "
-                             "arrays by the tick itself (fb_set_compact_out)",
-            "expand_ms": t_exp * 1e3,
-            "value_with_expand": n_assigned / (dt_c + tc + t_exp),
-            "per_task_readback": {"value": n_assigned / (dt_f + tc), "ms_per_tick": (dt_f + tc) * 1e3,
-                                  "readback_bytes": 4 * n_assigned},
-            "note": "launch + wait + pinned readback of the tick's decisions + orphans + evicted (uncommitted "
-                    "relaunch), plus the commit (average of 5); value_with_expand adds the host expansion of "
-                    "the compact form into one slot per task"}
+    # the compact form, for comparison
+    g.set_compact(True)
+    g.launch(1000.0, 10.0, n_pending=T)
+    g.wait()
+    obuf = g.pinned(max(len(st["log"]), 1), np.int64)  # room for every in-flight entry (fb_set_compact_out)
+    ebuf = g.pinned(max(len(st["reg"]), 1), np.int32)  # room for every worker
+    sbuf, cbuf = g.pinned(Q + 16, np.int32), g.pinned(Q + 16, np.uint8)
+    g.set_compact_out(sbuf, cbuf, obuf, ebuf)
+
+    def compact_path():
+        g.launch(1000.0, 10.0, n_pending=T)
+        g.wait()
+        g.outputs_compact(sbuf, cbuf, obuf, ebuf)
+
+    dt_c = timed(compact_path)
+    g.set_compact_out(None, None, None, None)
+    g.launch(1000.0, 10.0, n_pending=T)
+    g.wait()
+    sl, cc, _, _ = g.outputs_compact(sbuf, cbuf, obuf, ebuf)
+    out = np.zeros(max(n_assigned, 1), np.int32)
+    g.expand(sl, cc, out)
+    te = time.perf_counter()
+    for _ in range(5):
+        g.expand(sl, cc, out)
+    t_exp = (time.perf_counter() - te) / 5
+    ref = g.tick(1000.0, 10.0, n_pending=T, commit=False, pinned=True)["assign"]
+    if not np.array_equal(out[:n_assigned], ref[:n_assigned]):
+        raise SystemExit("host_observed: the expanded compact form differs from the per-task readback")
+    g.set_compact(False)
+    return {"value": n_assigned / (dt_t + tc), "unit": "assignments/s", "ms_per_tick": (dt_t + tc) * 1e3,
+            "readback_ms_per_tick": dt_t * 1e3, "commit_ms": tc * 1e3, "readback_bytes": 4 * n_assigned,
+            "readback_form": "per task: GpuBalancer.tick(pinned=True), the dispatcher's path -- status bytes + "
+                             "slots / orphans / evicted in one readback into reusable pinned arrays",
+            "compact": {"value": n_assigned / (dt_c + tc), "ms_per_tick": (dt_c + tc) * 1e3,
+                        "readback_bytes": 5 * len(sl), "expand_ms": t_exp * 1e3,
+                        "value_with_expand": n_assigned / (dt_c + tc + t_exp)},
+            "note": "launch + wait + readback of the tick's decisions (uncommitted relaunch), plus the commit "
+                    "(average of 5); compact: the tick writes slot + min(c, L+1) per LRU position into registered "
+                    "pinned arrays, value_with_expand adds the host expansion into one slot per task"}
 
 
 def committed_tick(st, T, reps=10):

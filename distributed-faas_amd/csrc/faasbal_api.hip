@@ -704,17 +704,20 @@ int enqueue_tick(fb_ctx *c) {
     a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
     // large tables for k_emit2: group rows too, scanned by k_plan2
     const bool gplan = !a.fused && a.segw && !c->shard;
-    if ((a.fused || gplan) && !c->l_win) {  // (a window tick uses no group rows)
-        // group rows: fused, about sqrt(nbq) groups of 2^gshift queue blocks (k_emit2 reads
-        // both); k_plan2, the smallest groups that make at most 64 rows (one workgroup each)
+    // sharded phase 2 with a round table of <= 128 rows: group rows instead of k_plan
+    const bool sgrp = c->shard && c->phase == 2 && R <= kRFused;
+    if ((a.fused || gplan || sgrp) && !c->l_win) {  // (a window tick uses no group rows)
+        // group rows: fused / sharded, about sqrt(nbq) groups of 2^gshift queue blocks (the
+        // emit reads both); k_plan2, the smallest groups that make at most 64 rows (one
+        // workgroup each)
         int gs = 0;
-        if (a.fused)
-            while ((1 << (2 * gs)) < nbq) ++gs;
+        if (a.fused || sgrp)
+            while ((1 << (2 * gs)) < nbq || cdiv(nbq, (int64_t)1 << gs) > 64) ++gs;
         else
             while (cdiv(nbq, (int64_t)1 << gs) > 64) ++gs;
         a.grp_on = 1;
         a.gshift = gs;
-        a.gstride = R + 4;
+        a.gstride = sgrp ? 2 * R + 4 : R + 4;
         a.ngrp = (int)cdiv(nbq, 1 << gs);
         if (a.ngrp > 64 || (int64_t)a.ngrp * a.gstride > kGrpWords)
             return fail(c, FB_ERANGE, "group rows (%d x %d words) exceed the reservation", a.ngrp, a.gstride);
@@ -1098,7 +1101,7 @@ int enqueue_tick(fb_ctx *c) {
             Timer t(c, "scan2");
             launch_scan(a, t.st());
         }
-        {
+        if (!a.grp_on) {  // wide tables: k_plan's column scans
             Timer t(c, "plan");
             launch_plan(a, t.st());
         }

@@ -1748,8 +1748,15 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             if ((int)threadIdx.x < rn) {
                 const int r = threadIdx.x;
                 t = wc[0][r] + wc[1][r] + wc[2][r] + wc[3][r];
+                const uint32_t ot = owc[0][r] + owc[1][r] + owc[2][r] + owc[3][r];
                 a.qcnt[(size_t)b * a.R + rc + r] = t;
-                a.ocnt[(size_t)b * a.R + rc + r] = owc[0][r] + owc[1][r] + owc[2][r] + owc[3][r];
+                a.ocnt[(size_t)b * a.R + rc + r] = ot;
+                // group rows (no k_plan): all positions in columns [0, R), this rank's in [R, 2R)
+                if (a.grp_on) {
+                    uint32_t *row = a.grp + (size_t)(b >> a.gshift) * a.gstride;
+                    if (t) atomicAdd(&row[rc + r], t);
+                    if (ot) atomicAdd(&row[a.R + rc + r], ot);
+                }
             }
             const uint32_t ts = wave_sum_u32(t);
             if (lane_id() == 0) l4[wave_id()] = ts;
@@ -1828,7 +1835,12 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         for (int w = 1; w < kWaves; ++w) bm = m4[w] > bm ? m4[w] : bm;
         a.qbm_raw[b] = bm;
         a.csum[b] = csum;
-        if (a.grp_on && bm > 0) atomicMax(&a.grp[(b >> a.gshift) * a.gstride + a.R], (uint32_t)bm);
+        if (a.shard == 2 && a.grp_on) {  // max c and capacity into columns 2R, 2R + 1
+            uint32_t *row = a.grp + (size_t)(b >> a.gshift) * a.gstride;
+            if (bm) atomicMax(&row[2 * a.R], (uint32_t)bm);
+            if (csum) atomicAdd(&row[2 * a.R + 1], (uint32_t)csum);
+        }
+        if (a.grp_on && a.shard != 2 && bm > 0) atomicMax(&a.grp[(b >> a.gshift) * a.gstride + a.R], (uint32_t)bm);
     }
     STAMP(a, SO, 15);
 }
@@ -3293,10 +3305,18 @@ constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // and the own-log base So(r) + own block prefix + own earlier segments (for the
 // log position), one register per 64 rounds, read with readlane in the round
 // loop; block prefixes from k_plan, segment counts from the phase-2 k_scan.
+// GRP: no k_plan before this launch -- the totals and this block's prefixes per round come
+// from the group rows k_scan's phase-2 blocks added (all / own counts, max c, capacity),
+// plus the earlier blocks of its own group; the orphan totals from the exchange records
+// and this rank's tile counts.
+template <bool GRP>
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     prefetch_args(a);
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
+    if (GRP) {  // the other parity's group rows, for the next launch's k_scan atomics
+        for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
+    }
     if (bid < a.nbq) {
         const int b = bid;
         const int R = a.R;
@@ -3307,13 +3327,81 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         const int sq = lq_slot(a, pq);
         const int32_t rawq = a.c_arr[pq];
         int64_t Av[kRCh], oAv[kRCh], pv[kRCh], opv[kRCh];
+        int64_t O, cap;
+        int maxc;
+        if (GRP) {
+            // 2R columns (round r of all positions, then of this rank's), tpc consecutive
+            // threads per column: each column's total over the group rows and this block's
+            // prefix (earlier groups + earlier blocks of its group), every tpc-th row per thread
+            __shared__ uint32_t sT[2][kRFused], sP[2][kRFused];
+            __shared__ uint32_t smx[kWaves], scap[kWaves], sorf[kWaves];
+            int tpc = 1;
+            while (tpc * 4 * R <= kBS) tpc *= 2;  // R = 32: 4 threads per column
+            const int col = (int)threadIdx.x / tpc, j = (int)threadIdx.x % tpc;
+            const int tab = col >= R ? 1 : 0, r = col - tab * R;
+            const int g0 = b >> a.gshift, b0 = g0 << a.gshift;
+            uint32_t tot = 0, pre = 0;
+            if (col < 2 * R) {
+                const uint32_t *cg = a.grp + col;
+#pragma unroll 4
+                for (int g = j; g < a.ngrp; g += tpc) {
+                    const uint32_t v = cg[(size_t)g * a.gstride];
+                    tot += v;
+                    pre += g < g0 ? v : 0u;
+                }
+                const uint32_t *bc = (tab ? a.ocnt : a.qcnt) + r;
+#pragma unroll 4
+                for (int bb = b0 + j; bb < b; bb += tpc) pre += bc[(size_t)bb * R];
+            }
+            for (int o = 1; o < tpc; o <<= 1) {  // the column's tpc threads are adjacent lanes
+                tot += (uint32_t)__shfl_xor((int)tot, o);
+                pre += (uint32_t)__shfl_xor((int)pre, o);
+            }
+            if (col < 2 * R && j == 0) {
+                sT[tab][r] = tot;
+                sP[tab][r] = pre;
+            }
+            // max c and capacity (threads < ngrp), every rank's orphans (the exchange records)
+            // (capacity < Q x 128 and orphans < the 2^31-entry log: 32-bit sums)
+            uint32_t mx = 0, cp = 0, orf = 0;
+            if ((int)threadIdx.x < a.ngrp) {
+                const uint32_t *row = a.grp + (size_t)threadIdx.x * a.gstride;
+                mx = row[2 * R];
+                cp = row[2 * R + 1];
+            }
+            for (int g = threadIdx.x; g < a.world * kXRecLines; g += kBS) orf += (uint32_t)a.xrec[(size_t)g * 16];
+            mx = wave_max_u32(mx);
+            cp = wave_sum_u32(cp);
+            orf = wave_sum_u32(orf);
+            if (lane == 0) {
+                smx[w] = mx;
+                scap[w] = cp;
+                sorf[w] = orf;
+            }
+            __syncthreads();
 #pragma unroll
-        for (int k = 0; k < kRCh; ++k) {
-            const int r = min(64 * k + lane, R - 1);
-            Av[k] = a.A[r];
-            oAv[k] = a.oA[r];
-            pv[k] = a.qpre[(size_t)b * R + r];
-            opv[k] = a.opre[(size_t)b * R + r];
+            for (int k = 0; k < kRCh; ++k) {
+                const int rr = min(64 * k + lane, R - 1);
+                Av[k] = sT[0][rr];
+                oAv[k] = sT[1][rr];
+                pv[k] = sP[0][rr];
+                opv[k] = sP[1][rr];
+            }
+            maxc = (int)max(max(smx[0], smx[1]), max(smx[2], smx[3]));
+            cap = (int64_t)scap[0] + scap[1] + scap[2] + scap[3];
+            O = (int64_t)sorf[0] + sorf[1] + sorf[2] + sorf[3];
+        } else {
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k) {
+                const int r = min(64 * k + lane, R - 1);
+                Av[k] = a.A[r];
+                oAv[k] = a.oA[r];
+                pv[k] = a.qpre[(size_t)b * R + r];
+                opv[k] = a.opre[(size_t)b * R + r];
+            }
+            O = a.P->O;
+            cap = a.P->cap_total;
+            maxc = a.P->maxc;
         }
         uint32_t segc[kRCh] = {0, 0, 0}, osegc[kRCh] = {0, 0, 0};
         {
@@ -3335,9 +3423,6 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                     osegc[k] += in ? osv[k][q] : 0u;
                 }
         }
-        const int64_t O = a.P->O;
-        int64_t cap = a.P->cap_total;
-        const int maxc = a.P->maxc;
         const int rlim = maxc < R ? maxc : R;
         if (maxc > R) cap = INT64_MAX;
         const int64_t N = (a.redist ? O : 0) + a.T;  // purge-only ticks report orphans, dispatch none
@@ -3373,11 +3458,30 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         if (maxc > R && L >= R - 1) status = 1;
         else if (a.head_local + N_eff > a.log_cap) status = 2;
         const int64_t p = N_eff - S_L;
-        const int64_t AL = (L < maxc && L < rlim) ? a.A[L] : 0;
+        // |A_L| from this wave's totals (lane L & 63 of chunk L >> 6)
+        const int64_t ALv = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Av[0] : (Lc == 1 ? Av[1] : Av[2])), Ll);
+        const int64_t AL = (L < maxc && L < rlim) ? ALv : 0;
+        int64_t O_loc = 0, n_ev = 0;
+        if (GRP && b == 0) {
+            // this rank's orphans and evictions (its phase-1 tile counts) for the host
+            __shared__ uint32_t sfo[kWaves], sev[kWaves];
+            uint32_t fo = 0, ev = 0;
+            for (int t = threadIdx.x; t < a.nbf; t += kBS) fo += a.fcnt[t];
+            for (int t = threadIdx.x; t < a.nbw; t += kBS) ev += a.wcnt[t];
+            fo = wave_sum_u32(fo);
+            ev = wave_sum_u32(ev);
+            if (lane == 0) {
+                sfo[w] = fo;
+                sev[w] = ev;
+            }
+            __syncthreads();
+            O_loc = (int64_t)sfo[0] + sfo[1] + sfo[2] + sfo[3];
+            n_ev = (int64_t)sev[0] + sev[1] + sev[2] + sev[3];
+        }
         if (b == 0 && threadIdx.x == 0) {
             a.hout->O = O;
-            a.hout->O_local = a.P->O_local;
-            a.hout->n_evicted = a.P->n_evicted;
+            a.hout->O_local = GRP ? O_loc : a.P->O_local;
+            a.hout->n_evicted = GRP ? n_ev : a.P->n_evicted;
             a.hout->cap_total = cap;
             a.hout->maxc = maxc;
             a.hout->L = L;
@@ -3475,12 +3579,20 @@ __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid) {
     const bool frole = bid < a.nbq + nbf4;
     const int t = 4 * (frole ? bid - a.nbq : bid - a.nbq - nbf4) + w;
     if (t >= (frole ? a.nbf : a.nbw)) return;
+    // the tile's offset: k_plan's scan of the tile counts, or (no k_plan: group rows) the
+    // wave's own sum of the earlier tiles' counts
+    auto tile_pre = [&](const uint32_t *cnt, const int64_t *pre) -> int64_t {
+        if (!a.grp_on) return pre[t];
+        uint32_t v = 0;
+        for (int i = lane; i < t; i += 64) v += cnt[i];
+        return (int64_t)wave_sum_u32(v);
+    };
     if (frole) {
         // own orphans (global sequence numbers, ascending): lane l holds flag bytes
         // 4l .. 4l+3 of tile t, i.e. local entries t*2048 + 32l .. +32
         const uint32_t f4 = reinterpret_cast<const uint32_t *>(a.ofl + (size_t)t * kBS)[lane];
         const uint32_t n = (uint32_t)__popc(f4);
-        int64_t o = a.fpre[t] + (int64_t)(wave_incl_scan_u32(n) - n);
+        int64_t o = tile_pre(a.fcnt, a.fpre) + (int64_t)(wave_incl_scan_u32(n) - n);
         const int64_t base = (int64_t)t * kFTile + (int64_t)lane * 4 * kFItems;
         for (uint32_t m = f4; m; m &= m - 1) a.orphans[o++] = (int64_t)a.lseq[base + __builtin_ctz(m)];
     } else {
@@ -3494,7 +3606,7 @@ __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid) {
             e |= ((s0 + q < a.W) && (sv & kStEvicted)) ? (1u << q) : 0u;
         }
         const uint32_t n = (uint32_t)__popc(e);
-        int64_t o = a.wpre[t] + (int64_t)(wave_incl_scan_u32(n) - n);
+        int64_t o = tile_pre(a.wcnt, a.wpre) + (int64_t)(wave_incl_scan_u32(n) - n);
         for (uint32_t m = e; m; m &= m - 1) a.evicted[o++] = a.slot_base + s0 + __builtin_ctz(m);
     }
 }
@@ -3886,8 +3998,11 @@ void launch_emit_shard(const TickArgs &a, Stream st) {
                               st.e0, st.e1, 0, a);
         return;
     }
-    hipExtLaunchKernelGGL(k_emit_shard, dim3(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4), dim3(kBS), 0, st.s, st.e0,
-                          st.e1, 0, a);
+    const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
+    if (a.grp_on)
+        hipExtLaunchKernelGGL(k_emit_shard<true>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    else
+        hipExtLaunchKernelGGL(k_emit_shard<false>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_evict_gather(int32_t *dst, const uint8_t *st, const uint32_t *wcnt, int64_t *wpre, int W, Stream s) {
     const int nt = cdiv(W, kBS);

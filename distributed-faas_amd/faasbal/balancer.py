@@ -378,13 +378,29 @@ class GpuBalancer:
             self.commit()
         return out
 
+    def _pinned_out(self):
+        """Reusable pinned output arrays sized for the waited tick (grown geometrically)."""
+        r = self.last
+        need = (r["n_assigned"], r["n_orphans_local"], r["n_evicted"])
+        have = getattr(self, "_pout", None)
+        if have is None or any(len(b) < n for b, n in zip(have, need)):
+            old = have or (np.zeros(0, np.int32),) * 3
+            self._pout = tuple(self.pinned(max(n, 2 * len(b), 1024), dt) for b, n, dt in
+                               zip(old, need, (np.int32, np.int64, np.int32)))
+        return self._pout
+
     def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
-             commit=True, outputs=True):
-        """One full tick.  Returns dict(result, reconnect, assign, orphans, evicted)."""
+             commit=True, outputs=True, pinned=False):
+        """One full tick.  Returns dict(result, reconnect, assign, orphans, evicted).
+        ``pinned=True`` (the drop-in dispatcher's path): the three lists come back in one
+        readback into reusable pinned arrays -- views valid until the next tick."""
         self.launch(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
         res = self.wait()
         out = dict(result=res)
-        if outputs:
+        if outputs and pinned:
+            a, o, e = self.outputs(*self._pinned_out())
+            out.update(reconnect=self.event_status(), assign=a, orphans=o, evicted=e)
+        elif outputs:
             out.update(reconnect=self.event_status(), assign=self.assignments(), orphans=self.orphans(),
                        evicted=self.evicted())
         if commit:

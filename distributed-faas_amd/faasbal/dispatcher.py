@@ -303,9 +303,12 @@ class GpuPushDispatcher:
                 val[i] = v
             elif k == EV_RESULT:
                 seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
+        # a one-GPU balancer hands the tick's assignments / orphans / evicted slots back in one
+        # readback into pinned arrays, consumed below before the next tick
+        tkw = {"pinned": True} if isinstance(self.balancer, GpuBalancer) else {}
         try:
             out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
-                                     n_pending=len(self.pending))
+                                     n_pending=len(self.pending), **tkw)
         except FaasbalError as e:
             # in-flight log full: the tick was not committed.  Compaction renumbers every
             # in-flight sequence, so the results' sequence numbers are looked up again
@@ -321,7 +324,7 @@ class GpuPushDispatcher:
                 if kind[i] == EV_RESULT:
                     seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
             out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
-                                     n_pending=len(self.pending))
+                                     n_pending=len(self.pending), **tkw)
         res = out["result"]
         # ---- per-message replies, in arrival order (:356-358, :374-387; start(): :284-288,
         #      where a result from an unknown identity is still HSET before the KeyError)
