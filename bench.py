@@ -661,19 +661,31 @@ def main():
         dom_bytes = logscan_bytes(W, F)
     else:
         dom_bytes = tick_bytes(W // world, Q, F // world, O // world, n_assigned // world)
-    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     B = tick_bytes(W, Q, F, O, n_assigned)
+    # roofline bytes: SURVEY.md §8(d) -- the dominant kernel's share of the tick's bytes
+    # (one-GPU configs[2]: the emit carries everything but k_scan's 16 B per worker read);
+    # the builder's per-kernel model (queue / record traffic §8(d) does not count) beside it
+    model_frac = dom_bytes / (dom_ms * 1e-3) / 1e9 / HBM_PEAK_GBS
+    bytes_model = "SURVEY.md 8(d)"
+    if dom == "emit" and world == 1 and not deque and set(kern) == {"scan", "emit"}:
+        dom_bytes = B - 16 * W
+        bytes_model = "SURVEY.md 8(d): tick bytes 24W + 4(N-O) + 4F + 8O minus k_scan's 16W read"
+    else:
+        bytes_model = "builder model (bench.py: %s_bytes)" % dom
+    achieved = dom_bytes / (dom_ms * 1e-3) / 1e9
     value = n_assigned * args.steps / dt  # whole job: the global tick's dispatches
     # HBM bytes per launch of the dominant kernel from the committed PMC passes of
     # this same command (tools_profile.sh -> tools/prof_summary.py), when they match
-    traffic, traffic_src = None, None
+    traffic, traffic_src, rocprof_ms = None, None, None
     tp = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(tp):
-        tj = json.load(open(tp))
-        if (tj.get("workers"), tj.get("tasks_per_tick"), tj.get("n_gpus")) == (W, T, world) and dom in tj["kernels"]:
+        tj = json.load(open(tp)).get("entries", {}).get("%d,%d,%d" % (W, T, world))
+        if tj and dom in tj["kernels"]:
             traffic = tj["kernels"][dom]["hbm_bytes"]
-            traffic_src = "profiles/%s_pmc.csv, %s_pmc_summary.json (2*FETCH_SIZE + WRITE_SIZE per launch)" % (
-                tj["tag"], tj["tag"])
+            rocprof_ms = (tj["kernels"][dom].get("trace_avg_ns") or 0) * 1e-6 or None
+            traffic_src = ("profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch, separate rocprofv3 --pmc "
+                           "passes), rocprof average from profiles/%s_kernel_stats.csv; summary profiles/%s_traffic.json"
+                           % (tj["tag"], tj["tag"], tj["tag"]))
     line = {
         "metric": "task assignments/sec + % HBM roofline, 1M tasks x 64K workers, 1/2/4/8 GPU",
         "value": value,
@@ -710,8 +722,9 @@ def main():
                    "parallelism": "dp1" if world == 1 else "worker-table shards x%d" % world},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes": dom_bytes,
-                     "kernel_avg_ms": dom_ms},
+                     "algorithmic_bytes": dom_bytes, "bytes_model": bytes_model,
+                     "kernel_avg_ms": dom_ms, "kernel_avg_ms_rocprof": rocprof_ms,
+                     "model_frac": model_frac},
         "tick": {"algorithmic_bytes": B, "device_ms": tick_dev_ms,
                  "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,
                  "kernels_avg_ms": {k: v[0] for k, v in kern.items()}},

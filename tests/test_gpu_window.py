@@ -253,3 +253,44 @@ def test_window_state_reads_refused_until_commit(eager):
         carried = n + len(b["orphans"]) - len(b["assign"])
     assert refused >= 3
     g.close()
+
+
+def _large_stream(g, o, ticks, eager):
+    g.set_eager_commit(eager)
+    carried, n_orph = 0, 0
+    for t, tk in enumerate(ticks):
+        n = carried + tk["n_new"]
+        args = (tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n)
+        a, b = g.tick(*args), o.tick(*args)
+        for k in ("reconnect", "assign", "orphans", "evicted"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg="tick %d: %s" % (t, k))
+        n_orph += len(b["orphans"])
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    sg, so = g.read_state(), o.export()
+    for k in ("reg", "queue", "log"):
+        np.testing.assert_array_equal(sg[k], so[k], err_msg=k)
+    m = so["reg"].astype(bool)
+    np.testing.assert_array_equal(sg["free"][m], so["free"][m])
+    np.testing.assert_array_equal(sg["hb"][m], so["hb"][m])
+    return n_orph
+
+
+@pytest.mark.parametrize("eager", [False, True], ids=["deferred", "eager"])
+def test_large_table_window_stream_vs_oracle(eager):
+    """Large tables (> 128K workers, auto mode, no in-flight counts: results clear their
+    log entries in place): window ticks whose k_logscan tests the log against the died
+    bitmap through its one-bit-per-word summary.  Every output and the state equal the
+    oracle's; deaths happen inside window ticks."""
+    W = 160_000
+    st = synth.zipf_state(W=W, seed=8, dead_frac=0.0)
+    ticks = synth.stream_ticks(st, n_ticks=6, seed=9, tasks_per_tick=8192, results_per_tick=8192, dt=0.15)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    cap = len(st["log"]) + 16 * 8192
+    g = GpuBalancer(W, cap, max_events=E)
+    g.load(st)
+    o = Oracle(W, cap, purge_mode=2)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    n_orph = _large_stream(g, o, ticks, eager)
+    wt, fb = g.window_stats()
+    assert wt >= 3 and n_orph > 0, (wt, fb, n_orph)
+    g.close()

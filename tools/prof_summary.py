@@ -52,8 +52,16 @@ def main(d, tag):
     cfg = bench["config"]
     traffic = dict(tag=tag, workers=cfg["workers"], tasks_per_tick=cfg["tasks_per_tick"], n_gpus=bench["n_gpus"],
                    kernels=out, note="HBM-side bytes per launch = 2*FETCH_SIZE + WRITE_SIZE (KiB->B), "
-                                     "rocprofv3 --pmc passes of bench.py, profiles/%s_pmc.csv" % tag)
-    json.dump(traffic, open(os.path.join(prof, "traffic.json"), "w"), indent=1)
+                                     "rocprofv3 --pmc passes of bench.py, profiles/%s_pmc.csv; trace_avg_ns from "
+                                     "profiles/%s_kernel_stats.csv" % (tag, tag))
+    json.dump(traffic, open(os.path.join(prof, "%s_traffic.json" % tag), "w"), indent=1)
+    # profiles/traffic.json: the latest summary per configuration (bench.py looks its own up)
+    tp = os.path.join(prof, "traffic.json")
+    allt = json.load(open(tp)) if os.path.exists(tp) else {}
+    if "entries" not in allt:
+        allt = {"entries": {}}
+    allt["entries"]["%d,%d,%d" % (traffic["workers"], traffic["tasks_per_tick"], traffic["n_gpus"])] = traffic
+    json.dump(allt, open(tp, "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 
 

@@ -33,10 +33,8 @@ def main():
         return stream_main(args)
     st = synth.zipf_state(W=args.workers, seed=0)
     W, T = args.workers, args.tasks
-    env = os.environ.get("FAASBAL_SPLIT_SLOTS", "-1")
-    split = env == "1" or (env == "-1" and args.workers > (1 << 17))  # the library's auto rule
-    fsep = os.environ.get("FAASBAL_LOGSCAN", "-1") == "1" or (
-        os.environ.get("FAASBAL_LOGSCAN", "-1") == "-1" and args.workers > (1 << 17))
+    split = args.workers > (1 << 17)  # the library's auto rules (fb_set_path "split_slots" / "logscan")
+    fsep = args.workers > (1 << 17)
     g = GpuBalancer(W, 2 * len(st["log"]) + T + 16, max_events=1, lib_path=STAMPS_SO)
     g.load(st)
     nbw = -(-W // 256)
