@@ -1113,11 +1113,13 @@ int enqueue_tick(fb_ctx *c) {
     if (c->cm_pending) {
         // an idle tick's commit (evicted records, orphaned log entries) rides in k_scan when
         // k_scan purges the slots and reads no log entry itself
-        if (a.slots_in_scan && !a.slots_in_apply && (a.f_emit || a.f_sep) && !c->deque) {
+        // (per-tile orphan segments are cleared by k_emit2's log workgroups, tile by tile)
+        const bool seg_ok = !c->cm.oseg || (a.f_emit && c->cm.oseg_tiles <= nbf);
+        if (a.slots_in_scan && !a.slots_in_apply && (a.f_emit || a.f_sep) && !c->deque && seg_ok) {
             a.cm_fold = 1;
             a.cm_tiles = c->cm.oseg ? c->cm.oseg_tiles : 0;
-            a.cm_n_orph = c->cm.n_orph;
-            a.cm_blocks = std::max(1, c->cm.oseg ? (int)cdiv(c->cm.oseg_tiles, kWaves) : (int)cdiv(c->cm.n_orph, kBS));
+            a.cm_n_orph = c->cm.oseg ? 0 : c->cm.n_orph;
+            a.cm_blocks = c->cm.oseg ? 0 : std::max(1, (int)cdiv(c->cm.n_orph, kBS));
             c->cm_pending = false;
         } else if ((rc = flush_commit(c))) {
             return rc;

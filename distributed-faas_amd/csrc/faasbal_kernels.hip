@@ -1580,15 +1580,9 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     }
     if (a.cm_fold && bid >= (int)gridDim.x - a.cm_blocks) {
         // ---- the previous tick's orphaned log entries leave the log (its folded commit)
-        const int cb = bid - ((int)gridDim.x - a.cm_blocks);
-        if (a.cm_tiles > 0) {  // per-tile segments: a wave per tile
-            const int t = cb * kWaves + wave_id();
-            const uint32_t n = t < a.cm_tiles ? a.fcnt[t] : 0u;
-            for (uint32_t i = lane_id(); i < n; i += 64) a.log_slot[a.orphans[(int64_t)t * kFTile + i]] = -1;
-        } else {
-            const int64_t i = (int64_t)cb * kBS + threadIdx.x;
-            if (i < a.cm_n_orph) a.log_slot[a.orphans[i]] = -1;
-        }
+        // (a dense list; per-tile segments are cleared by k_emit2's log workgroup of each tile)
+        const int64_t i = (int64_t)(bid - ((int)gridDim.x - a.cm_blocks)) * kBS + threadIdx.x;
+        if (i < a.cm_n_orph) a.log_slot[a.orphans[i]] = -1;
         return;
     }
     if (bid >= a.nbq) {
@@ -2557,6 +2551,10 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
     const int64_t nlog = a.head_in;
     const int64_t tbase = (int64_t)t * kFTile;
     const int64_t last4 = nlog > 0 ? ((nlog - 1) & ~(int64_t)3) : 0;
+    // the previous tick's orphans of this tile (its commit, folded into this tick: an idle
+    // tick after an idle tick) leave the log here; their slots died then, so this tick
+    // flags none of them whichever value its loads below see
+    const uint32_t pc = (a.cm_fold && t < a.cm_tiles) ? a.fcnt[t] : 0u;
     int32_t v[2][4];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -2584,6 +2582,8 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
         }
     }
     lds_barrier();
+    // (read before the block scans' barriers; the segment is rewritten after them)
+    for (uint32_t i = tid; i < pc; i += kBS) a.log_slot[a.orphans[tbase + i]] = -1;
     int64_t o = tbase;  // this tile's segment; entry order within the tile: k, then tid, then j
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
