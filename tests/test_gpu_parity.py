@@ -674,3 +674,30 @@ def test_idle_ticks_commit_folded_into_scan(W, dead):
         carried = n + len(b["orphans"]) - len(b["assign"])
     _cmp_state(g, o, 6)
     g.close()
+
+
+@pytest.mark.parametrize("path", ["fused", "plan"])
+@pytest.mark.parametrize("L", [0, 1, 30, 31, 32, 33, 62])
+def test_fill_levels_around_table_widths(monkeypatch, path, L):
+    """Fill levels either side of the 32 / 64-row round tables (a table is chosen from the
+    largest free count, so L + 2 rows must fit), a partial round L, dead workers and their
+    orphans dispatched first, on the fused and the k_plan paths, against the oracle."""
+    if path == "plan":
+        monkeypatch.setitem(TEST_PATHS, "plan", 1)
+    W = 3000
+    rng = np.random.default_rng(100 + L)
+    free = rng.integers(L + 2, L + 40, W).astype(np.int32)  # every live worker has c > L + 1
+    hb = np.where(rng.random(W) < 0.05, 900.0, 999.0)        # 5 % expire at now = 1000
+    log = rng.integers(0, W, 4 * W).astype(np.int32)
+    st = dict(reg=np.ones(W, np.uint8), free=free, hb=hb, epoch=np.zeros(W, np.uint32),
+              queue=rng.permutation(W).astype(np.int32), log=log)
+    g, o = _pair(st, len(log) + W * (L + 2) + 16)
+    alive = int((hb > 990.0).sum())
+    dead_inflight = int(np.isin(log, np.nonzero(hb < 990.0)[0]).sum())
+    T = alive * L + alive // 3 - dead_inflight  # L full rounds, then a third of round L
+    args = (1000.0, 10.0, [], [], [], [], [], max(T, 0))
+    a, b = g.tick(*args), o.tick(*args)
+    if T > 0:
+        assert a["result"]["fill_level"] == L, a["result"]
+    _cmp_out(a, b, 0)
+    _cmp_state(g, o, 0)
