@@ -6,6 +6,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 T=${1:-r04}
 timeout -k 10 300 python -u bench.py > gpurun_out/${T}_bench.json 2> gpurun_out/${T}_bench.err || { tail -20 gpurun_out/${T}_bench.err; exit 3; }
 cat gpurun_out/${T}_bench.json
+timeout -k 10 180 python -u tools/stamps.py --reps 50 > gpurun_out/${T}_stamps.txt 2>&1 || { tail -20 gpurun_out/${T}_stamps.txt; exit 4; }
 bash tools_profile.sh ${T}_c2 > gpurun_out/${T}_prof_c2.log 2>&1 || { tail -20 gpurun_out/${T}_prof_c2.log; exit 5; }
 bash tools_profile.sh ${T}_c3 --workload cfg3 > gpurun_out/${T}_prof_c3.log 2>&1 || { tail -20 gpurun_out/${T}_prof_c3.log; exit 6; }
 timeout -k 10 300 python -u bench.py --workload cfg3 --no-cpu-baseline > gpurun_out/${T}_cfg3.json 2> gpurun_out/${T}_cfg3.err || { tail -20 gpurun_out/${T}_cfg3.err; exit 7; }

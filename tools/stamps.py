@@ -47,7 +47,7 @@ def main():
         g.wait()
         d = g.debug_read()[: 4 * G1 * 16].reshape(4 * G1, 16).astype(np.int64)
         acc.append(d.copy())
-    report(np.stack(acc), nbw, nbf, nbq, split, fsep)
+    report(np.stack(acc), nbw, nbf, nbq, split, fsep, femit=not split and not fsep)
 
 
 def stream_main(args):
@@ -84,8 +84,10 @@ def stream_main(args):
     report(np.stack(acc), nbw, nbf, nbq, False, True)
 
 
-def report(d, nbw, nbf, nbq, split, fsep):
-    """d: reps x rows x 16 stamps."""
+def report(d, nbw, nbf, nbq, split, fsep, femit=False):
+    """d: reps x rows x 16 stamps.  femit: fused one-GPU ticks (k_scan without log
+    blocks; k_emit2's log role one workgroup per tile, then the slot tiles four per
+    workgroup)."""
     G1 = nbw + nbf + nbq
     S = nbw  # k_scan rows start here
     E0 = G1 if split else G1 + nbw  # k_emit rows start here
@@ -106,6 +108,10 @@ def report(d, nbw, nbf, nbq, split, fsep):
         kernels = {"scan": (S, S + nbf + nbw + nbq), "emit": (E0, E0 + G1)}
         roles = {"scan.Q": (S, S + nbq), "scan.F": (S + nbq, S + nbq + nbf), "scan.W": (S + nbq + nbf, S + G1)}
     nbf4, nbw4 = -(-nbf // 4), -(-nbw // 4)  # k_emit2: one wave per compaction tile
+    if femit:
+        kernels["scan"] = (S, S + nbq + nbw)
+        roles = {"scan.Q": (S, S + nbq), "scan.W": (S + nbq, S + nbq + nbw)}
+        nbf4 = nbf  # one log workgroup per tile
     roles.update({"emit.Q": (E0, E0 + nbq), "emit.F": (E0 + nbq, E0 + nbq + nbf4),
                   "emit.W": (E0 + nbq + nbf4, E0 + nbq + nbf4 + nbw4)})
     starts = {}
