@@ -2555,6 +2555,9 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
     // tick after an idle tick) leave the log here; their slots died then, so this tick
     // flags none of them whichever value its loads below see
     const uint32_t pc = (a.cm_fold && t < a.cm_tiles) ? a.fcnt[t] : 0u;
+    // ... their first 256 log positions loaded with the tile (a tile's previous segment
+    // holds ~100 at configs[2]), so the clear below is a store, not a load round
+    const int64_t oq0 = (a.cm_fold && t < a.cm_tiles) ? a.orphans[tbase + tid] : 0;
     int32_t v[2][4];
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -2583,7 +2586,8 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
     }
     lds_barrier();
     // (read before the block scans' barriers; the segment is rewritten after them)
-    for (uint32_t i = tid; i < pc; i += kBS) a.log_slot[a.orphans[tbase + i]] = -1;
+    if ((uint32_t)tid < pc) a.log_slot[oq0] = -1;
+    for (uint32_t i = tid + kBS; i < pc; i += kBS) a.log_slot[a.orphans[tbase + i]] = -1;
     int64_t o = tbase;  // this tile's segment; entry order within the tile: k, then tid, then j
 #pragma unroll
     for (int k = 0; k < 2; ++k) {
@@ -2976,9 +2980,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     // thread per flag byte / slot, so they do not queue behind the queue role
     if (a.f_emit && bid >= cb0 && bid < cb0 + a.nbf) {  // f_emit: one log workgroup per tile
         extern __shared__ __attribute__((aligned(16))) unsigned long long dynbm[];
+        STAMP(a, SO, 0);
         emit_log_tile(a, bid - cb0, dynbm);
+        STAMP(a, SO, 15);
         return;
     }
+    STAMP(a, SO, 0);
     const bool frole = !a.f_emit && bid < cb0 + nbf4;
     const int t0 = 4 * (frole ? bid - cb0 : bid - cb0 - nbf4);
     const int t = t0 + w;

@@ -28,6 +28,8 @@ def main():
     ap.add_argument("--stream", action="store_true", help="committed configs[4] ticks with messages")
     ap.add_argument("--hb-frac", type=float, default=0.01)
     ap.add_argument("--dump", default="", help="stream: save the raw stamp rows (npz)")
+    ap.add_argument("--fold", action="store_true",
+                    help="the tick after a committed tick (its commit folded into k_scan / k_emit2)")
     args = ap.parse_args()
     if args.stream:
         return stream_main(args)
@@ -35,7 +37,7 @@ def main():
     W, T = args.workers, args.tasks
     split = args.workers > (1 << 17)  # the library's auto rules (fb_set_path "split_slots" / "logscan")
     fsep = args.workers > (1 << 17)
-    g = GpuBalancer(W, 2 * len(st["log"]) + T + 16, max_events=1, lib_path=STAMPS_SO)
+    g = GpuBalancer(W, 2 * len(st["log"]) + 2 * T + 65536, max_events=1, lib_path=STAMPS_SO)
     g.load(st)
     nbw = -(-W // 256)
     nbf = -(-len(st["log"]) // 2048)
@@ -43,6 +45,15 @@ def main():
     G1 = nbw + nbf + nbq
     acc = []
     for _ in range(args.reps):
+        if args.fold:
+            g.load(st)
+            g.launch(1000.0, 10.0, n_pending=T)
+            r0 = g.wait()
+            g.commit()  # deferred into the next launch
+            # the folded tick's grid: the committed queue and log
+            nbf = -(-int(r0["log_head"]) // 2048)
+            nbq = max(1, -(-int(r0["queue_len"]) // 256))
+            G1 = nbw + nbf + nbq
         g.launch(1000.0, 10.0, n_pending=T)
         g.wait()
         d = g.debug_read()[: 4 * G1 * 16].reshape(4 * G1, 16).astype(np.int64)
