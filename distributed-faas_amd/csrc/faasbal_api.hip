@@ -285,6 +285,11 @@ struct fb_ctx {
     int64_t *opre = nullptr, *oA = nullptr;
     uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
     int64_t xcap = 0;
+    // the exchange records' copy the next phase 1 writes (two, by exchange parity: a phase 2
+    // with block rows zeroes the other and flips it -- a collective step, so every rank
+    // agrees), and whether that copy is known zero (then an idle tick's phase 1 needs no memset)
+    int xpar = 0;
+    bool xz_ok = false;
     int phase = 0;                                    // 1: phase 1 enqueued; 2: phase 2 enqueued
     int shard_R = 0;                                  // > 0: round rows a relaunch asked for (FB_ERERUN)
     hipStream_t own_s = nullptr;                      // the context's own stream (fb_set_stream may borrow another)
@@ -467,19 +472,31 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
 
 // Exchange buffer of a sharded tick, summed by one uint8 all-reduce: every byte
 // has at most one nonzero contributor (the owner of the slot, event or position),
-// so the SUM is exact.  [0, c8) is zeroed before phase 1; c8 is written in full.
+// so the SUM is exact -- except the block rows, whose bytes are 4-bit digits that at
+// most kXRowsMaxWorld ranks add (<= 240).  [rec, c8) -- two copies of the per-rank
+// records (by launch parity), the event regions -- is zero before phase 1 (a memset, or
+// for an idle tick the previous phase 2's zeroing of this parity's records); c8 and the
+// rows are written in full.
 struct XLayout {
-    size_t rec, front, back, evs, c8, total;
+    size_t rec, front, back, evs, c8, rows, total;
 };
+// Exchanged block rows for a tick of this shape (0: phase 2 re-counts the c values):
+// <= 16 ranks, a table of <= kRFused rows, <= kXRowsMaxBlocks queue blocks
+inline size_t xrows_bytes(int world, int R, int64_t Qlog) {
+    const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
+    if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused || nbq > kXRowsMaxBlocks) return 0;
+    return (size_t)nbq * xr_row(R);
+}
 // xcw: bytes per exchanged c (1 while the round table has <= kRFused rows, else 2)
-XLayout xlayout(int world, int64_t E, int64_t Qlog, int xcw = 1) {
+XLayout xlayout(int world, int64_t E, int64_t Qlog, int xcw = 1, size_t rows = 0) {
     XLayout x;
     x.rec = 0;
-    x.front = (size_t)8 * kXRecWords * world;
+    x.front = (size_t)2 * 8 * kXRecWords * world;
     x.back = x.front + 4 * (size_t)E;
     x.evs = x.back + 4 * (size_t)E;
     x.c8 = (x.evs + (size_t)E + 1) & ~(size_t)1;  // 2-byte aligned for the wide form
-    x.total = (x.c8 + (size_t)xcw * (size_t)Qlog + 15) & ~(size_t)15;
+    x.rows = (x.c8 + (size_t)xcw * (size_t)Qlog + 15) & ~(size_t)15;
+    x.total = (x.rows + rows + 15) & ~(size_t)15;
     return x;
 }
 inline int xc_width(int R) { return R > kRFused ? 2 : 1; }
@@ -662,7 +679,8 @@ int enqueue_tick(fb_ctx *c) {
     int rc;
     if ((rc = ensure_table(c, R, nbq))) return rc;
     const int cur = c->cur, nxt = 1 - cur;
-    const XLayout xl = xlayout(c->world, E, Qlog, xc_width(R));
+    const size_t xrb = c->shard ? xrows_bytes(c->world, R, Qlog) : 0;
+    const XLayout xl = xlayout(c->world, E, Qlog, xc_width(R), xrb);
     int32_t *front = c->front_list, *back = c->back_list;
     uint8_t *evs = c->ev_status;
     if (c->shard) {
@@ -672,7 +690,8 @@ int enqueue_tick(fb_ctx *c) {
         front = (int32_t *)(c->xbuf + xl.front);
         back = (int32_t *)(c->xbuf + xl.back);
         evs = c->xbuf + xl.evs;
-        if (c->phase != 2) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
+        // (an idle tick whose records the last phase 2 zeroed has nothing else to clear)
+        if (c->phase != 2 && !(E == 0 && c->xz_ok)) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
     }
     TickArgs a{};
     a.W = W;
@@ -705,7 +724,7 @@ int enqueue_tick(fb_ctx *c) {
     // large tables for k_emit2: group rows too, scanned by k_plan2
     const bool gplan = !a.fused && a.segw && !c->shard;
     // sharded phase 2 with a round table of <= 128 rows: group rows instead of k_plan
-    const bool sgrp = c->shard && c->phase == 2 && R <= kRFused;
+    const bool sgrp = c->shard && c->phase == 2 && R <= kRFused && !xrb;
     if ((a.fused || gplan || sgrp) && !c->l_win) {  // (a window tick uses no group rows)
         // group rows: fused / sharded, about sqrt(nbq) groups of 2^gshift queue blocks (the
         // emit reads both); k_plan2, the smallest groups that make at most 64 rows (one
@@ -1013,7 +1032,14 @@ int enqueue_tick(fb_ctx *c) {
         a.lseq_out = c->lseq;
         a.xc8 = c->xbuf + xl.c8;
         a.xcw = xc_width(R);
-        a.xrec = (unsigned long long *)(c->xbuf + xl.rec);
+        // this tick's copy of the records; phase 2 with block rows zeroes the other
+        const size_t xrw = (size_t)c->world * kXRecWords;
+        a.xrec = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)c->xpar * xrw;
+        a.xrows = xrb ? c->xbuf + xl.rows : nullptr;
+        if (xrb && c->phase == 2) {
+            a.xz = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)(c->xpar ^ 1) * xrw;
+            a.xz_words = (int)xrw;
+        }
         a.ocnt = c->ocnt;
         a.osegcnt = c->osegcnt;
         a.opre = c->opre;
@@ -1097,6 +1123,17 @@ int enqueue_tick(fb_ctx *c) {
     }
     if (a.shard == 2) {
         if (R > kShardMaxR) return fail(c, FB_ERANGE, "sharded tick: round table of %d rows (limit %d)", R, kShardMaxR);
+        if (a.xrows) {
+            // exchanged block rows: k_emit_shard alone (it also zeroes the other records copy,
+            // which the next tick's phase 1 writes)
+            Timer t(c, "emit");
+            launch_emit_shard(a, t.st());
+            HIPCHK(c, hipGetLastError());
+            c->xpar ^= 1;
+            c->xz_ok = true;
+            return FB_OK;
+        }
+        c->xz_ok = false;  // the next phase 1 clears the records
         {
             Timer t(c, "scan2");
             launch_scan(a, t.st());
@@ -1639,7 +1676,10 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
     c->head = log_head;
     c->head_local = log_len;
     c->tick += 1;
-    c->maxc_hint = maxc;
+    // the first tick's round table from what every rank knows alike (the exchange layout
+    // depends on it): its events' values; a fill level beyond it relaunches wider
+    (void)maxc;
+    c->maxc_hint = 1;
     c->launched = c->waited = false;
     c->phase = 0;
     return FB_OK;
@@ -1684,6 +1724,8 @@ int fb_bind_exchange(fb_ctx *c, void *device_buffer, int64_t bytes) {
     HIPCHK(c, stream_wait(c));
     c->xbuf = (uint8_t *)device_buffer;
     c->xcap = bytes;
+    c->xpar = 0;
+    c->xz_ok = false;
     return FB_OK;
 }
 
@@ -1691,9 +1733,16 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
     if (!c || !bytes) return FB_EINVAL;
     const int64_t E = n_events < 0 ? c->E_cap : n_events;
     const int64_t Qn = n_events < 0 ? c->Wq_cap : (c->launched ? c->l_Qn : c->Qn);
-    // the maximum: room for the wide form; a launched tick: its own width
-    const int xcw = n_events < 0 ? 2 : xc_width(c->launched ? c->l_R : kRFused);
-    *bytes = (int64_t)xlayout(c->world, E, Qn + 2 * E, xcw).total;
+    // the maximum: room for the wide form or for the block rows of a <= kRFused-row table,
+    // whichever is larger; a launched tick: its own width and rows
+    const int64_t Qlog = Qn + 2 * E;
+    if (n_events < 0) {
+        *bytes = (int64_t)std::max(xlayout(c->world, E, Qlog, 2).total,
+                                   xlayout(c->world, E, Qlog, 1, xrows_bytes(c->world, kRFused, Qlog)).total);
+    } else {
+        const int R = c->launched ? c->l_R : kRFused;
+        *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xrows_bytes(c->world, R, Qlog)).total;
+    }
     return FB_OK;
 }
 

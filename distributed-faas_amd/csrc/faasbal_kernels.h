@@ -13,6 +13,24 @@ constexpr int kStagePar = 16384;   // host: event batches this large are staged 
 // 128-byte lines (device atomics on one line serialise, ~6 ns each)
 constexpr int kXRecLines = 8;
 constexpr int kXRecWords = kXRecLines * 16;  // u64 words per rank (1 KB)
+// Exchanged block rows (sharded ticks whose round table has <= kRFused rows and whose
+// LRU order spans <= kXRowsMaxBlocks queue blocks, <= kXRowsMaxWorld ranks): phase 1
+// writes, per queue block, its own positions' counts of c > r for r <= R as three
+// 4-bit digits, one byte each ([block][digit][xr_stride(R)] bytes); the SUM all-reduce
+// adds at most 16 digits of 15 per byte, so the rows arrive as every rank's counts and
+// phase 2 is one launch (no re-count of the exchanged c values, no group rows).
+constexpr int kXRowsMaxBlocks = 256;  // packed 16-bit column sums: 256 x 240 < 65536
+constexpr int kXRowsMaxWorld = 16;
+constexpr int kXRowDigits = 3;  // a block count is <= 256 < 16^3
+__host__ __device__ constexpr int xr_stride(int R) { return (R + 1 + 3) & ~3; }
+// a block's row: the three digit rows, padded to 16 bytes (phase 2 reads it in int4s)
+__host__ __device__ constexpr int xr_row(int R) { return (kXRowDigits * xr_stride(R) + 15) & ~15; }
+constexpr int kXRowMaxBytes = (kXRowDigits * ((128 + 1 + 3) & ~3) + 15) & ~15;
+// phase 2: the parts (lanes) per 16-byte load column of the digit rows, a power of two
+// with every column's parts in one workgroup; own rows (R / 4 columns) use kBS / (R / 4)
+__host__ __device__ constexpr int xr_parts(int R) {
+    return (xr_row(R) >> 4) * 32 <= kBS ? 32 : ((xr_row(R) >> 4) * 16 <= kBS ? 16 : 8);
+}
 constexpr int kFItems = 8;         // log entries per thread in log-role blocks
 constexpr int kFTile = kBS * kFItems;
 #ifndef FAASBAL_RS_ITEMS
@@ -397,6 +415,10 @@ struct TickArgs {
     uint8_t *xc8;                  // exchange: c per LRU position (single contributor per byte), xcw bytes each:
     int xcw;                       // 1: min(c, 255) while the round table has <= 128 rows, 2: min(c, 65535)
     unsigned long long *xrec;      // exchange: per rank kXRecLines orphan-count partials, one per 128-B line
+                                   // (two copies by launch parity: phase 2 zeroes the next tick's)
+    uint8_t *xrows;                // exchanged block rows (kXRowsMaxBlocks; null: phase 2 re-counts the c values)
+    unsigned long long *xz;        // phase 2: the other launch parity's exchange records, zeroed for the next tick
+    int xz_words;
     uint32_t *ocnt;                // [block][round] counts of this rank's positions
     uint32_t *osegcnt;             // [64-position segment][round] counts of this rank's positions
     int64_t *opre, *oA;

@@ -1705,6 +1705,49 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         // them (exact below the round table: its rows stay below the clamp).
         // Per-wave atomics on one exchange word cost ~10 ns each, serialised --
         // 14 K of them per tick at 8 ranks.
+        if (a.xrows) {
+            // ... and, with exchanged block rows, this block's counts of c > r (own
+            // positions; r <= R): per wave from a histogram of min(c, R + 1) in LDS
+            // (k_scan's scheme), summed over the waves; the row as 4-bit digits into the
+            // exchange (the SUM over ranks: every rank's counts), the own counts as words
+            __shared__ uint32_t xh[kWaves][kRFused + 2];
+            const int R = a.R, lane = lane_id(), w = wave_id();
+            uint32_t *h = xh[w];
+            for (int i = lane; i <= R + 1; i += 64) h[i] = 0;
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            atomicAdd(&h[c < R + 1 ? c : R + 1], 1u);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            __builtin_amdgcn_wave_barrier();
+            uint32_t carry = 0;
+#pragma unroll
+            for (int k = 0; k < 3; ++k) {
+                const int r = 64 * k + lane;
+                const uint32_t P = carry + wave_incl_scan_u32(r <= R ? h[r] : 0u);
+                if (r < kBS) wc[w][r] = r <= R ? 64u - P : 0u;
+                carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+            }
+            // max c (the byte's clamp, as exchanged) into word 1 of one of the rank's record
+            // lines (8 lines: same-line device atomics serialise)
+            const uint32_t wmx = wave_max_u32((uint32_t)(c < 255 ? c : 255));
+            if (lane == 0) m4[w] = (int32_t)wmx;
+            lds_barrier();
+            const int xs = xr_stride(R), t = threadIdx.x;
+            if (t == 0) {
+                const int32_t bm = max(max(m4[0], m4[1]), max(m4[2], m4[3]));
+                if (bm > 0)
+                    atomicMax(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16 + 1], (unsigned long long)bm);
+            }
+            uint8_t *const row = a.xrows + (size_t)b * xr_row(R);
+            if (t < xs) {
+                const uint32_t n = wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];  // 0 past R
+#pragma unroll
+                for (int d = 0; d < kXRowDigits; ++d) row[d * xs + t] = (uint8_t)((n >> (4 * d)) & 15u);
+                if (t < R) a.ocnt[(size_t)b * R + t] = n;
+            } else if (t < xs + xr_row(R) - kXRowDigits * xs) {
+                row[kXRowDigits * xs + (t - xs)] = 0;  // the row's padding
+            }
+        }
         STAMP(a, SO, 15);
         return;
     }
@@ -3302,6 +3345,19 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
 
 // ------------------------------------------------------------ k_emit_shard
 __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid);
+// Sum over aligned groups of G adjacent lanes (G = 8, 16, 32), every lane of a group left
+// with its total: DPP quad permutes (lanes ^1, ^2), then the 8- and 16-lane mirrors (each
+// pairs a lane with the other half of its group once the halves are uniform), then the
+// 32-lane swizzle
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    if (G >= 16) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    if (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);  // lane ^ 16 within 32
+    return x;
+}
 constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // Phase 2 of a sharded tick.  Every rank computes the global water-filling from
 // the exchanged counts (identical on all ranks), writes the whole next LRU queue,
@@ -3316,12 +3372,20 @@ constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // from the group rows k_scan's phase-2 blocks added (all / own counts, max c, capacity),
 // plus the earlier blocks of its own group; the orphan totals from the exchange records
 // and this rank's tile counts.
-template <bool GRP>
+// XR (with GRP): no phase-2 k_scan either -- every block's counts arrived in the exchange
+// as digit rows (phase 1, a.xrows), this rank's in its own rows (ocnt); each block sums the
+// rows of all blocks (totals) and of the blocks before it (prefix), and counts its waves'
+// rounds itself; max c and the capacity follow from the totals.
+template <bool GRP, bool XR>
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     prefetch_args(a);
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
-    if (GRP) {  // the other parity's group rows, for the next launch's k_scan atomics
+    const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows (stamps builds)
+    STAMP(a, SO, 0);
+    if (XR) {  // the other parity's exchange records, for the next tick's phase 1
+        for (int i = bid * kBS + (int)threadIdx.x; i < a.xz_words; i += (int)gridDim.x * kBS) a.xz[i] = 0ull;
+    } else if (GRP) {  // the other parity's group rows, for the next launch's k_scan atomics
         for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
     }
     if (bid < a.nbq) {
@@ -3336,7 +3400,168 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         int64_t Av[kRCh], oAv[kRCh], pv[kRCh], opv[kRCh];
         int64_t O, cap;
         int maxc;
-        if (GRP) {
+        uint32_t segc[kRCh] = {0, 0, 0}, osegc[kRCh] = {0, 0, 0};
+        if (XR) {
+            // ---- the block rows of every block, summed per column: tot over all blocks,
+            // pre over the blocks before b.  All positions: the exchanged digit rows (xr_row
+            // bytes per block); this rank's: its own count rows (R words).  Thread (load
+            // column q, part j) loads the 16-byte column q of rows j, j + Pp, ... (parts the
+            // fast index, Pp a power of two), 8 rows per round, both row kinds in flight
+            // together; the Pp parts of a column are adjacent lanes and meet by shuffles.
+            __shared__ uint32_t xcol[2][kXRowMaxBytes];  // per digit-row byte: tot / pre over the blocks
+            __shared__ uint32_t ocol[2][kRFused];        // per own column: tot / pre
+            __shared__ uint32_t swc[kWaves][kRFused + 1], sowc[kWaves][kRFused + 1];
+            __shared__ uint32_t sred[kWaves][3];
+            const int t = threadIdx.x;
+            // every rank's orphans and max c (their records; world * 8 <= kBS lines), issued
+            // first and consumed after the rows' loads
+            const int gx = t < a.world * kXRecLines ? t : 0;
+            const unsigned long long xo = a.xrec[(size_t)gx * 16], xm = a.xrec[(size_t)gx * 16 + 1];
+            uint32_t orf = 0, mx = 0;
+            const int xs = xr_stride(R), nq16 = xr_row(R) >> 4, Pp = xr_parts(R);
+            const int nq = R >> 2, Pp2 = kBS / nq;
+            const int q = t / Pp, j = t % Pp, q2 = t / Pp2, j2 = t % Pp2;
+            // packed: bytes two to a word (16-bit halves; <= kXRowsMaxBlocks x 240 each)
+            uint32_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+            uint32_t ot[4] = {0, 0, 0, 0}, op[4] = {0, 0, 0, 0};
+            {
+                const uint4 *src = reinterpret_cast<const uint4 *>(a.xrows) + q;
+                const uint4 *ow = reinterpret_cast<const uint4 *>(a.ocnt) + q2;
+                const bool xon = q < nq16;
+                for (int r0 = 0; r0 < a.nbq; r0 += 8 * Pp) {  // (rounds of 8 rows per thread)
+                    uint4 v[8], vo[8];
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int bb = r0 + j + k * Pp, b2 = (r0 / Pp) * Pp2 + j2 + k * Pp2;
+                        v[k] = (xon && bb < a.nbq) ? src[(size_t)bb * nq16] : make_uint4(0, 0, 0, 0);
+                        vo[k] = b2 < a.nbq ? ow[(size_t)b2 * nq] : make_uint4(0, 0, 0, 0);
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const bool in = r0 + j + k * Pp < b;
+                        const uint32_t w4[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            const uint32_t e = w4[u] & 0x00ff00ffu, o = (w4[u] >> 8) & 0x00ff00ffu;
+                            tp[2 * u] += e;
+                            tp[2 * u + 1] += o;
+                            pp[2 * u] += in ? e : 0u;
+                            pp[2 * u + 1] += in ? o : 0u;
+                        }
+                        const bool in2 = (r0 / Pp) * Pp2 + j2 + k * Pp2 < b;
+                        const uint32_t o4[4] = {vo[k].x, vo[k].y, vo[k].z, vo[k].w};
+#pragma unroll
+                        for (int u = 0; u < 4; ++u) {
+                            ot[u] += o4[u];
+                            op[u] += in2 ? o4[u] : 0u;
+                        }
+                    }
+                }
+            }
+            STAMPW(a, SO, 1);
+            // this wave's rounds (all / own lanes) from histograms of min(c, R): the in-block
+            // bases of the later waves
+            {
+                const int cw_ = pos < a.Qlog ? cq : 0;
+                const int ocw = (cw_ > 0 && sq >= 0 && own_slot(a, sq) >= 0) ? cw_ : 0;
+                uint32_t *ha = swc[w], *ho = sowc[w];
+                for (int i = lane; i <= R; i += 64) {
+                    ha[i] = 0;
+                    ho[i] = 0;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                atomicAdd(&ha[cw_ < R ? cw_ : R], 1u);
+                atomicAdd(&ho[ocw < R ? ocw : R], 1u);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                uint32_t ca = 0, co = 0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {  // count(c > r) = 64 - #(lanes with min(c, R) <= r)
+                    const int r = 64 * k + lane;
+                    const uint32_t hv = r < R ? ha[r] : 0u, hw = r < R ? ho[r] : 0u;
+                    const uint32_t Pa = ca + wave_incl_scan_u32(hv), Po = co + wave_incl_scan_u32(hw);
+                    ca = (uint32_t)__builtin_amdgcn_readlane((int)Pa, 63);
+                    co = (uint32_t)__builtin_amdgcn_readlane((int)Po, 63);
+                    __builtin_amdgcn_wave_barrier();
+                    if (r < R) {
+                        ha[r] = 64u - Pa;
+                        ho[r] = 64u - Po;
+                    }
+                }
+            }
+            // the parts of each column: adjacent lanes (Pp = Pp2, 8 / 16 / 32), DPP sums
+            auto gsum = [&](auto g) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    tp[u] = group_sum<decltype(g)::value>(tp[u]);
+                    pp[u] = group_sum<decltype(g)::value>(pp[u]);
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    ot[u] = group_sum<decltype(g)::value>(ot[u]);
+                    op[u] = group_sum<decltype(g)::value>(op[u]);
+                }
+            };
+            if (Pp == 32) gsum(std::integral_constant<int, 32>{});
+            else if (Pp == 16) gsum(std::integral_constant<int, 16>{});
+            else gsum(std::integral_constant<int, 8>{});
+            if (j == 0 && q < nq16) {
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    // packed word u: int4 word u / 2, even (u even) / odd bytes; halves 2 bytes apart
+                    const int by = q * 16 + (u >> 1) * 4 + (u & 1);
+                    xcol[0][by] = tp[u] & 0xffffu;
+                    xcol[0][by + 2] = tp[u] >> 16;
+                    xcol[1][by] = pp[u] & 0xffffu;
+                    xcol[1][by + 2] = pp[u] >> 16;
+                }
+            }
+            if (j2 == 0) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    ocol[0][q2 * 4 + u] = ot[u];
+                    ocol[1][q2 * 4 + u] = op[u];
+                }
+            }
+            orf = t < a.world * kXRecLines ? (uint32_t)xo : 0u;
+            mx = t < a.world * kXRecLines ? (uint32_t)xm : 0u;
+            orf = wave_sum_u32(orf);
+            mx = wave_max_u32(mx);
+            if (lane == 0) {
+                sred[w][1] = orf;
+                sred[w][2] = mx;
+            }
+            __syncthreads();
+            STAMP(a, SO, 4);
+            // the capacity sum_r<R A(r) = sum of c when max c <= R
+            uint32_t cp = t < R ? xcol[0][t] + (xcol[0][xs + t] << 4) + (xcol[0][2 * xs + t] << 8) : 0u;
+            cp = wave_sum_u32(cp);
+            if (lane == 0) sred[w][0] = cp;
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k) {
+                const int rr = min(64 * k + lane, R - 1);
+                Av[k] = xcol[0][rr] + (xcol[0][xs + rr] << 4) + (xcol[0][2 * xs + rr] << 8);
+                pv[k] = xcol[1][rr] + (xcol[1][xs + rr] << 4) + (xcol[1][2 * xs + rr] << 8);
+                oAv[k] = ocol[0][rr];
+                opv[k] = ocol[1][rr];
+                uint32_t sc = 0, osc = 0;
+#pragma unroll
+                for (int qq = 0; qq < kWaves - 1; ++qq) {
+                    const bool in = qq < w && 64 * k + lane < R;
+                    sc += in ? swc[qq][rr] : 0u;
+                    osc += in ? sowc[qq][rr] : 0u;
+                }
+                segc[k] = sc;
+                osegc[k] = osc;
+            }
+            __syncthreads();
+            // max c (clamped to the byte) from every rank's records
+            maxc = (int)max(max(sred[0][2], sred[1][2]), max(sred[2][2], sred[3][2]));
+            cap = (int64_t)sred[0][0] + sred[1][0] + sred[2][0] + sred[3][0];
+            O = (int64_t)sred[0][1] + sred[1][1] + sred[2][1] + sred[3][1];
+            STAMP(a, SO, 5);
+        } else if (GRP) {
             // 2R columns (round r of all positions, then of this rank's), tpc consecutive
             // threads per column: each column's total over the group rows and this block's
             // prefix (earlier groups + earlier blocks of its group), every tpc-th row per thread
@@ -3410,8 +3635,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             cap = a.P->cap_total;
             maxc = a.P->maxc;
         }
-        uint32_t segc[kRCh] = {0, 0, 0}, osegc[kRCh] = {0, 0, 0};
-        {
+        if (!XR) {
             uint32_t sv[kRCh][kWaves - 1], osv[kRCh][kWaves - 1];
 #pragma unroll
             for (int k = 0; k < kRCh; ++k)
@@ -3501,6 +3725,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 a.hout->n_local = oSL;  // every worker saturated: all own capacity used
             }
         }
+        STAMP(a, SO, 6);
         if (status) return;
         const int c = pos < a.Qlog ? cq : 0;
         const int s = sq;
@@ -3573,6 +3798,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 if (own) a.free_out[ls].y = 1;
             }
         }
+        STAMP(a, SO, 15);
         return;
     }
     shard_compact(a, bid);
@@ -3589,7 +3815,7 @@ __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid) {
     // the tile's offset: k_plan's scan of the tile counts, or (no k_plan: group rows) the
     // wave's own sum of the earlier tiles' counts
     auto tile_pre = [&](const uint32_t *cnt, const int64_t *pre) -> int64_t {
-        if (!a.grp_on) return pre[t];
+        if (!a.grp_on && !a.xrows) return pre[t];
         uint32_t v = 0;
         for (int i = lane; i < t; i += 64) v += cnt[i];
         return (int64_t)wave_sum_u32(v);
@@ -3969,7 +4195,8 @@ void launch_scan(const TickArgs &a, Stream st) {
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
     const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
     hipExtLaunchKernelGGL(k_logscan, dim3(grid), dim3(kLsBS), lds, st.s, st.e0, st.e1, 0, a);
-}void launch_plan(const TickArgs &a, Stream st) {
+}
+void launch_plan(const TickArgs &a, Stream st) {
     if (a.grp_on)
         hipExtLaunchKernelGGL(k_plan2, dim3(a.ngrp + 2), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
     else
@@ -4006,10 +4233,12 @@ void launch_emit_shard(const TickArgs &a, Stream st) {
         return;
     }
     const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
-    if (a.grp_on)
-        hipExtLaunchKernelGGL(k_emit_shard<true>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    if (a.xrows)
+        hipExtLaunchKernelGGL(k_emit_shard<true, true>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    else if (a.grp_on)
+        hipExtLaunchKernelGGL(k_emit_shard<true, false>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
     else
-        hipExtLaunchKernelGGL(k_emit_shard<false>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+        hipExtLaunchKernelGGL(k_emit_shard<false, false>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_evict_gather(int32_t *dst, const uint8_t *st, const uint32_t *wcnt, int64_t *wpre, int W, Stream s) {
     const int nt = cdiv(W, kBS);
