@@ -2651,6 +2651,20 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
     if (tid == 0) a.fcnt[t] = (uint32_t)(o - tbase);
 }
 
+// Sum over aligned groups of G adjacent lanes (G = 2 .. 32), every lane of a group left
+// with its total: DPP quad permutes (lanes ^1, ^2), then the 8- and 16-lane mirrors (each
+// pairs a lane with the other half of its group once the halves are uniform), then the
+// 32-lane swizzle
+template <int G>
+__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+    if (G >= 4) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+    if (G >= 8) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+    if (G >= 16) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
+    if (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);  // lane ^ 16 within 32
+    return x;
+}
+
 // XCD-aware order of the queue blocks: workgroups are dealt round-robin over the 8
 // XCDs (placement is a speed matter only), so logical block L = (i mod 8) * n/8 + i / 8
 // puts consecutive LRU segments on one XCD.  Each round's task range of block L ends
@@ -2779,8 +2793,9 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 totv[k] = tot_f[rr];
             }
         } else {
-            // thread t: round r = t mod R, part p = t / R of the rows
-            const int P = kBS / R, r = (int)threadIdx.x & (R - 1), p = (int)threadIdx.x / R;
+            // thread t: round r = t / P, part p = t mod P of the rows (a round's parts in
+            // adjacent lanes: summed by DPP, no LDS pass over them)
+            const int P = kBS / R, r = (int)threadIdx.x / P, p = (int)threadIdx.x & (P - 1);
             const int g = b >> a.gshift, gsz = 1 << a.gshift, ng = a.ngrp;
             const int gs = a.gstride;
             uint32_t pre = 0, tot = 0;
@@ -2812,8 +2827,20 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // (ngrp <= 64: wave 0 holds them)
             const int gi = min((int)threadIdx.x, ng - 1) * gs + R;
             const uint32_t mg = a.grp[gi], og = a.grp[gi + 1], eg = a.grp[gi + 2];
-            gpre[threadIdx.x] = pre;
-            gtot[threadIdx.x] = tot;
+            if (P == 8) {
+                pre = group_sum<8>(pre);
+                tot = group_sum<8>(tot);
+            } else if (P == 4) {
+                pre = group_sum<4>(pre);
+                tot = group_sum<4>(tot);
+            } else {
+                pre = group_sum<2>(pre);
+                tot = group_sum<2>(tot);
+            }
+            if (p == 0) {
+                gpre[r] = pre;
+                gtot[r] = tot;
+            }
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
 #pragma unroll
@@ -2840,18 +2867,12 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             O = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
             nev = (int64_t)red[0][1] + red[1][1] + red[2][1] + red[3][1];
             maxc = (int)max(max(red[0][3], red[1][3]), max(red[2][3], red[3][3]));
-            // this lane's rounds: the sum of the P parts
+            // this lane's rounds
 #pragma unroll
             for (int k = 0; k < NCH; ++k) {
                 const int rr = 64 * k + lane;
-                uint32_t sp = 0, st_ = 0;
-                if (rr < R)
-                    for (int q = 0; q < P; ++q) {
-                        sp += gpre[q * R + rr];
-                        st_ += gtot[q * R + rr];
-                    }
-                prev[k] = sp;
-                totv[k] = st_;
+                prev[k] = rr < R ? gpre[rr] : 0u;
+                totv[k] = rr < R ? gtot[rr] : 0u;
             }
         }
         STAMP(a, SO, 1);
@@ -3345,19 +3366,6 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
 
 // ------------------------------------------------------------ k_emit_shard
 __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid);
-// Sum over aligned groups of G adjacent lanes (G = 8, 16, 32), every lane of a group left
-// with its total: DPP quad permutes (lanes ^1, ^2), then the 8- and 16-lane mirrors (each
-// pairs a lane with the other half of its group once the halves are uniform), then the
-// 32-lane swizzle
-template <int G>
-__device__ __forceinline__ uint32_t group_sum(uint32_t x) {
-    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
-    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
-    x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-    if (G >= 16) x += (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false);  // row_mirror
-    if (G >= 32) x += (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x401F);  // lane ^ 16 within 32
-    return x;
-}
 constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // Phase 2 of a sharded tick.  Every rank computes the global water-filling from
 // the exchanged counts (identical on all ranks), writes the whole next LRU queue,
