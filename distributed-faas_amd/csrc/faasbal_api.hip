@@ -282,6 +282,7 @@ struct fb_ctx {
     int64_t head_local = 0, l_head_local = 0;
     uint32_t *lseq = nullptr;                         // global sequence of each local log entry
     uint32_t *ocnt = nullptr, *osegcnt = nullptr;
+    uint32_t *xg_acc = nullptr, *xg_tk = nullptr, *ogrp = nullptr;  // exchanged group rows (phase 1 -> 2)
     int64_t *opre = nullptr, *oA = nullptr;
     uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
     int64_t xcap = 0;
@@ -478,7 +479,7 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
 // for an idle tick the previous phase 2's zeroing of this parity's records); c8 and the
 // rows are written in full.
 struct XLayout {
-    size_t rec, front, back, evs, c8, rows, total;
+    size_t rec, front, back, evs, c8, rows, grows, total;
 };
 // Exchanged block rows for a tick of this shape (0: phase 2 re-counts the c values):
 // <= 16 ranks, a table of <= kRFused rows, <= kXRowsMaxBlocks queue blocks
@@ -487,8 +488,14 @@ inline size_t xrows_bytes(int world, int R, int64_t Qlog) {
     if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused || nbq > kXRowsMaxBlocks) return 0;
     return (size_t)nbq * xr_row(R);
 }
+// ... and the group rows (R = kXGroupR only)
+inline size_t xgrows_bytes(int world, int R, int64_t Qlog) {
+    if (R != kXGroupR || !xrows_bytes(world, R, Qlog)) return 0;
+    const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
+    return (size_t)cdiv(nbq, kXGroupBlocks) * xg_row(R);
+}
 // xcw: bytes per exchanged c (1 while the round table has <= kRFused rows, else 2)
-XLayout xlayout(int world, int64_t E, int64_t Qlog, int xcw = 1, size_t rows = 0) {
+XLayout xlayout(int world, int64_t E, int64_t Qlog, int xcw = 1, size_t rows = 0, size_t grows = 0) {
     XLayout x;
     x.rec = 0;
     x.front = (size_t)2 * 8 * kXRecWords * world;
@@ -496,7 +503,8 @@ XLayout xlayout(int world, int64_t E, int64_t Qlog, int xcw = 1, size_t rows = 0
     x.evs = x.back + 4 * (size_t)E;
     x.c8 = (x.evs + (size_t)E + 1) & ~(size_t)1;  // 2-byte aligned for the wide form
     x.rows = (x.c8 + (size_t)xcw * (size_t)Qlog + 15) & ~(size_t)15;
-    x.total = (x.rows + rows + 15) & ~(size_t)15;
+    x.grows = (x.rows + rows + 15) & ~(size_t)15;
+    x.total = (x.grows + grows + 15) & ~(size_t)15;
     return x;
 }
 inline int xc_width(int R) { return R > kRFused ? 2 : 1; }
@@ -680,7 +688,8 @@ int enqueue_tick(fb_ctx *c) {
     if ((rc = ensure_table(c, R, nbq))) return rc;
     const int cur = c->cur, nxt = 1 - cur;
     const size_t xrb = c->shard ? xrows_bytes(c->world, R, Qlog) : 0;
-    const XLayout xl = xlayout(c->world, E, Qlog, xc_width(R), xrb);
+    const size_t xgb = c->shard ? xgrows_bytes(c->world, R, Qlog) : 0;
+    const XLayout xl = xlayout(c->world, E, Qlog, xc_width(R), xrb, xgb);
     int32_t *front = c->front_list, *back = c->back_list;
     uint8_t *evs = c->ev_status;
     if (c->shard) {
@@ -1036,6 +1045,10 @@ int enqueue_tick(fb_ctx *c) {
         const size_t xrw = (size_t)c->world * kXRecWords;
         a.xrec = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)c->xpar * xrw;
         a.xrows = xrb ? c->xbuf + xl.rows : nullptr;
+        a.xgrows = xgb ? c->xbuf + xl.grows : nullptr;
+        a.xg_acc = c->xg_acc;
+        a.xg_tk = c->xg_tk;
+        a.ogrp = c->ogrp;
         if (xrb && c->phase == 2) {
             a.xz = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)(c->xpar ^ 1) * xrw;
             a.xz_words = (int)xrw;
@@ -1345,6 +1358,12 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->osegcnt, 4 * tab);
         ap.add(&c->opre, tab);
         ap.add(&c->oA, 128);
+        // exchanged group rows: per group the running sums and ticket (zero between ticks:
+        // the arena is zeroed, each group's last block resets them) and this rank's row
+        const size_t ng = (size_t)kXRowsMaxBlocks / kXGroupBlocks;
+        ap.add(&c->xg_acc, ng * kXgAccStride);
+        ap.add(&c->xg_tk, ng);
+        ap.add(&c->ogrp, ng * kXGroupR);
     }
     int rc = arena_commit(c, ap);
     if (!rc && hipMemset(c->bad_min, 0x7f, 4) != hipSuccess) rc = fail(c, FB_EHIP, "hipMemset(bad_min) failed");
@@ -1741,7 +1760,8 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
                                    xlayout(c->world, E, Qlog, 1, xrows_bytes(c->world, kRFused, Qlog)).total);
     } else {
         const int R = c->launched ? c->l_R : kRFused;
-        *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xrows_bytes(c->world, R, Qlog)).total;
+        *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xrows_bytes(c->world, R, Qlog),
+                                  xgrows_bytes(c->world, R, Qlog)).total;
     }
     return FB_OK;
 }

@@ -26,6 +26,15 @@ __host__ __device__ constexpr int xr_stride(int R) { return (R + 1 + 3) & ~3; }
 // a block's row: the three digit rows, padded to 16 bytes (phase 2 reads it in int4s)
 __host__ __device__ constexpr int xr_row(int R) { return (kXRowDigits * xr_stride(R) + 15) & ~15; }
 constexpr int kXRowMaxBytes = (kXRowDigits * ((128 + 1 + 3) & ~3) + 15) & ~15;
+// ... and at R = 32 (the configs[2] shapes), per group of 16 queue blocks too: the group's
+// last phase-1 block (a ticket per group) writes the group's sums as a 4-digit row (a group
+// count is <= 16 x 256 < 16^4) and this rank's own group row, so a phase-2 block reads the
+// <= 16 group rows and the rows of the earlier blocks of its group (16 lanes per load column)
+constexpr int kXGroupBlocks = 16;
+constexpr int kXGroupDigits = 4;
+constexpr int kXGroupR = 32;
+__host__ __device__ constexpr int xg_row(int R) { return (kXGroupDigits * xr_stride(R) + 15) & ~15; }
+constexpr int kXgAccStride = 36;  // words per group accumulator row (R + 1 = 33 columns)
 // phase 2: the parts (lanes) per 16-byte load column of the digit rows, a power of two
 // with every column's parts in one workgroup; own rows (R / 4 columns) use kBS / (R / 4)
 __host__ __device__ constexpr int xr_parts(int R) {
@@ -417,6 +426,9 @@ struct TickArgs {
     unsigned long long *xrec;      // exchange: per rank kXRecLines orphan-count partials, one per 128-B line
                                    // (two copies by launch parity: phase 2 zeroes the next tick's)
     uint8_t *xrows;                // exchanged block rows (kXRowsMaxBlocks; null: phase 2 re-counts the c values)
+    uint8_t *xgrows;               // exchanged group rows (R = kXGroupR; null: phase 2 sums the block rows)
+    uint32_t *xg_acc, *xg_tk;      // phase 1: per group the running sums and the ticket (zero between ticks)
+    uint32_t *ogrp;                // phase 1 -> 2: this rank's group rows [group][R]
     unsigned long long *xz;        // phase 2: the other launch parity's exchange records, zeroed for the next tick
     int xz_words;
     uint32_t *ocnt;                // [block][round] counts of this rank's positions

@@ -1739,13 +1739,42 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                     atomicMax(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16 + 1], (unsigned long long)bm);
             }
             uint8_t *const row = a.xrows + (size_t)b * xr_row(R);
+            const uint32_t n = t < xs ? wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t] : 0u;  // 0 past R
             if (t < xs) {
-                const uint32_t n = wc[0][t] + wc[1][t] + wc[2][t] + wc[3][t];  // 0 past R
 #pragma unroll
                 for (int d = 0; d < kXRowDigits; ++d) row[d * xs + t] = (uint8_t)((n >> (4 * d)) & 15u);
                 if (t < R) a.ocnt[(size_t)b * R + t] = n;
             } else if (t < xs + xr_row(R) - kXRowDigits * xs) {
                 row[kXRowDigits * xs + (t - xs)] = 0;  // the row's padding
+            }
+            if (a.xgrows) {
+                // the group's sums: memory-side adds, then a ticket; the group's last block
+                // takes the sums (resetting them for the next tick) and writes the group's
+                // digit row into the exchange and this rank's group row
+                __shared__ int xlast;
+                const int g = b / kXGroupBlocks;
+                const int nbg = min(kXGroupBlocks, a.nbq - g * kXGroupBlocks);
+                // (no fence: the adds are device-scope atomics, performed at the coherence
+                // point before each wave's vmcnt wait; the ticket comes after every wave's wait,
+                // and the last block reads the sums with atomics at that same point)
+                uint32_t *acc = a.xg_acc + (size_t)g * kXgAccStride;
+                if (t <= R && n) atomicAdd(&acc[t], n);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+                if (t == 0) xlast = atomicAdd(&a.xg_tk[g], 1u) == (uint32_t)(nbg - 1) ? 1 : 0;
+                __syncthreads();
+                if (xlast) {
+                    uint8_t *const gr = a.xgrows + (size_t)g * xg_row(R);
+                    if (t < xs) {
+                        const uint32_t v = t <= R ? atomicExch(&acc[t], 0u) : 0u;
+#pragma unroll
+                        for (int d = 0; d < kXGroupDigits; ++d) gr[d * xs + t] = (uint8_t)((v >> (4 * d)) & 15u);
+                        if (t < R) a.ogrp[(size_t)g * R + t] = v;
+                    } else if (t < xs + xg_row(R) - kXGroupDigits * xs) {
+                        gr[kXGroupDigits * xs + (t - xs)] = 0;
+                    }
+                    if (t == 0) a.xg_tk[g] = 0u;
+                }
             }
         }
         STAMP(a, SO, 15);
@@ -3429,10 +3458,67 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             const int xs = xr_stride(R), nq16 = xr_row(R) >> 4, Pp = xr_parts(R);
             const int nq = R >> 2, Pp2 = kBS / nq;
             const int q = t / Pp, j = t % Pp, q2 = t / Pp2, j2 = t % Pp2;
+            const bool xg = a.xgrows != nullptr;  // group rows (R = kXGroupR)
+            __shared__ uint32_t gsum[3][kXGroupDigits * 36], osum[3][kXGroupR];  // group tot / pre, block pre
+            if (xg) {
+                // ---- lanes 16 i .. 16 i + 15: one 16-byte column of the <= 16 group rows or of
+                // the rows of the blocks of b's group before b (lane & 15 = row); pass A the
+                // digit rows (9 group + 7 block columns), pass B this rank's rows (8 + 8)
+                const int g0 = b / kXGroupBlocks, ng = (a.nbq + kXGroupBlocks - 1) / kXGroupBlocks;
+                const int ri = t & 15;
+                const bool ga = t < 144, gb = t < 128;
+                const int ca = ga ? t >> 4 : (t - 144) >> 4, cb = gb ? t >> 4 : (t - 128) >> 4;
+                const int blk = g0 * kXGroupBlocks + ri;
+                const bool va = ga ? ri < ng : blk < b, vb = gb ? ri < ng : blk < b;
+                const uint4 z = make_uint4(0, 0, 0, 0);
+                const uint4 v = !va ? z
+                                    : (ga ? reinterpret_cast<const uint4 *>(a.xgrows)[(size_t)ri * 9 + ca]
+                                          : reinterpret_cast<const uint4 *>(a.xrows)[(size_t)blk * 7 + ca]);
+                const uint4 vo = !vb ? z
+                                     : (gb ? reinterpret_cast<const uint4 *>(a.ogrp)[(size_t)ri * 8 + cb]
+                                           : reinterpret_cast<const uint4 *>(a.ocnt)[(size_t)blk * 8 + cb]);
+                const bool pa = ga ? ri < g0 : va, pb = gb ? ri < g0 : vb;  // in the prefix
+                uint32_t gt[8], gp[8], ot4[4], op4[4];
+                const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, o4[4] = {vo.x, vo.y, vo.z, vo.w};
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const uint32_t e = w4[u] & 0x00ff00ffu, o = (w4[u] >> 8) & 0x00ff00ffu;
+                    gt[2 * u] = group_sum<16>(e);
+                    gt[2 * u + 1] = group_sum<16>(o);
+                    gp[2 * u] = group_sum<16>(pa ? e : 0u);
+                    gp[2 * u + 1] = group_sum<16>(pa ? o : 0u);
+                    ot4[u] = group_sum<16>(o4[u]);
+                    op4[u] = group_sum<16>(pb ? o4[u] : 0u);
+                }
+                if (ri == 0) {
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) {
+                        const int by = ca * 16 + (u >> 1) * 4 + (u & 1);
+                        if (ga) {
+                            gsum[0][by] = gt[u] & 0xffffu;
+                            gsum[0][by + 2] = gt[u] >> 16;
+                            gsum[1][by] = gp[u] & 0xffffu;
+                            gsum[1][by + 2] = gp[u] >> 16;
+                        } else {
+                            gsum[2][by] = gp[u] & 0xffffu;
+                            gsum[2][by + 2] = gp[u] >> 16;
+                        }
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        if (gb) {
+                            osum[0][cb * 4 + u] = ot4[u];
+                            osum[1][cb * 4 + u] = op4[u];
+                        } else {
+                            osum[2][cb * 4 + u] = op4[u];
+                        }
+                    }
+                }
+            }
             // packed: bytes two to a word (16-bit halves; <= kXRowsMaxBlocks x 240 each)
             uint32_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             uint32_t ot[4] = {0, 0, 0, 0}, op[4] = {0, 0, 0, 0};
-            {
+            if (!xg) {
                 const uint4 *src = reinterpret_cast<const uint4 *>(a.xrows) + q;
                 const uint4 *ow = reinterpret_cast<const uint4 *>(a.ocnt) + q2;
                 const bool xon = q < nq16;
@@ -3499,7 +3585,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 }
             }
             // the parts of each column: adjacent lanes (Pp = Pp2, 8 / 16 / 32), DPP sums
-            auto gsum = [&](auto g) {
+            auto psum = [&](auto g) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     tp[u] = group_sum<decltype(g)::value>(tp[u]);
@@ -3511,10 +3597,11 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                     op[u] = group_sum<decltype(g)::value>(op[u]);
                 }
             };
-            if (Pp == 32) gsum(std::integral_constant<int, 32>{});
-            else if (Pp == 16) gsum(std::integral_constant<int, 16>{});
-            else gsum(std::integral_constant<int, 8>{});
-            if (j == 0 && q < nq16) {
+            if (xg) {
+            } else if (Pp == 32) psum(std::integral_constant<int, 32>{});
+            else if (Pp == 16) psum(std::integral_constant<int, 16>{});
+            else psum(std::integral_constant<int, 8>{});
+            if (!xg && j == 0 && q < nq16) {
 #pragma unroll
                 for (int u = 0; u < 8; ++u) {
                     // packed word u: int4 word u / 2, even (u even) / odd bytes; halves 2 bytes apart
@@ -3525,7 +3612,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                     xcol[1][by + 2] = pp[u] >> 16;
                 }
             }
-            if (j2 == 0) {
+            if (!xg && j2 == 0) {
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     ocol[0][q2 * 4 + u] = ot[u];
@@ -3542,17 +3629,28 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             }
             __syncthreads();
             STAMP(a, SO, 4);
+            // column r's totals and prefixes: from the digits (group rows: 4 digits, block rows 3)
+            auto tot_all = [&](int r) -> uint32_t {
+                return xg ? gsum[0][r] + (gsum[0][xs + r] << 4) + (gsum[0][2 * xs + r] << 8) + (gsum[0][3 * xs + r] << 12)
+                          : xcol[0][r] + (xcol[0][xs + r] << 4) + (xcol[0][2 * xs + r] << 8);
+            };
+            auto pre_all = [&](int r) -> uint32_t {
+                return xg ? gsum[1][r] + (gsum[1][xs + r] << 4) + (gsum[1][2 * xs + r] << 8) + (gsum[1][3 * xs + r] << 12) +
+                                gsum[2][r] + (gsum[2][xs + r] << 4) + (gsum[2][2 * xs + r] << 8)
+                          : xcol[1][r] + (xcol[1][xs + r] << 4) + (xcol[1][2 * xs + r] << 8);
+            };
             // the capacity sum_r<R A(r) = sum of c when max c <= R
-            uint32_t cp = t < R ? xcol[0][t] + (xcol[0][xs + t] << 4) + (xcol[0][2 * xs + t] << 8) : 0u;
+            uint32_t cp = t < R ? tot_all(t) : 0u;
             cp = wave_sum_u32(cp);
             if (lane == 0) sred[w][0] = cp;
 #pragma unroll
             for (int k = 0; k < kRCh; ++k) {
                 const int rr = min(64 * k + lane, R - 1);
-                Av[k] = xcol[0][rr] + (xcol[0][xs + rr] << 4) + (xcol[0][2 * xs + rr] << 8);
-                pv[k] = xcol[1][rr] + (xcol[1][xs + rr] << 4) + (xcol[1][2 * xs + rr] << 8);
-                oAv[k] = ocol[0][rr];
-                opv[k] = ocol[1][rr];
+                const bool kin = 64 * k < R;  // (chunks past the table: lanes never read)
+                Av[k] = kin ? tot_all(rr) : 0u;
+                pv[k] = kin ? pre_all(rr) : 0u;
+                oAv[k] = !kin ? 0u : (xg ? osum[0][rr] : ocol[0][rr]);
+                opv[k] = !kin ? 0u : (xg ? osum[1][rr] + osum[2][rr] : ocol[1][rr]);
                 uint32_t sc = 0, osc = 0;
 #pragma unroll
                 for (int qq = 0; qq < kWaves - 1; ++qq) {
