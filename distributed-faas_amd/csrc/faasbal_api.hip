@@ -1756,8 +1756,11 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
     // whichever is larger; a launched tick: its own width and rows
     const int64_t Qlog = Qn + 2 * E;
     if (n_events < 0) {
+        // the wide form at the largest queue, or a queue of at most kXRowsMaxBlocks blocks
+        // with a 128-row table's block rows (a 32-row table's block + group rows are smaller)
+        const int64_t Qr = std::min<int64_t>(Qlog, (int64_t)kXRowsMaxBlocks * kBS);
         *bytes = (int64_t)std::max(xlayout(c->world, E, Qlog, 2).total,
-                                   xlayout(c->world, E, Qlog, 1, xrows_bytes(c->world, kRFused, Qlog)).total);
+                                   xlayout(c->world, E, Qr, 1, xrows_bytes(c->world, kRFused, Qr)).total);
     } else {
         const int R = c->launched ? c->l_R : kRFused;
         *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xrows_bytes(c->world, R, Qlog),

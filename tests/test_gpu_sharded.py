@@ -298,3 +298,32 @@ def test_sharded_wide_table_with_tight_log_shards(world):
     _cmp(bals, o, a, b, 0)
     for x in bals:
         x.close()
+
+
+@pytest.mark.parametrize("world,nbq,cap", [(3, 1, 30), (3, 17, 30), (3, 256, 30), (3, 257, 30), (3, 17, 60),
+                                           (3, 256, 120), (2, 40, 120), (16, 17, 30)])
+def test_sharded_exchanged_rows_shapes(world, nbq, cap):
+    """Phase 2 from the exchanged block rows (<= 256 queue blocks, <= 16 ranks) and, at a
+    32-row table, group rows (16 blocks per group, a partial last group): queue lengths
+    around those limits (257 blocks: the phase-2 scan instead), tables of 32 / 64 / 128
+    rows (the second tick sizes its table from the first's max free count), 16 ranks."""
+    rng = np.random.default_rng(1000 * nbq + cap + world)
+    W = max(world, nbq * 256 - 10)
+    now = 1000.0
+    free = rng.integers(0, cap + 1, W).astype(np.int32)
+    hb = np.where(rng.random(W) < 0.05, now - 10.5, now - rng.random(W) * 9.0)
+    queue = rng.permutation(np.nonzero(free > 0)[0]).astype(np.int32)
+    if len(queue) < W - 12:  # fill the queue to the target length with free-0 workers (c = 1)
+        rest = np.setdiff1d(np.arange(W), queue)[: W - 12 - len(queue)]
+        queue = rng.permutation(np.concatenate([queue, rest])).astype(np.int32)
+    log = rng.integers(-1, W, 3 * W).astype(np.int32)
+    st = dict(reg=np.ones(W, np.uint8), free=free, hb=hb, epoch=np.zeros(W, np.uint32), queue=queue, log=log)
+    n_new = max(1, int(W * cap / 8))
+    bals, o = _group(st, world, len(log) + 4 * n_new + W + 16, max_events=64)
+    carried = 0
+    for t in range(3):
+        args = (now + 0.1 * t, 10.0, [], [], [], [], [], carried + n_new)
+        a, r = _group_tick(bals, *args)
+        b = o.tick(*args)
+        _cmp(bals, o, a, b, t)
+        carried = carried + n_new + len(b["orphans"]) - len(b["assign"])
