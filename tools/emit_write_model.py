@@ -1,5 +1,8 @@
 """Model of k_emit2's task-store bytes at configs[2] (VERDICT r3 ask 4).
 
+Refuted by measurement (profiles/NOTES_r04.md): granule-aligned block runs wrote the same
+PMC bytes at configs[3], so run ends merge in L2; kept as the record of the hypothesis.
+
 Every wave stores its active lanes' tasks of a round as one contiguous run of 4-byte
 slots (task index base(r) + its rank among the wave's active lanes); a run starts and
 ends inside a memory granule that the neighbouring wave's run shares.  If each store
