@@ -485,7 +485,11 @@ struct XLayout {
 // <= 16 ranks, a table of <= kRFused rows, <= kXRowsMaxBlocks queue blocks
 inline size_t xrows_bytes(int world, int R, int64_t Qlog) {
     const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
-    if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused || nbq > kXRowsMaxBlocks) return 0;
+    // (phase 2 walks the digit rows and this rank's rows in the same rounds: their parts per
+    // column must agree, as they do for the 32 / 64 / 128-row tables)
+    if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused || nbq > kXRowsMaxBlocks ||
+        xr_parts(R) != kBS / (R / 4))
+        return 0;
     return (size_t)nbq * xr_row(R);
 }
 // ... and the group rows (R = kXGroupR only)
