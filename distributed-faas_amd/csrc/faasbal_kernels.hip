@@ -3460,6 +3460,10 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             const int q = t / Pp, j = t % Pp, q2 = t / Pp2, j2 = t % Pp2;
             const bool xg = a.xgrows != nullptr;  // group rows (R = kXGroupR)
             __shared__ uint32_t gsum[3][kXGroupDigits * 36], osum[3][kXGroupR];  // group tot / pre, block pre
+            // (the group path's lane map: 9 + 7 digit-row and 8 + 8 own-row load columns at R = 32)
+            static_assert(xg_row(kXGroupR) == 9 * 16 && xr_row(kXGroupR) == 7 * 16 && kXGroupR / 4 == 8,
+                          "group-row lane map");
+            static_assert(kXRowsMaxBlocks <= kXGroupBlocks * 16, "<= 16 group rows per column");
             if (xg) {
                 // ---- lanes 16 i .. 16 i + 15: one 16-byte column of the <= 16 group rows or of
                 // the rows of the blocks of b's group before b (lane & 15 = row); pass A the
