@@ -3695,9 +3695,12 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
 #pragma unroll 4
                 for (int bb = b0 + j; bb < b; bb += tpc) pre += bc[(size_t)bb * R];
             }
-            for (int o = 1; o < tpc; o <<= 1) {  // the column's tpc threads are adjacent lanes
-                tot += (uint32_t)__shfl_xor((int)tot, o);
-                pre += (uint32_t)__shfl_xor((int)pre, o);
+            if (tpc == 4) {  // the column's tpc threads are adjacent lanes: DPP sums
+                tot = group_sum<4>(tot);
+                pre = group_sum<4>(pre);
+            } else if (tpc == 2) {
+                tot = group_sum<2>(tot);
+                pre = group_sum<2>(pre);
             }
             if (col < 2 * R && j == 0) {
                 sT[tab][r] = tot;
