@@ -1885,14 +1885,15 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 // fused: the group's row of round totals (memory-side atomics, no return)
                 if (a.grp_on && t) atomicAdd(&a.grp[(b >> a.gshift) * a.gstride + rc + threadIdx.x], t);
             }
-            if (tab == 0) {
+            if (tab == 0 && !a.fused) {
                 // sum_r count(c > r) over r < R = sum of min(c, R): the block's capacity when c <= R
+                // (k_plan's; a fused k_emit2 sums the totals of the group rows itself)
                 const uint32_t ts = wave_sum_u32(t);
                 if (lane_id() == 0) l4[wave_id()] = ts;
                 lds_barrier();
                 csum += (unsigned long long)l4[0] + l4[1] + l4[2] + l4[3];
             }
-            lds_barrier();
+            if (rc + kBS < a.R) lds_barrier();  // (wc is rewritten by the next column chunk)
         }
     }
     }
