@@ -3475,13 +3475,16 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                 const int ca = ga ? t >> 4 : (t - 144) >> 4, cb = gb ? t >> 4 : (t - 128) >> 4;
                 const int blk = g0 * kXGroupBlocks + ri;
                 const bool va = ga ? ri < ng : blk < b, vb = gb ? ri < ng : blk < b;
-                const uint4 z = make_uint4(0, 0, 0, 0);
-                const uint4 v = !va ? z
-                                    : (ga ? reinterpret_cast<const uint4 *>(a.xgrows)[(size_t)ri * 9 + ca]
-                                          : reinterpret_cast<const uint4 *>(a.xrows)[(size_t)blk * 7 + ca]);
-                const uint4 vo = !vb ? z
-                                     : (gb ? reinterpret_cast<const uint4 *>(a.ogrp)[(size_t)ri * 8 + cb]
-                                           : reinterpret_cast<const uint4 *>(a.ocnt)[(size_t)blk * 8 + cb]);
+                // both loads unconditional (clamped rows, one pointer per lane) and masked after:
+                // a guarded load would become a branch with its own wait
+                const int rg = min(ri, ng - 1), rb = min(blk, a.nbq - 1);
+                const uint4 *pa_ = ga ? reinterpret_cast<const uint4 *>(a.xgrows) + (size_t)rg * 9 + ca
+                                      : reinterpret_cast<const uint4 *>(a.xrows) + (size_t)rb * 7 + ca;
+                const uint4 *pb_ = gb ? reinterpret_cast<const uint4 *>(a.ogrp) + (size_t)rg * 8 + cb
+                                      : reinterpret_cast<const uint4 *>(a.ocnt) + (size_t)rb * 8 + cb;
+                uint4 v = *pa_, vo = *pb_;
+                if (!va) v = make_uint4(0, 0, 0, 0);
+                if (!vb) vo = make_uint4(0, 0, 0, 0);
                 const bool pa = ga ? ri < g0 : va, pb = gb ? ri < g0 : vb;  // in the prefix
                 uint32_t gt[8], gp[8], ot4[4], op4[4];
                 const uint32_t w4[4] = {v.x, v.y, v.z, v.w}, o4[4] = {vo.x, vo.y, vo.z, vo.w};
@@ -3524,16 +3527,23 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             uint32_t tp[8] = {0, 0, 0, 0, 0, 0, 0, 0}, pp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
             uint32_t ot[4] = {0, 0, 0, 0}, op[4] = {0, 0, 0, 0};
             if (!xg) {
-                const uint4 *src = reinterpret_cast<const uint4 *>(a.xrows) + q;
+                const uint4 *src = reinterpret_cast<const uint4 *>(a.xrows) + (q < nq16 ? q : 0);
                 const uint4 *ow = reinterpret_cast<const uint4 *>(a.ocnt) + q2;
                 const bool xon = q < nq16;
                 for (int r0 = 0; r0 < a.nbq; r0 += 8 * Pp) {  // (rounds of 8 rows per thread)
                     uint4 v[8], vo[8];
+                    // unconditional loads of clamped rows, masked after (no branch per load)
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
                         const int bb = r0 + j + k * Pp, b2 = (r0 / Pp) * Pp2 + j2 + k * Pp2;
-                        v[k] = (xon && bb < a.nbq) ? src[(size_t)bb * nq16] : make_uint4(0, 0, 0, 0);
-                        vo[k] = b2 < a.nbq ? ow[(size_t)b2 * nq] : make_uint4(0, 0, 0, 0);
+                        v[k] = src[(size_t)min(bb, a.nbq - 1) * nq16];
+                        vo[k] = ow[(size_t)min(b2, a.nbq - 1) * nq];
+                    }
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const int bb = r0 + j + k * Pp, b2 = (r0 / Pp) * Pp2 + j2 + k * Pp2;
+                        if (!(xon && bb < a.nbq)) v[k] = make_uint4(0, 0, 0, 0);
+                        if (b2 >= a.nbq) vo[k] = make_uint4(0, 0, 0, 0);
                     }
 #pragma unroll
                     for (int k = 0; k < 8; ++k) {
