@@ -583,11 +583,14 @@ def main():
         from faasbal.sharded import ShardedBalancer
         g = ShardedBalancer(rank, world, W, 2 * F + T + 16, max_events=1, device=dev)
         g.load(st)
+        # the balancer's stream is torch's current stream for the whole run: the exchange
+        # all-reduce is enqueued on it (phase 2 ordered after it, no host sync) without a
+        # stream switch per step
+        torch.cuda.set_stream(g.stream)
 
         def step():
             g.launch(1000.0, 10.0, n_pending=T)
-            with torch.cuda.stream(g.stream):
-                dist.all_reduce(g.exchange(), async_op=True).wait()  # phase 2 ordered after it on g.stream
+            dist.all_reduce(g.exchange())
             g.cont()
     step()
     res = g.wait()

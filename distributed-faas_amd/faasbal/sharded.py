@@ -108,8 +108,11 @@ class ShardedBalancer(GpuBalancer):
         self._xbytes = n.value
 
     def exchange(self):
-        """The tick's exchange region (a view of the bound torch tensor)."""
-        return self.xbuf[: self._xbytes]
+        """The tick's exchange region (a view of the bound torch tensor, kept while its size is)."""
+        xv = getattr(self, "_xview", None)
+        if xv is None or xv.numel() != self._xbytes:
+            xv = self._xview = self.xbuf[: self._xbytes]
+        return xv
 
     def cont(self):
         self._chk(self.lib.fb_tick_continue(self.h))
