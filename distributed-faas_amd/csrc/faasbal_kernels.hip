@@ -3872,10 +3872,32 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         // ---- full rounds r < min(L, max own c of the wave): own lanes append their task
         const int owmx = (int)wave_max_u32((uint32_t)oc);
         const int rfull = L < owmx ? L : owmx;
+        // (32-bit byte offsets from the arena base when it spans < 4 GB: a saddr store per
+        // array, as k_emit2's rounds; four rounds per step)
+        char *const ab = a.arena;
+        const uint32_t so = (uint32_t)((char *)lslot - ab), qo = (uint32_t)((char *)lseq - ab);
 #pragma unroll
         for (int k = 0; k < kRCh; ++k) {
             const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
-            for (int i = 0; i < r1; ++i) {
+            int i = 0;
+            if (a.arena32) {
+                for (; i + 3 < r1; i += 4) {
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int r = 64 * k + i + u;
+                        const uint64_t m = __ballot(c > r);
+                        const uint64_t om = __ballot(oc > r);
+                        const uint32_t base = (uint32_t)__builtin_amdgcn_readlane(basev[k], i + u);
+                        const uint32_t obase = (uint32_t)__builtin_amdgcn_readlane(obasev[k], i + u);
+                        if (oc > r) {
+                            const uint32_t lp4 = 4u * (obase + popc_lt(om));
+                            *reinterpret_cast<int32_t *>(ab + (so + lp4)) = s;
+                            *reinterpret_cast<uint32_t *>(ab + (qo + lp4)) = hin + base + popc_lt(m);
+                        }
+                    }
+                }
+            }
+            for (; i < r1; ++i) {
                 const int r = 64 * k + i;
                 const uint64_t m = __ballot(c > r);
                 const uint64_t om = __ballot(oc > r);
