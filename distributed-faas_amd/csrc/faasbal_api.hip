@@ -1164,6 +1164,7 @@ int enqueue_tick(fb_ctx *c) {
         HIPCHK(c, hipGetLastError());
         return FB_OK;
     }
+    a.free_pre = (a.segw && a.slots_in_scan && !a.slots_in_apply && !c->deque && !c->l_win) ? 1 : 0;
     if (c->cm_pending) {
         // an idle tick's commit (evicted records, orphaned log entries) rides in k_scan when
         // k_scan purges the slots and reads no log entry itself

@@ -322,6 +322,11 @@ struct TickArgs {
     // k_emit2's log workgroups flag the orphans against the died bitmap in LDS and write
     // them into per-tile segments (orphans[t*2048 + i], i < fcnt[t])
     int f_emit;
+    // free_pre (one-GPU ticks on k_emit2 whose slot purge runs in k_scan): the purge writes
+    // a queued slot's next free count as if the tick served it c times ({free - c, 0}, what
+    // every position with c <= L gets) and k_emit2 rewrites only the positions with c > L --
+    // dense stores instead of one scattered 8-byte store per served worker
+    int free_pre;
     uint32_t tick;
     double now, tte;
     int64_t Qn, Qlog, head_in, T, log_cap;

@@ -93,6 +93,15 @@ __device__ __forceinline__ void wt_store(T *p, T v) {
 #endif
 }
 
+// Diagnostic builds only (tools/write_probe.py): k_emit2 output arrays whose stores are
+// dropped, to attribute the kernel's WRITE_SIZE per array -- 1 trash rows (inactive lanes
+// branch instead), 2 full-round task stores, 4 next free counts, 8 next queue, 16 orphans,
+// 32 round-L task stores.  0 in every product build.
+#ifndef FAASBAL_DIAG_NOW
+#define FAASBAL_DIAG_NOW 0
+#endif
+constexpr int kDiagNow = FAASBAL_DIAG_NOW;
+
 // k_emit2 after k_plan(2) counts the per-segment round counts of its block in LDS (1)
 // or reads the ones k_scan stored (0: 2 x 4.7 MB per streaming tick)
 #ifndef FAASBAL_SEG_LDS
@@ -1391,7 +1400,9 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         // queued: a live position of this tick's LRU queue (committed and kept, or a
         // front / back insertion) -- k_emit2 then rewrites only the slots it serves
         const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
-        a.free_out[s] = make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
+        const int32_t cq = c.fr > 1 ? c.fr : 1;  // its position's c
+        a.free_out[s] = (a.free_pre && queued) ? make_int2(c.fr - cq, 0)
+                                               : make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
         if (a.bud) {
             // untouched: the committed free count is c.fr; a slot without a record has none
             const uint32_t pin = c.t ? ip : (c.reg0 ? (uint32_t)(b0 - c.fr) : 0u);
@@ -2675,7 +2686,8 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
         uint32_t tot;
         const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(m), l4, tot);
         int64_t oo = o + ex;
-        for (uint32_t mm = m; mm; mm &= mm - 1) wt_store(a.orphans + oo++, (int64_t)(e0 + __builtin_ctz(mm)));
+        if (!(kDiagNow & 16))
+            for (uint32_t mm = m; mm; mm &= mm - 1) wt_store(a.orphans + oo++, (int64_t)(e0 + __builtin_ctz(mm)));
         o += tot;
     }
     if (tid == 0) a.fcnt[t] = (uint32_t)(o - tbase);
@@ -2972,8 +2984,52 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             basev[k] = (int32_t)Sv[k] + rbv[k];  // valid for r <= rlim
         }
         STAMP(a, SO, 2);
-        // ---- full rounds r < min(L, max c of the wave): every active lane takes one task
         int32_t *const out = a.log_slot + a.head_in;
+        // ---- round L (partial: ranks < pL) and round L + 1 (ranks for the next queue)
+        const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
+        const int rbL = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, Lc), Ll);
+        const int rbL1 = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, L1c), L1l);
+        const uint64_t mL = __ballot(c > L);
+        const int64_t rankL = (int64_t)rbL + popc_lt(mL);
+        const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
+        // round L's stores and the position's next state (free count, next queue)
+        auto finish = [&]() {
+            if (!(kDiagNow & 32) && c > L && rankL < pL) wt_store(out + S_L + rankL, s);
+            if (c > 0) {
+                int64_t n_q = c < L ? c : L;
+                if (c > L && rankL < pL) n_q += 1;
+                int64_t np = -1;
+                if (c > L) {
+                    if (rankL >= pL) np = rankL - pL;
+                    else if (c > L1) np = (AL - pL) + exL1;
+                    // the one position of rank pL in A_L knows the next queue's length
+                    if (rankL == pL) a.hout->new_qlen = (AL - pL) + exL1;
+                }
+                if (a.deque) {
+                    deque_finish(a, pos, s, c, L, n_q, c > L && rankL < pL, np);
+                    return;
+                }
+                // the worker's next {free, queued}: one 8-byte store, only for the workers served
+                // this tick -- the slot role already wrote {free, 1} for every queued one (a
+                // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
+                // (free_pre: the purge wrote {raw - c, 0}, this position's value when c <= L)
+                if (!(kDiagNow & 4) && (a.free_pre ? c > L : (n_q != 0 || np < 0))) {
+                    wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
+                }
+
+                if (!(kDiagNow & 8) && np >= 0) {
+                    wt_store(a.queue_out + np, s);
+                    wt_store(a.qfree_out + np, raw - (int32_t)n_q);
+                    wt_store(a.qhb_out + np, hb0);
+                }
+            }
+        };
+        // heartbeat loop: issued before the full rounds, so the scattered free-count stores
+        // are under way while the rounds store (configs[2]: 10.30 -> 10.16 us per tick; as
+        // agent-scope stores no change, as nontemporal stores +0.7 us)
+        const bool fin_first = !a.deque;
+        if (fin_first) finish();
+        // ---- full rounds r < min(L, max c of the wave): every active lane takes one task
         const int wmx = (int)wave_max_u32((uint32_t)c);
         const int rfull = L < wmx ? L : wmx;
 #pragma unroll
@@ -2987,6 +3043,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // the 19 rounds from 2.0 K to 3.6 K cycles: rejected.)
             // (one 1 KB trash row per block, 1024 rows: no line shared between blocks)
             int32_t *const tr = a.trash + (size_t)(blockIdx.x & (kTrashRows - 1)) * kBS + threadIdx.x;
+            if (kDiagNow & 2) i = r1;
             if (!PLAN && a.arena32) {
                 // every buffer lies in the context's arena (< 4 GB): 32-bit byte offsets from
                 // one scalar base -- a select and a saddr store per round, no 64-bit math
@@ -3001,7 +3058,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                         const uint64_t m = __ballot(act);
                         const uint32_t po = __builtin_amdgcn_readlane(bo, i + u) + 4u * popc_lt(m);
                         const uint32_t off = to + ((po - to) & (0u - (uint32_t)act));
-                        wt_store((int32_t *)(ab + off), s);
+                        if (!(kDiagNow & 1)) wt_store((int32_t *)(ab + off), s);
+                        else if (act) wt_store((int32_t *)(ab + po), s);
                     }
                 }
             }
@@ -3032,40 +3090,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             }
         }
         STAMP(a, SO, 3);
-        // ---- round L (partial: ranks < pL) and round L + 1 (ranks for the next queue)
-        const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
-        const int rbL = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, Lc), Ll);
-        const int rbL1 = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, L1c), L1l);
-        const uint64_t mL = __ballot(c > L);
-        const int64_t rankL = (int64_t)rbL + popc_lt(mL);
-        if (c > L && rankL < pL) wt_store(out + S_L + rankL, s);
-        const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
-        if (c > 0) {
-            int64_t n_q = c < L ? c : L;
-            if (c > L && rankL < pL) n_q += 1;
-            int64_t np = -1;
-            if (c > L) {
-                if (rankL >= pL) np = rankL - pL;
-                else if (c > L1) np = (AL - pL) + exL1;
-                // the one position of rank pL in A_L knows the next queue's length
-                if (rankL == pL) a.hout->new_qlen = (AL - pL) + exL1;
-            }
-            if (a.deque) {
-                deque_finish(a, pos, s, c, L, n_q, c > L && rankL < pL, np);
-                STAMP(a, SO, 15);
-                return;
-            }
-            // the worker's next {free, queued}: one 8-byte store, only for the workers served
-            // this tick -- the slot role already wrote {free, 1} for every queued one (a
-            // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
-            if (n_q != 0 || np < 0) wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
-
-            if (np >= 0) {
-                wt_store(a.queue_out + np, s);
-                wt_store(a.qfree_out + np, raw - (int32_t)n_q);
-                wt_store(a.qhb_out + np, hb0);
-            }
-        }
+        if (!fin_first) finish();
         STAMP(a, SO, 15);
         return;
     }
