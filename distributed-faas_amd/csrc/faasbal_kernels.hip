@@ -3953,7 +3953,6 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
             if (c > L && rankL < p) n_q += 1;
-            if (own) a.free_out[ls].x = rawq - (int32_t)n_q;
             int64_t np = -1;
             if (c > L) {
                 if (rankL >= p) np = rankL - p;
@@ -3964,10 +3963,9 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                     a.hout->n_local = oSL + orankL;
                 }
             }
-            if (np >= 0) {
-                a.queue_out[np] = s;  // the next queue is replicated on every rank
-                if (own) a.free_out[ls].y = 1;
-            }
+            // the owned worker's next {free, queued} in one 8-byte store (the purge wrote {., 0})
+            if (own) a.free_out[ls] = make_int2(rawq - (int32_t)n_q, np >= 0 ? 1 : 0);
+            if (np >= 0) a.queue_out[np] = s;  // the next queue is replicated on every rank
         }
         STAMP(a, SO, 15);
         return;
@@ -4162,7 +4160,6 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
     if (c > 0) {
         int64_t n_q = c < L ? c : L;
         if (c > L && rankL < p) n_q += 1;
-        if (own) a.free_out[ls].x = rawq - (int32_t)n_q;
         int64_t np = -1;
         if (c > L) {
             if (rankL >= p) np = rankL - p;
@@ -4172,10 +4169,9 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
                 a.hout->n_local = oSL + orankL;
             }
         }
-        if (np >= 0) {
-            a.queue_out[np] = s;
-            if (own) a.free_out[ls].y = 1;
-        }
+        // the owned worker's next {free, queued} in one 8-byte store (the purge wrote {., 0})
+        if (own) a.free_out[ls] = make_int2(rawq - (int32_t)n_q, np >= 0 ? 1 : 0);
+        if (np >= 0) a.queue_out[np] = s;
     }
 }
 
