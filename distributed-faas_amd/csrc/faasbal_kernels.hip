@@ -69,28 +69,12 @@ namespace fb {
     } while (0)
 #endif
 
-// Output stores of the emission kernel: write-through (agent-scope relaxed atomic
-// store = global_store ... sc1) so the lines do not stay dirty in the writing XCD's
-// L2 -- a predecessor's dirty lines stagger the next kernel's start across XCDs by
-// ~1 us while they are written back -- but sc1 stores cost more than they save
-// on configs[2] (11.2 vs 11.0 us per tick), so plain stores are the default
-// (FAASBAL_WT=1: write-through, A/B knob).
-#ifndef FAASBAL_WT
-#define FAASBAL_WT 0
-#endif
+// Output stores of the emission kernel: plain stores.  (Write-through -- agent-scope
+// relaxed stores, global_store ... sc1 -- keeps the lines from staying dirty in the writing
+// XCD's L2, but cost more than it saved on configs[2]: 11.2 vs 11.0 us per tick.)
 template <typename T>
 __device__ __forceinline__ void wt_store(T *p, T v) {
-#if FAASBAL_WT
-    static_assert(sizeof(T) == 4 || sizeof(T) == 8, "4- or 8-byte stores");
-    if constexpr (sizeof(T) == 4)
-        __hip_atomic_store(reinterpret_cast<uint32_t *>(p), __builtin_bit_cast(uint32_t, v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    else
-        __hip_atomic_store(reinterpret_cast<uint64_t *>(p), __builtin_bit_cast(uint64_t, v), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-#else
     *p = v;
-#endif
 }
 
 // Diagnostic builds only (tools/write_probe.py): k_emit2 output arrays whose stores are
@@ -102,16 +86,10 @@ __device__ __forceinline__ void wt_store(T *p, T v) {
 #endif
 constexpr int kDiagNow = FAASBAL_DIAG_NOW;
 
-// k_emit2 after k_plan(2) counts the per-segment round counts of its block in LDS (1)
-// or reads the ones k_scan stored (0: 2 x 4.7 MB per streaming tick)
-#ifndef FAASBAL_SEG_LDS
-#define FAASBAL_SEG_LDS 1
-#endif
-// Fused ticks: orphan / eviction totals through atomics into the group rows (1), or
-// read back by every emit queue block from the per-block counts (0).
-#ifndef FAASBAL_GRP_OW
-#define FAASBAL_GRP_OW 1
-#endif
+// k_emit2 after k_plan(2) counts the per-segment round counts of its block in LDS
+// (reading the ones k_scan stores would move 2 x 4.7 MB per streaming tick)
+// Fused ticks: orphan / eviction totals through atomics into the group rows (reading
+// back every per-block count in each emit queue block was slower)
 
 __device__ __forceinline__ int lane_id() { return threadIdx.x & 63; }
 __device__ __forceinline__ int wave_id() { return threadIdx.x >> 6; }
@@ -342,13 +320,10 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 // the ~1 KB block pays one scalar-cache miss round per newly touched 64-byte line,
 // in dependent rounds.  Touching one dword of every line up front (a value the
 // kernel then depends on) puts the whole block into the scalar cache in one round;
-// the later field loads hit it.  (FAASBAL_KA_PREFETCH=0: off, A/B knob.)
-#ifndef FAASBAL_KA_PREFETCH
-#define FAASBAL_KA_PREFETCH 1
-#endif
+// the later field loads hit it.
 template <class A>
 __device__ __forceinline__ void prefetch_args(const A &a) {
-    if constexpr (FAASBAL_KA_PREFETCH) {
+    {
         constexpr int nl = (int)((sizeof(A) + 63) / 64);
         const uint32_t *w = reinterpret_cast<const uint32_t *>(&a);
         uint32_t x = 0;
@@ -997,7 +972,7 @@ __device__ __forceinline__ void count_wpart(const EvArgs &a, int part, uint32_t 
 }
 __device__ __forceinline__ void count_evicted(const EvArgs &a, int tile, uint32_t n) {
     atomicAdd(&a.wcnt[tile], n);
-    if (FAASBAL_GRP_OW && a.grp) atomicAdd(&a.grp[(tile % a.ngrp) * a.gstride + a.R + 2], n);
+    if (a.grp) atomicAdd(&a.grp[(tile % a.ngrp) * a.gstride + a.R + 2], n);
 }
 // orphans of dead registrations into column R + 1 of a group row (f_emit ticks: k_emit2
 // sums every row for O before the fill level; no log scan precedes it)
@@ -1433,7 +1408,7 @@ __device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t 
         const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
         a.wcnt[blk] = n;
         // fused: evictions into column R + 2 of a group row (k_emit2 sums every row)
-        if (FAASBAL_GRP_OW && a.grp_on && n) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 2], n);
+        if (a.grp_on && n) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 2], n);
     }
 }
 
@@ -1582,7 +1557,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
             const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
             a.fcnt[b] = n;
             // fused: orphans into column R + 1 of a group row (k_emit2 sums every row)
-            if (FAASBAL_GRP_OW && a.grp_on && n) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], n);
+            if (a.grp_on && n) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], n);
             if (a.shard && n)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)n);
         }
@@ -1884,7 +1859,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 }
                 wc[wave_id()][g * 64 + lane_id()] = cnt;
                 // per 64-position segment (k_emit2 derives its rank bases from these rows)
-                if ((a.fused || !FAASBAL_SEG_LDS) && a.segw && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
+                if (a.fused && a.segw && tab == 0 && r0 < rc + rn && g * 64 + lane_id() < rn)
                     a.segcnt[(size_t)(4 * b + wave_id()) * a.R + r0 + lane_id()] = cnt;
             }
             lds_barrier();
@@ -2085,7 +2060,7 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
         wtot += cnt;
         if (lane == 0) {
             a.fcnt[b] = cnt;
-            if (FAASBAL_GRP_OW && a.grp_on && cnt) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], cnt);
+            if (a.grp_on && cnt) atomicAdd(&a.grp[(b % a.ngrp) * a.gstride + a.R + 1], cnt);
             if (a.shard && cnt)
                 atomicAdd(&a.xrec[a.rank * kXRecWords + (b & (kXRecLines - 1)) * 16], (unsigned long long)cnt);
         }
@@ -2230,11 +2205,6 @@ __global__ __launch_bounds__(kBS) void k_plan2(TickArgs a) {
         const bool gin = (int)threadIdx.x < ng;
         const uint32_t mg = gin ? a.grp[gi] : 0u, og = gin ? a.grp[gi + 1] : 0u, eg = gin ? a.grp[gi + 2] : 0u;
         uint32_t fo = og, wo = eg;
-        if (!FAASBAL_GRP_OW) {  // A/B builds without the orphan / eviction atomics
-            fo = wo = 0;
-            for (int i = threadIdx.x; i < a.nbf; i += kBS) fo += a.fcnt[i];
-            for (int i = threadIdx.x; i < a.nbw; i += kBS) wo += a.wcnt[i];
-        }
         const uint32_t mo = wave_max_u32(mg);
         fo = wave_sum_u32(fo);
         wo = wave_sum_u32(wo);
@@ -2713,11 +2683,7 @@ __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
 // where block L + 1's begins, in the middle of a 128-byte line: written from one XCD's
 // L2 the two halves merge there, from two XCDs each L2 writes back a partial line.
 // A bijection on [0, n) for any n.
-#ifndef FAASBAL_XCD_MAP
-#define FAASBAL_XCD_MAP 1
-#endif
 __device__ __forceinline__ int xcd_block(int i, int n) {
-    if (!FAASBAL_XCD_MAP) return i;
     const int x = i & 7, y = i >> 3, q = n >> 3, r = n & 7;
     return x * q + (x < r ? x : r) + y;
 }
@@ -2769,7 +2735,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         uint32_t segc[NCH];
         // large tables only: on the fused (configs[2]) path the histogram sits on the
         // critical path between the loads and the barrier (11.13 -> 11.45 us per tick)
-        constexpr bool kSegLds = PLAN && FAASBAL_SEG_LDS;
+        constexpr bool kSegLds = PLAN;
         __shared__ uint32_t shist[kWaves][kRFused + 1];
         __shared__ uint32_t sseg[kWaves][kRFused];
         if constexpr (kSegLds)
@@ -2892,11 +2858,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             mo = gin ? mg : 0u;
             fo = gin ? og : 0u;
             wo = gin ? eg : 0u;
-            if (!FAASBAL_GRP_OW) {
-                fo = wo = 0;
-                for (int i = threadIdx.x; i < a.nbf; i += kBS) fo += a.fcnt[i];
-                for (int i = threadIdx.x; i < a.nbw; i += kBS) wo += a.wcnt[i];
-            }
             fo = wave_sum_u32(fo);
             wo = wave_sum_u32(wo);
             mo = wave_max_u32(mo);
