@@ -144,7 +144,14 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
     K, Wu = min(args.steps, 50), min(args.warmup, 5)  # 64K distinct results per tick from the initial log
     st = synth.zipf_state(W=W, seed=0, dead_frac=0.0)
     ticks = synth.stream_ticks(st, n_ticks=Wu + 2 * K, seed=2, tasks_per_tick=T, results_per_tick=T,
-                               hb_frac=args.hb_frac)
+                               hb_frac=args.hb_frac, dt=0.0 if args.stream_quiet else 0.01)
+    if args.stream_quiet:
+        # no churn: no re-registrations and a clock that ages nobody, so no registration dies
+        # (the log scan is skipped on window ticks)
+        for tk in ticks:
+            keep = tk["ev_kind"] != synth.EV_REGISTER
+            for k in ("ev_kind", "ev_slot", "ev_val", "ev_ts", "ev_seq"):
+                tk[k] = tk[k][keep]
     E = max(len(t["ev_kind"]) for t in ticks)
     cap = len(st["log"]) + (Wu + 2 * K + 2) * 2 * T
     carried = [0]
@@ -293,9 +300,10 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
         "dtype": "int32",
         "data": "synthetic (faasbal.synth.zipf_state(W, seed=0, dead_frac=0) + stream_ticks(seed=2))",
         "config": {"workload": "configs[4]: %d workers%s, %d new tasks + %d results + %d joins + %d heartbeats "
-                               "per tick, 10 ms per tick, committed ticks"
+                               "per tick, %s, committed ticks"
                                % (W, "" if world == 1 else " sharded by worker-id range over %d GPUs" % world, T, T,
-                                  max(1, W // 1000), max(1, int(args.hb_frac * W))),
+                                  0 if args.stream_quiet else max(1, W // 1000), max(1, int(args.hb_frac * W)),
+                                  "a clock that ages nobody (no churn)" if args.stream_quiet else "10 ms per tick"),
                    "workers": W, "events_per_tick": stats["events"] / K, "assigned_per_tick": stats["assigned"] / K,
                    "events_in": {"hbm": "HBM-resident (every tick's batch copied to the GPU before the timed "
                                          "region; read in place, checked by the tick's first kernel)",
@@ -505,6 +513,8 @@ def main():
                     help="stream workload: skip the PCIe-inclusive (pinned batches) pass beside the value")
     ap.add_argument("--pageable-events", action="store_true",
                     help="stream: messages in pageable numpy arrays (staging copies them into pinned memory)")
+    ap.add_argument("--stream-quiet", action="store_true",
+                    help="stream workload without churn: no re-registrations, no expiry (nobody dies)")
     ap.add_argument("--hb-frac", type=float, default=0.01,
                     help="stream: heartbeats per tick as a fraction of the workers (1.0: a 1M-message storm)")
     args = ap.parse_args()

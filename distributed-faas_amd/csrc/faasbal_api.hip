@@ -155,6 +155,7 @@ struct fb_ctx {
     uint32_t *wticket = nullptr;
     int64_t *cw = nullptr;  // commit word of the launched tick (device; eager commits read it)
     uint32_t *lpart = nullptr, *wpart = nullptr;
+    uint32_t *died_tag = nullptr;  // window ticks: the launch stamp of the last tick a registration died in
     int64_t win_slack = 8192;  // window positions scanned beyond the tasks' estimate (grows on a miss)
     int64_t last_O = 0;
     int last_L = -1;
@@ -582,7 +583,7 @@ int win_alloc(fb_ctx *c) {
     auto r256 = [](size_t b) { return (b + 255) & ~(size_t)255; };
     const size_t bytes = 2 * (r256(qcap * 4) * 2 + r256(qcap * 8) + r256(W * 4)) + r256(2 * E * 4) +
                          r256(kWinMaxCh * 8) +
-                         r256(256) + r256(1024 * 4) + r256(64 * 32 * 4);
+                         r256(256) + r256(1024 * 4) + r256(256) + r256(64 * 32 * 4);
     void *m = nullptr;
     hipError_t e = hipMalloc(&m, bytes);
     if (e != hipSuccess) return fail(c, FB_ENOMEM, "hipMalloc(window buffers %zu B) failed: %s", bytes, hipGetErrorString(e));
@@ -601,6 +602,7 @@ int win_alloc(fb_ctx *c) {
     c->wlb = (unsigned long long *)take(kWinMaxCh * 8);
     c->wticket = (uint32_t *)take(256);
     c->lpart = (uint32_t *)take(1024 * 4);
+    c->died_tag = (uint32_t *)take(256);
     c->wpart = (uint32_t *)take(64 * 32 * 4);
     const int k = c->qcur;
     if (c->Qn) {
@@ -860,6 +862,7 @@ int enqueue_tick(fb_ctx *c) {
         ea.free_out = c->free_[nxt];
         ea.dmask = (!a.slots_in_scan || a.f_sep || a.f_emit || c->l_win) ? c->dmask : nullptr;
         ea.wpart = c->l_win ? c->wpart : nullptr;
+        ea.died_tag = c->l_win ? c->died_tag : nullptr;
         if (c->l_win) {  // k_emit_win's look-back granules and ticket start from zero
             ea.wlb = c->wlb;
             ea.wlb_n = 2 * (int)cdiv(E, kWinCh) + c->l_nchW;
@@ -1106,6 +1109,7 @@ int enqueue_tick(fb_ctx *c) {
         a.lstamp = c->lstamp;
         const int nch = a.nchB + a.nchF + a.nchW;
         a.lpart = c->lpart;
+        a.died_tag = c->died_tag;
         a.n_lpart = head > 0 ? ls_grid : 0;
         if (head > 0) {
             Timer t(c, "logscan");
@@ -1265,6 +1269,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         ap.add(&c->wlb, (size_t)kWinMaxCh);
         ap.add(&c->wticket, (size_t)64);
         ap.add(&c->lpart, (size_t)1024);
+        ap.add(&c->died_tag, (size_t)64);
         ap.add(&c->wpart, (size_t)64 * 32);
     }
     ap.add(&c->reg, W);

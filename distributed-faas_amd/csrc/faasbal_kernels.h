@@ -264,6 +264,7 @@ struct EvArgs {
     uint8_t *st;
     int2 *free_out;
     unsigned long long *dmask;  // died bitmap (null: not needed), zeroed by k_ev_link, atomicOr
+    uint32_t *died_tag;         // window ticks: set to lstamp when a registration dies (null: not needed)
     uint32_t *wcnt;             // evictions per 256-slot tile, zeroed by k_ev_link, atomicAdd
     uint32_t *grp;              // group rows (null: none); evictions into column R + 2
     int ngrp, gstride, R;
@@ -383,6 +384,7 @@ struct TickArgs {
     int64_t *cw;                 // commit word {failed, window head, window length} (eager commits)
     int64_t cw_tag;              // failures store this launch's link stamp into cw[0]
     uint32_t *lpart;             // k_logscan: orphans per log workgroup
+    uint32_t *died_tag;          // window ticks: == lstamp iff the apply's purge saw a registration die
     int n_lpart;
     uint32_t *wpart;             // evictions / live queued slots, 64 partials (EvArgs::wpart)
     const int32_t *pos_in;       // committed position of each queued slot

@@ -988,6 +988,7 @@ __device__ __forceinline__ bool SlotRun::purge(const EvArgs &a, uint32_t s, int 
     // in-flight entries (a dead slot's budget is never read)
     if (a.bud_next) a.bud_next[s] = (int32_t)((alive && !died) ? infl0 - ncl : 0u) + fr;
     if (died && a.dmask) atomicOr(&a.dmask[s >> 6], 1ull << (s & 63));
+    if (died && a.died_tag) *a.died_tag = a.lstamp;  // (the same value from every writer)
     if (evicted) count_evicted(a, (int)(s >> 8), 1u);
     count_orphans(a, (int)(s >> 8), no);
     return queued;
@@ -1022,6 +1023,7 @@ __device__ __forceinline__ void apply_slot_block(const EvArgs &a, int blk) {
     const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
     if (lane_id() == 0) {
         if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
+        if (a.died_tag && dm) *a.died_tag = a.lstamp;
         if (ne) count_evicted(a, blk, ne);
         count_orphans(a, blk, nw);
         if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
@@ -1989,6 +1991,14 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows
     STAMP(a, SO, 0);
     const int lblk = (int)blockIdx.x, nlblk = (int)gridDim.x;
+    if (a.died_tag && *a.died_tag != a.lstamp) {
+        // window tick in which no registration died: no entry is an orphan, so the log is
+        // not read -- every tile's count and every workgroup's partial are zero
+        for (int b = lblk * kLsBS + (int)threadIdx.x; b < a.nbf; b += nlblk * kLsBS) a.fcnt[b] = 0;
+        if (threadIdx.x == 0) a.lpart[lblk] = 0;
+        STAMP(a, SO, 15);
+        return;
+    }
     const int n4 = (((a.W + 63) >> 6) + 1) >> 1;
     const uint4 *src = reinterpret_cast<const uint4 *>(a.dmask);
     for (int i0 = 0; i0 < n4; i0 += kLsBS * 8) {

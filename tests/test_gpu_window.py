@@ -71,6 +71,39 @@ def test_window_stream_vs_oracle(seed, W, T, dt, eager):
     g.close()
 
 
+@pytest.mark.parametrize("eager", [False, True])
+@pytest.mark.parametrize("seed,W,T", [(0, 8192, 512), (1, 20000, 2048)])
+def test_window_ticks_without_deaths(seed, W, T, eager):
+    """Window ticks in which no registration dies (no re-registrations, a clock that does
+    not age anyone) skip the log scan (k_logscan reads no entry: every tile count zero);
+    every third tick the clock jumps 0.4 s (~4 % of the workers expire) and keeps its
+    re-registrations, so its orphans are flagged.  Alternating the two checks that a
+    stale death mark of an earlier launch never passes for this one."""
+    st, ticks = _stream(seed, W, T, 0.0, n_ticks=12)
+    E = max(len(t["ev_kind"]) for t in ticks)
+    g, o = _pair(st, 3 * len(st["log"]) + 24 * T + 16, max_events=E, purge_mode=2, eager=eager)
+    carried = 0
+    n_orph = []
+    off = 0.0
+    for t, tk in enumerate(ticks):
+        if t % 3 != 2:  # drop the re-registrations: nobody dies this tick
+            keep = tk["ev_kind"] != synth.EV_REGISTER
+            tk = dict(tk, **{k: tk[k][keep] for k in ("ev_kind", "ev_slot", "ev_val", "ev_ts", "ev_seq")})
+        else:
+            off += 0.4
+        n = carried + tk["n_new"]
+        args = (tk["now"] + off, 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"] + off, tk["ev_seq"], n)
+        a, b = g.tick(*args), o.tick(*args)
+        _cmp(g, o, a, b, t)
+        n_orph.append(len(b["orphans"]))
+        carried = n + len(b["orphans"]) - len(b["assign"])
+    wt, fb = g.window_stats()
+    assert wt >= 6, "window ticks: %d (fallbacks %d)" % (wt, fb)
+    assert all(n_orph[t] == 0 for t in range(len(ticks)) if t % 3 != 2)
+    assert any(n_orph[t] > 0 for t in range(len(ticks)) if t % 3 == 2), n_orph
+    g.close()
+
+
 @pytest.mark.parametrize("seed", range(24))
 def test_window_random_vs_oracle(seed, eager=False):
     """Every message kind and edge case of the random scenarios (register 0 / -1 of a
