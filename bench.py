@@ -701,7 +701,9 @@ def main():
             traffic = tj["kernels"][dom]["hbm_bytes"]
             rocprof_ms = (tj["kernels"][dom].get("trace_avg_ns") or 0) * 1e-6 or None
             traffic_src = ("profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch, separate rocprofv3 --pmc "
-                           "passes), rocprof average from profiles/%s_kernel_stats.csv; summary profiles/%s_traffic.json"
+                           "passes; the x2 FETCH_SIZE correction is calibrated for 16-B-per-lane streaming reads, "
+                           "so for this kernel's 4-8 B gathers the figure is an upper bound), rocprof average from "
+                           "profiles/%s_kernel_stats.csv; summary profiles/%s_traffic.json"
                            % (tj["tag"], tj["tag"], tj["tag"]))
     line = {
         "metric": "task assignments/sec + % HBM roofline, 1M tasks x 64K workers, 1/2/4/8 GPU",
@@ -741,7 +743,9 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes": dom_bytes, "bytes_model": bytes_model,
                      "kernel_avg_ms": dom_ms, "kernel_avg_ms_rocprof": rocprof_ms,
-                     "model_frac": model_frac},
+                     "model_frac": model_frac,
+                     # the whole tick on the driver's clock: SURVEY.md 8(d) tick bytes / ms_per_step
+                     "tick_frac": B / (dt / args.steps) / 1e9 / HBM_PEAK_GBS},
         "tick": {"algorithmic_bytes": B, "device_ms": tick_dev_ms,
                  "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,
                  "kernels_avg_ms": {k: v[0] for k, v in kern.items()}},
@@ -764,10 +768,13 @@ def main():
         cm["device_ms_with_commit"] = tick_dev_ms + cm["commit_in_tick_ms"]
         cm["ms_per_step_with_commit"] = dt * 1e3 / args.steps + cm["commit_in_tick_ms"]
         cm["value_with_commit"] = n_assigned / (cm["ms_per_step_with_commit"] * 1e-3)
-        cm["note"] = ("the tick's commit folded into the next tick (folded): the evicted records' deletion in "
-                      "k_scan's W role, the orphaned log entries cleared by k_emit2's log workgroup of each tile "
-                      "(fused ticks) or by extra k_scan blocks; commit_in_tick_ms = the kernels with it - without "
-                      "it on the same state; ms_per_step_with_commit = ms_per_step + that")
+        cm["note"] = ("the configs[2] tick's commit (its 3277-ish evicted records' deletion and its orphaned log "
+                      "entries) folded into the NEXT tick (folded): the records in k_scan's W role, the log entries "
+                      "by k_emit2's log workgroup of each tile (fused ticks) or extra k_scan blocks. That next tick "
+                      "runs on the committed, depleted state (kernels_ms: fewer queued positions and tasks than the "
+                      "timed step's tick.kernels_avg_ms), so only the delta carries over: commit_in_tick_ms = its "
+                      "kernels with the fold pending - the same tick relaunched without it (same state); "
+                      "ms_per_step_with_commit = ms_per_step + that delta")
         line["committed"] = cm
     if world == 1 and not args.no_host_observed:
         line["host_observed"] = host_observed(g, st, T, min(args.steps, 50), n_assigned)

@@ -247,6 +247,9 @@ struct fb_ctx {
     int logscan = -1;      // "logscan": -1 auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
     int split_slots = -1;  // "split_slots": -1 auto (separate k_slots launch once the records outgrow L2)
+    // "fault_qlen": the next fb_tick_wait overwrites the device-reported queue length with this
+    // value before validating it (tests of check_lengths; -1 = off)
+    int64_t fault_qlen = -1;
     // deque contexts (fb_create_deque): PushDispatcher.start, task_dispatcher.py:251-322
     int deque = 0;
     int32_t *tokcnt[2] = {nullptr, nullptr}, *xw[2] = {nullptr, nullptr}, *kl[2] = {nullptr, nullptr};
@@ -734,7 +737,7 @@ int enqueue_tick(fb_ctx *c) {
     // small round tables: k_emit derives the cross-block prefixes itself (2 launches per tick)
     // fused: k_emit2 reduces the (small) round table in every block, no k_plan launch
     a.fused = (!c->shard && !c->force_plan && R <= kRFused && (int64_t)nbq * R <= (int64_t)kTabLd * kBS * 4) ? 1 : 0;
-    // large tables with R <= 128: k_emit2 after k_plan (FAASBAL_FORCE_PLAN=2: the chunked k_emit)
+    // large tables with R <= 128: k_emit2 after k_plan (fb_set_path("plan", 2): the chunked k_emit)
     a.segw = (!c->shard && R <= kRFused && c->force_plan != 2) ? 1 : 0;
     // large tables for k_emit2: group rows too, scanned by k_plan2
     const bool gplan = !a.fused && a.segw && !c->shard;
@@ -784,7 +787,7 @@ int enqueue_tick(fb_ctx *c) {
     if (a.f_sep) a.slots_in_scan = 1;
     // fused one-GPU ticks: O from the slot purge's in-flight counts, the orphans flagged
     // and compacted by k_emit2's log workgroups (k_scan without log blocks); not when the
-    // log role was asked to run as k_logscan (FAASBAL_LOGSCAN=1)
+    // log role was asked to run as k_logscan (fb_set_path("logscan", 1))
     const int nbfe = (int)cdiv(nbf, 4);
     const size_t bm16 = (size_t)(((W + 63) / 64 + 1) / 2) * 16;
     a.f_emit = (defer && a.fused && !a.f_sep && W <= kLdsBitmapSlots && nbfe <= kFEmitMaxBlocks &&
@@ -1083,9 +1086,10 @@ int enqueue_tick(fb_ctx *c) {
     }
 #endif
     if (c->l_win) {
-        // window tick (E > 0, purge in the apply launch): k_logscan's count workgroups count
-        // the chunks of [backs][fronts][window prefix] while its log workgroups write the
-        // orphans into per-tile segments; k_emit_win serves, appends and reports the window
+        // window tick (E > 0, purge in the apply launch): k_logscan writes the orphans into
+        // per-tile segments and a partial count per workgroup (nothing, when no registration
+        // died: died_tag); k_emit_win counts the chunks of [backs][fronts][window prefix] by
+        // decoupled look-back, serves, appends and reports the window
         a.win = 1;
         a.wseg = 1;
         a.nbf = nbf;
@@ -1706,7 +1710,9 @@ int fb_load_shard(fb_ctx *c, int32_t slot_base, int32_t n_workers, const uint8_t
     c->head_local = log_len;
     c->tick += 1;
     // the first tick's round table from what every rank knows alike (the exchange layout
-    // depends on it): its events' values; a fill level beyond it relaunches wider
+    // depends on it): its events' values and fb_set_round_hint (the loaded state's global
+    // max free count, which the caller knows from the global state); the rank's own max
+    // (maxc above) would differ between ranks.  A fill level beyond it relaunches wider.
     (void)maxc;
     c->maxc_hint = 1;
     c->launched = c->waited = false;
@@ -2027,6 +2033,11 @@ int fb_tick_launch_staged(fb_ctx *c, double tte, int64_t n_pending) {
     c->l_win = win_plan(c);
     for (int j = 0; j < 3; ++j) c->l_chk[j] = E ? c->st_chk[j] : nullptr;
     c->hout->bad_ev = 0;  // set by k_ev_link when it finds an invalid message
+    // lengths every finished tick writes: a value left unwritten reads back as -1 and fails
+    // check_lengths instead of becoming a copy size (a relaunch overwrites them again)
+    c->hout->new_qlen = -1;
+    c->hout->win_head = -1;
+    c->hout->win_qlen = -1;
     const int rc = enqueue_tick(c);
     if (rc) return rc;
     c->l_eager = false;
@@ -2066,6 +2077,42 @@ int fb_purge_launch(fb_ctx *c, double now, double tte) {
     if (rc) return rc;
     c->next_purge_only = true;
     return fb_tick_launch_staged(c, tte, 0);
+}
+
+// Every length a finished tick reports becomes a copy size or a kernel bound later
+// (fb_read_state's queue copy, the commit's grids, the readbacks): a value outside its
+// buffer is a device fault, reported here with both numbers, before anything uses it.
+// (task_dispatcher.py:327: the queue new_qlen describes.)
+static int check_lengths(fb_ctx *c) {
+    const HostOut &p = *c->hout;
+    const int64_t O = p.O, N = p.N_eff;
+    if (O < 0 || O > c->l_head)
+        return fail(c, FB_EHIP, "device-reported orphans %lld outside [0, %lld] (log head)", (long long)O,
+                    (long long)c->l_head);
+    if (c->shard && (p.O_local < 0 || p.O_local > c->l_head_local || p.O_local > O))
+        return fail(c, FB_EHIP, "device-reported local orphans %lld outside [0, %lld] (local log head)",
+                    (long long)p.O_local, (long long)std::min<int64_t>(c->l_head_local, O));
+    if (p.n_evicted < 0 || p.n_evicted > c->W)
+        return fail(c, FB_EHIP, "device-reported evictions %lld outside [0, %d] (slots)", (long long)p.n_evicted, c->W);
+    if (N < 0 || N > c->l_T + O)
+        return fail(c, FB_EHIP, "device-reported dispatches %lld outside [0, %lld] (pending + orphans)", (long long)N,
+                    (long long)(c->l_T + O));
+    if (c->shard && (p.n_local < 0 || p.n_local > N))
+        return fail(c, FB_EHIP, "device-reported local dispatches %lld outside [0, %lld]", (long long)p.n_local,
+                    (long long)N);
+    if (c->l_win) {
+        if (p.win_head < c->l_qoff || p.new_qlen < 0 || p.win_head > c->qcap || p.new_qlen > c->qcap - p.win_head)
+            return fail(c, FB_EHIP, "device-reported window [%lld, +%lld) outside the queue buffer [%lld, %lld)",
+                        (long long)p.win_head, (long long)p.new_qlen, (long long)c->l_qoff, (long long)c->qcap);
+        if (p.win_qlen < 0 || p.win_qlen > p.new_qlen || p.win_qlen > c->Wq_cap)
+            return fail(c, FB_EHIP, "device-reported queue length %lld outside [0, %lld] (window length)",
+                        (long long)p.win_qlen, (long long)std::min<int64_t>(p.new_qlen, c->Wq_cap));
+    } else if (p.new_qlen < 0 || (!c->deque && p.new_qlen > c->qcap)) {
+        // (deque contexts: a length past the token capacity is FB_ENOSPC below)
+        return fail(c, FB_EHIP, "device-reported queue length %lld outside [0, %lld] (queue buffer)",
+                    (long long)p.new_qlen, (long long)c->qcap);
+    }
+    return FB_OK;
 }
 
 int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
@@ -2163,6 +2210,16 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
         c->reruns++;
         int rc = enqueue_tick(c);
         if (rc) return rc;
+    }
+    if (c->fault_qlen >= 0) {
+        c->hout->new_qlen = c->fault_qlen;
+        c->hout->win_qlen = c->fault_qlen;
+        c->fault_qlen = -1;
+    }
+    if (int rc_ = check_lengths(c)) {
+        c->l_eager = false;
+        c->launched = false;  // the tick is not committed (its launch read only committed state)
+        return rc_;
     }
     const HostOut &p = *c->hout;
     if (c->deque && p.new_qlen > c->Wq_cap)
@@ -2317,13 +2374,10 @@ int fb_get_local_assignments(fb_ctx *c, int64_t first, int64_t n, int64_t *task,
     return FB_OK;
 }
 
-// Device -> host copy of a waited tick's output on the context stream.  Into pinned
-// memory (fb_host_alloc) it is one DMA at PCIe rate; into pageable memory the
-// runtime stages it.
 // Device -> host copy enqueued on the context stream: into pinned host memory by a
 // copy kernel whose stores cross PCIe directly (the DMA engine path measured 137 to
 // 344 us for 4 MB on different boxes, the kernel path is not tied to it), else by
-// hipMemcpyAsync.  (FAASBAL_D2H_KERNEL=0: always hipMemcpyAsync.)
+// hipMemcpyAsync (pageable memory: the runtime stages it).
 static int d2h(fb_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!bytes) return FB_OK;
     if ((bytes & 3) == 0) {
@@ -2724,6 +2778,13 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     return FB_OK;
 }
 
+int fb_set_round_hint(fb_ctx *c, int32_t max_free) {
+    if (!c) return FB_EINVAL;
+    if (c->launched) return fail(c, FB_ESTATE, "fb_set_round_hint between ticks only");
+    c->maxc_hint = std::max<int32_t>(1, max_free);
+    return FB_OK;
+}
+
 int fb_set_path(fb_ctx *c, const char *name, int value) {
     if (!c || !name) return FB_EINVAL;
     if (c->launched) return fail(c, FB_ESTATE, "fb_set_path between ticks only");
@@ -2734,6 +2795,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "split_slots" && value >= -1 && value <= 1) c->split_slots = value;
     else if (n == "ev_ll" && (value == 0 || value == 1)) c->ev_ll = value;
     else if (n == "rs_wide" && (value == 0 || value == 1)) c->rs_wide = value;
+    else if (n == "fault_qlen") c->fault_qlen = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }

@@ -90,20 +90,6 @@ constexpr int kWinMaxCh = 4096;
 constexpr int32_t kTomb = INT32_MIN;  // qfree of a window position whose slot left the queue
 // st bit: the slot was in the committed queue at tick start (window commits)
 constexpr uint8_t kStQ0 = 8;
-// Per-slot in-flight slabs (large one-GPU heartbeat contexts): the log
-// sequences of a slot's in-flight entries in kSlab slots with an occupancy mask, so a
-// window tick finds a dead worker's orphans without scanning the log.  sidx[q]: entry
-// q's index in its slot's slab (kNoSidx: not in one); a slot whose entries outgrow its
-// slab is flagged (sovf) and its death sends the tick to the general path (k_logscan).
-constexpr int kSlab = 64;
-constexpr uint8_t kNoSidx = 0xff;
-struct Slabs {
-    int32_t *slab;             // [W][kSlab]
-    unsigned long long *mask;  // [W]
-    uint8_t *sidx;             // [log capacity]
-    uint8_t *ovf;              // [W]
-};
-
 // Committed per-slot heartbeat: last_heartbeat, NaN when the slot holds no record
 // (so the log scan's one 8-byte gather per in-flight entry decides liveness
 // without a registered flag); the first log sequence of the current registration
@@ -199,7 +185,6 @@ struct CommitArgs {
     // results; nbap blocks walk the appended positions grid-stride
     const int64_t *eager;      // the tick's commit word (TickArgs::cw)
     int64_t cw_tag;            // its launch's link stamp: cw[0] == cw_tag means the tick failed
-    Slabs sl;                  // (slab contexts) a slot whose registration died gets an empty slab
 };
 
 struct EvArgs {
@@ -278,14 +263,6 @@ struct EvArgs {
     uint32_t *wticket;
     int64_t *cw;                // commit word {failed: link stamp, window head, window length} (null: none)
     unsigned long long *dbg;    // diagnostic stamps (FAASBAL_STAMPS builds; null until the first tick allocated them)
-    // slab contexts: k_ev_link appends the log entries [ap_from, ap_to) to their slots'
-    // slabs (idempotently: a relaunch appends nothing twice) over ap_blocks extra blocks,
-    // and zeroes the nbf orphan tile counts and the two counters of k_emit_win's orphan
-    // role; k_ev_apply_ll takes an entry its result completes out of its slot's slab
-    Slabs sl;
-    int64_t ap_from, ap_to;
-    int ap_blocks, nbf_zero;
-    uint32_t *fcnt, *orc;
 };
 
 // one argument block for k_scan / k_plan / k_emit
@@ -391,13 +368,6 @@ struct TickArgs {
     int32_t *tomb;               // per back / front list entry: the committed position of a queued slot
                                  // it moved (-1: none), 2 E entries
     int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
-    // slab window ticks (no k_logscan): k_emit_win's first nor workgroups (by ticket) find the
-    // orphans of the slots that died (dmask) in their slabs, write them into the per-tile
-    // segments (unsorted inside a tile; the readback sorts) and count them into orc[0], then
-    // orc[1] += 1; the chunks wait for orc[1] == nor before they need O
-    Slabs sl;
-    int nor;
-    uint32_t *orc;
 
     // the previous tick's commit folded into this k_scan (one-GPU heartbeat contexts, an
     // idle tick after an idle tick): the W role deletes the records that tick evicted
@@ -512,8 +482,8 @@ struct CopyMulti {
     int otiles;
 };
 void launch_copy_multi(const CopyMulti &m, Stream st);
-// the dense orphan list from per-tile segments (dst may be host-mapped memory); each
-// segment's entries sorted ascending on the way (slab window ticks leave them unsorted)
+// the dense orphan list from per-tile segments (dst may be host-mapped memory): the
+// segments concatenated in tile order (each is ascending already, so the list is)
 void launch_orph_gather(int64_t *dst, const int64_t *src, const uint32_t *cnt, int ntile, Stream st);
 
 }  // namespace fb

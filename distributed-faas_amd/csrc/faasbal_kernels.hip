@@ -1742,14 +1742,19 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 __shared__ int xlast;
                 const int g = b / kXGroupBlocks;
                 const int nbg = min(kXGroupBlocks, a.nbq - g * kXGroupBlocks);
-                // (no fence: the adds are device-scope atomics, performed at the coherence
-                // point before each wave's vmcnt wait; the ticket comes after every wave's wait,
-                // and the last block reads the sums with atomics at that same point)
+                // the adds are device-scope atomics, performed at the coherence point before
+                // each wave's vmcnt wait; the ticket is an agent-scope acq_rel RMW after every
+                // wave's wait (the memory model's release / acquire pair, not just the
+                // hardware's ordering), and the last block reads the sums with atomics
                 uint32_t *acc = a.xg_acc + (size_t)g * kXgAccStride;
                 if (t <= R && n) atomicAdd(&acc[t], n);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
                 __syncthreads();
-                if (t == 0) xlast = atomicAdd(&a.xg_tk[g], 1u) == (uint32_t)(nbg - 1) ? 1 : 0;
+                if (t == 0)
+                    xlast = __hip_atomic_fetch_add(&a.xg_tk[g], 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                                    (uint32_t)(nbg - 1)
+                                ? 1
+                                : 0;
                 __syncthreads();
                 if (xlast) {
                     uint8_t *const gr = a.xgrows + (size_t)g * xg_row(R);

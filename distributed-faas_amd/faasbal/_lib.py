@@ -26,7 +26,8 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_tick_continue", "fb_create_deque", "fb_tick_stage", "fb_tick_launch_staged", "fb_host_alloc",
            "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign", "fb_get_outputs",
            "fb_read_inflight", "fb_set_compact", "fb_get_outputs_compact", "fb_expand_compact",
-           "fb_set_window", "fb_window_stats", "fb_set_compact_out", "fb_set_eager_commit", "fb_set_path")
+           "fb_set_window", "fb_window_stats", "fb_set_compact_out", "fb_set_eager_commit", "fb_set_path",
+           "fb_set_round_hint")
 
 
 class TickResult(C.Structure):
@@ -130,6 +131,7 @@ def load(path=None):
         "fb_get_outputs_compact": (C.c_int, [_P, _P, _P, i64, C.POINTER(i64), _P, _P]),
         "fb_expand_compact": (C.c_int, [_P, _P, _P, i64, _P]),
         "fb_set_path": (C.c_int, [_P, C.c_char_p, C.c_int]),
+        "fb_set_round_hint": (C.c_int, [_P, C.c_int32]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name, None)

@@ -305,7 +305,9 @@ class GpuPushDispatcher:
                 seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
         # a one-GPU balancer hands the tick's assignments / orphans / evicted slots back in one
         # readback into pinned arrays, consumed below before the next tick
-        tkw = {"pinned": True} if isinstance(self.balancer, GpuBalancer) else {}
+        # (exactly a GpuBalancer: a ShardedBalancer subclass has no pinned path; shard groups
+        # are the sharded route)
+        tkw = {"pinned": True} if type(self.balancer) is GpuBalancer else {}
         try:
             out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
                                      n_pending=len(self.pending), **tkw)

@@ -85,6 +85,11 @@ class ShardedBalancer(GpuBalancer):
         self._chk(self.lib.fb_load_shard(self.h, sh["base"], sh["n"], _p(sh["reg"]), _p(sh["free"]), _p(sh["hb"]),
                                          _p(sh["epoch"]), _p(sh["queue"]), len(sh["queue"]), _p(sh["log_slot"]),
                                          _p(sh["log_seq"]), len(sh["log_slot"]), sh["log_head"]))
+        # the round table of the first tick from the GLOBAL max free count (every rank
+        # computes it from the same global state, so the exchange layouts agree)
+        q = np.asarray(st["queue"], np.int64)
+        mf = int(np.asarray(st["free"])[q].max()) if len(q) else 1
+        self._chk(self.lib.fb_set_round_hint(self.h, max(1, min(mf, 1 << 30))))
         self.n_workers = sh["n"]
 
     def read_state(self, with_log=True):

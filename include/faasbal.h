@@ -315,6 +315,13 @@ int fb_load_shard(fb_ctx *ctx, int32_t slot_base, int32_t n_workers, const uint8
                   const int32_t *queue, int64_t queue_len, const int32_t *log_slot, const uint32_t *log_seq,
                   int64_t log_len, int64_t log_head);
 int fb_read_shard_log(fb_ctx *ctx, uint32_t *log_seq, int64_t *log_len, int64_t *log_head);
+/* Between ticks: the largest free count any queued worker of the loaded state has (the
+ * GLOBAL maximum, the same on every rank), which sizes the next tick's round table.
+ * A sharded context cannot take it from its own shard: the exchange layout depends on
+ * the table, so every rank must agree.  Without it the first tick after fb_load_shard
+ * starts narrow and a wider fill level costs one FB_ERERUN relaunch.  Replaces nothing in
+ * the reference (it sizes a buffer, task_dispatcher.py:393-419 has none). */
+int fb_set_round_hint(fb_ctx *ctx, int32_t max_free);
 /* Exchange buffer size for a tick of n_events events (n_events < 0: the maximum). */
 int fb_exchange_bytes(fb_ctx *ctx, int32_t n_events, int64_t *bytes);
 /* Device buffer (same size on every rank) the ranks all-reduce between phases. */

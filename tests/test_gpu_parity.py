@@ -353,6 +353,28 @@ def test_log_full_is_an_error():
         g.tick(1000.0, 10.0, n_pending=5000)
 
 
+@pytest.mark.parametrize("window", [0, 1])
+def test_device_reported_lengths_are_validated(window):
+    """fb_tick_wait checks every device-reported length against its buffer before any
+    copy uses it: a queue length past the buffer (injected into the results) fails the
+    tick with FB_EHIP naming the number; the tick is not committed and the next one runs
+    against the oracle as if it never happened."""
+    st = synth.zipf_state(W=2048, seed=3)
+    g, o = _pair(st, len(st["log"]) * 2 + 100_000)
+    g.set_window(window)
+    args = (1000.0, 10.0, [], [], [], [], [], 500)   # fill level 0: the next tick may be a window tick
+    a, b = g.tick(*args), o.tick(*args)
+    _cmp_out(a, b, 0)
+    g.set_path("fault_qlen", 1 << 40)
+    args = (1001.0, 10.0, [synth.EV_HEARTBEAT], [5], [0], [1000.5], [-1], 300)
+    with pytest.raises(FaasbalError, match="queue length|window"):
+        g.tick(*args)
+    a, b = g.tick(*args), o.tick(*args)
+    _cmp_out(a, b, 1)
+    _cmp_state(g, o, 1)
+    assert g.window_stats()[0] == window
+
+
 def test_invalid_events_rejected():
     st = synth.uniform_state(W=10, seed=1)
     g = GpuBalancer(10, 1000)

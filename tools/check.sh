@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-4 check pass on one box: the GPU suite (per-test timeout), smoke, the default bench
+# Check pass on one box: the GPU suite (per-test timeout), smoke, the default bench
 # line.  Each step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out

@@ -4,7 +4,7 @@ rank of the N-GPU bench computes per tick, minus the all-reduce.  strong (defaul
 bench.py --gpus N): the configs[2] table of 64K workers / 1M tasks split N ways;
 weak: N x 64K workers / N x 1M tasks.  Reports rank 0 and the slowest rank.
 
-    python tools/shard_probe.py [--world 2 4 8 --reps 50 --scaling strong]
+    python tools/shard_probe.py [--world 2 4 8 --reps 50 --scaling strong --workload tick|cfg3]
 """
 import argparse
 import os
@@ -25,10 +25,13 @@ def main():
     ap.add_argument("--world", type=int, nargs="+", default=[2, 4, 8])
     ap.add_argument("--reps", type=int, default=50)
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"))
+    ap.add_argument("--workload", default="tick", choices=("tick", "cfg3"),
+                    help="tick: configs[2] (64K workers, 1M tasks); cfg3: configs[3] (1M workers, 16M tasks)")
     args = ap.parse_args()
     for world in args.world:
         k = world if args.scaling == "weak" else 1
-        W, T = 65536 * k, 1_000_000 * k
+        W0, T0 = (1 << 20, 16_000_000) if args.workload == "cfg3" else (65536, 1_000_000)
+        W, T = W0 * k, T0 * k
         st = synth.zipf_state(W=W, seed=0)
         F = len(st["log"])
         bals = [ShardedBalancer(r, world, W, 2 * F // world + T + 16, max_events=1) for r in range(world)]
@@ -63,8 +66,8 @@ def main():
             kt = b.timing_read()
             pers.append({k: round(ms / args.reps * 1e3, 2) for k, (ms, n) in kt.items()})
         slow = max(range(world), key=lambda r: sum(pers[r].values()))
-        print("%s world %d: rank-0 device us per tick %s (sum %.1f); slowest rank %d: sum %.1f; exchange %d B, "
-              "serial wall %.0f us" % (args.scaling, world, pers[0], sum(pers[0].values()), slow,
+        print("%s %s world %d: rank-0 device us per tick %s (sum %.1f); slowest rank %d: sum %.1f; exchange %d B, "
+              "serial wall %.0f us" % (args.workload, args.scaling, world, pers[0], sum(pers[0].values()), slow,
                                        sum(pers[slow].values()), bals[0].exchange().numel(), dt * 1e6), flush=True)
         for b in bals:
             b.timing_enable(False)
