@@ -269,7 +269,11 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
     g.sync()
     barrier()
     dt = time.perf_counter() - t0
+    B_ticks = 0  # SURVEY.md 8(d) bytes of the timed ticks (the log pass only on ticks with a death)
     for i, r in zip(range(Wu, Wu + K), rs):
+        Ni, Oi = int(r["n_assigned"]), int(r["n_orphans"])
+        Fi = int(r["log_head"]) - Ni if (Oi or int(r["n_evicted"])) else 0
+        B_ticks += tick_bytes(W // world, 0, Fi // world, Oi, Ni, len(ticks[i]["ev_kind"]))
         stats["assigned"] += int(r["n_assigned"])
         stats["orphans"] += int(r["n_orphans"])
         stats["evicted"] += int(r["n_evicted"])  # sharded: this rank's evictions (summed below)
@@ -304,7 +308,8 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
                                % (W, "" if world == 1 else " sharded by worker-id range over %d GPUs" % world, T, T,
                                   0 if args.stream_quiet else max(1, W // 1000), max(1, int(args.hb_frac * W)),
                                   "a clock that ages nobody (no churn)" if args.stream_quiet else "10 ms per tick"),
-                   "workers": W, "events_per_tick": stats["events"] / K, "assigned_per_tick": stats["assigned"] / K,
+                   "workers": W, "tasks_per_tick": T, "events_per_tick": stats["events"] / K,
+                   "assigned_per_tick": stats["assigned"] / K,
                    "events_in": {"hbm": "HBM-resident (every tick's batch copied to the GPU before the timed "
                                          "region; read in place, checked by the tick's first kernel)",
                                   "pinned": "pinned host memory (H2D copies inside the timed region)",
@@ -314,6 +319,30 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
         "tick": {"device_us_per_tick": sum(per_tick.values()), "kernels_us_per_tick": per_tick,
                  "kernels_us_per_launch": kern},
     }
+    # roofline: the dominant kernel's share of SURVEY.md 8(d)'s tick bytes (one GPU: the apply
+    # launch carries the slot purge, 24 B per worker, and the messages, 17 B each) over its
+    # event-timed launch average; tick_frac: the whole tick's 8(d) bytes on the driver's clock
+    dom = max(kern, key=lambda k: kern[k])
+    Eavg = stats["events"] / K
+    dom_bytes = (24 * W // world + 17 * Eavg) if dom == "ev_apply" else None
+    traffic, traffic_src = None, None
+    tp = os.path.join(REPO, "profiles", "traffic.json")
+    if os.path.exists(tp):
+        tj = json.load(open(tp)).get("entries", {}).get("stream,%d,%d,%d" % (W, T, world))
+        if tj and dom in tj["kernels"]:
+            traffic = tj["kernels"][dom]["hbm_bytes"]
+            traffic_src = ("profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch, separate rocprofv3 --pmc "
+                           "passes; the x2 FETCH_SIZE correction is calibrated for streaming reads, so for random "
+                           "gathers it is an upper bound)" % tj["tag"])
+    ach = dom_bytes / (kern[dom] * 1e-6) / 1e9 if dom_bytes else None
+    line["roofline"] = {"bound": "hbm", "kernel": dom, "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": ach / HBM_PEAK_GBS if ach else None, "traffic": traffic, "traffic_source": traffic_src,
+                        "algorithmic_bytes": dom_bytes,
+                        "bytes_model": "SURVEY.md 8(d) share: 24 W (the purge's 16 B read + 8 B write per worker) "
+                                       "+ 17 E (messages)",
+                        "kernel_avg_ms": kern[dom] * 1e-3,
+                        "tick_bytes": B_ticks / K,
+                        "tick_frac": B_ticks / dt / 1e9 / HBM_PEAK_GBS}
     if pcie is not None:
         line["pcie_inclusive"] = pcie
     if world == 1:

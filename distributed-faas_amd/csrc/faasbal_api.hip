@@ -287,6 +287,7 @@ struct fb_ctx {
     uint32_t *lseq = nullptr;                         // global sequence of each local log entry
     uint32_t *ocnt = nullptr, *osegcnt = nullptr;
     uint32_t *xg_acc = nullptr, *xg_tk = nullptr, *ogrp = nullptr;  // exchanged group rows (phase 1 -> 2)
+    uint32_t *xs_tk = nullptr;                        // k_xscan's ticket
     int64_t *opre = nullptr, *oA = nullptr;
     uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
     int64_t xcap = 0;
@@ -485,20 +486,25 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
 struct XLayout {
     size_t rec, front, back, evs, c8, rows, grows, total;
 };
-// Exchanged block rows for a tick of this shape (0: phase 2 re-counts the c values):
-// <= 16 ranks, a table of <= kRFused rows, <= kXRowsMaxBlocks queue blocks
+// Exchanged block rows for a tick of this shape: 0 none (phase 2 re-counts the c values:
+// > 16 ranks or a table wider than kRFused rows); 1 a one-launch phase 2 that sums the rows
+// itself (<= kXRowsMaxBlocks queue blocks); 2 the same rows for larger queues, their columns
+// scanned by k_plan before k_emit_shard (configs[3]: 3.5 K blocks)
+inline int xrows_mode(int world, int R, int64_t Qlog) {
+    const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
+    if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused) return 0;
+    // (the one-launch phase 2 walks the digit rows and this rank's rows in the same rounds:
+    // their parts per column must agree, as they do for the 32 / 64 / 128-row tables)
+    if (nbq <= kXRowsMaxBlocks && xr_parts(R) == kBS / (R / 4)) return 1;
+    return (nbq > kXRowsMaxBlocks && R == kXGroupR) ? 2 : 0;  // (k_xscan decodes 32-round rows)
+}
 inline size_t xrows_bytes(int world, int R, int64_t Qlog) {
     const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
-    // (phase 2 walks the digit rows and this rank's rows in the same rounds: their parts per
-    // column must agree, as they do for the 32 / 64 / 128-row tables)
-    if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused || nbq > kXRowsMaxBlocks ||
-        xr_parts(R) != kBS / (R / 4))
-        return 0;
-    return (size_t)nbq * xr_row(R);
+    return xrows_mode(world, R, Qlog) ? (size_t)nbq * xr_row(R) : 0;
 }
-// ... and the group rows (R = kXGroupR only)
+// ... and the group rows (one-launch form, R = kXGroupR only)
 inline size_t xgrows_bytes(int world, int R, int64_t Qlog) {
-    if (R != kXGroupR || !xrows_bytes(world, R, Qlog)) return 0;
+    if (R != kXGroupR || xrows_mode(world, R, Qlog) != 1) return 0;
     const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
     return (size_t)cdiv(nbq, kXGroupBlocks) * xg_row(R);
 }
@@ -1055,6 +1061,15 @@ int enqueue_tick(fb_ctx *c) {
         const size_t xrw = (size_t)c->world * kXRecWords;
         a.xrec = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)c->xpar * xrw;
         a.xrows = xrb ? c->xbuf + xl.rows : nullptr;
+        a.xplan = (xrb && xrows_mode(c->world, R, Qlog) == 2) ? 1 : 0;
+        if (a.xplan) {
+            // k_xscan's outputs in the plan tables (unused on this path): per-block prefixes in
+            // qpre's words, the chunk prefixes and totals in opre's
+            a.xpre = reinterpret_cast<uint32_t *>(c->qpre);
+            a.xct = reinterpret_cast<uint32_t *>(c->opre);
+            a.xA = a.xct + (size_t)cdiv(nbq, kBS) * 2 * R;
+            a.xtk = c->xs_tk;
+        }
         a.xgrows = xgb ? c->xbuf + xl.grows : nullptr;
         a.xg_acc = c->xg_acc;
         a.xg_tk = c->xg_tk;
@@ -1150,7 +1165,12 @@ int enqueue_tick(fb_ctx *c) {
         if (R > kShardMaxR) return fail(c, FB_ERANGE, "sharded tick: round table of %d rows (limit %d)", R, kShardMaxR);
         if (a.xrows) {
             // exchanged block rows: k_emit_shard alone (it also zeroes the other records copy,
-            // which the next tick's phase 1 writes)
+            // which the next tick's phase 1 writes); large queues: k_plan's column scans of the
+            // rows first
+            if (a.xplan) {
+                Timer t(c, "plan");
+                launch_xscan(a, t.st());
+            }
             Timer t(c, "emit");
             launch_emit_shard(a, t.st());
             HIPCHK(c, hipGetLastError());
@@ -1377,6 +1397,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
         const size_t ng = (size_t)kXRowsMaxBlocks / kXGroupBlocks;
         ap.add(&c->xg_acc, ng * kXgAccStride);
         ap.add(&c->xg_tk, ng);
+        ap.add(&c->xs_tk, (size_t)64);  // k_xscan's ticket (zero: the arena is zeroed, the last workgroup resets it)
         ap.add(&c->ogrp, ng * kXGroupR);
     }
     int rc = arena_commit(c, ap);
@@ -1772,11 +1793,15 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
     // whichever is larger; a launched tick: its own width and rows
     const int64_t Qlog = Qn + 2 * E;
     if (n_events < 0) {
-        // the wide form at the largest queue, or a queue of at most kXRowsMaxBlocks blocks
-        // with a 128-row table's block rows (a 32-row table's block + group rows are smaller)
+        // the largest of: the wide form at the largest queue; a queue of at most
+        // kXRowsMaxBlocks blocks with a 128-row table's block rows (the one-launch form; a
+        // 32-row table's block + group rows are smaller); the largest queue with a 32-row
+        // table's block rows (the k_xscan form)
         const int64_t Qr = std::min<int64_t>(Qlog, (int64_t)kXRowsMaxBlocks * kBS);
-        *bytes = (int64_t)std::max(xlayout(c->world, E, Qlog, 2).total,
-                                   xlayout(c->world, E, Qr, 1, xrows_bytes(c->world, kRFused, Qr)).total);
+        *bytes = (int64_t)std::max({xlayout(c->world, E, Qlog, 2).total,
+                                    xlayout(c->world, E, Qr, 1, xrows_bytes(c->world, kRFused, Qr)).total,
+                                    xlayout(c->world, E, Qlog, 1, xrows_bytes(c->world, kXGroupR, Qlog),
+                                            xgrows_bytes(c->world, kXGroupR, Qlog)).total});
     } else {
         const int R = c->launched ? c->l_R : kRFused;
         *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xrows_bytes(c->world, R, Qlog),

@@ -404,6 +404,13 @@ struct TickArgs {
                                    // (two copies by launch parity: phase 2 zeroes the next tick's)
     uint8_t *xrows;                // exchanged block rows (kXRowsMaxBlocks; null: phase 2 re-counts the c values)
     uint8_t *xgrows;               // exchanged group rows (R = kXGroupR; null: phase 2 sums the block rows)
+    int xplan;                     // large queues (> kXRowsMaxBlocks blocks, R = kXGroupR): phase 2 is k_xscan's
+                                   // prefix scans of the exchanged digit rows / own rows, then k_emit_shard
+    uint32_t *xpre;                // k_xscan: [block][2R] exclusive prefixes inside the block's 256-block chunk
+                                   // (rounds of all positions, then this rank's)
+    uint32_t *xct;                 // [chunk][2R] chunk totals, turned into exclusive prefixes over the chunks
+    uint32_t *xA;                  // [2R] totals A(r) (all, then this rank's)
+    uint32_t *xtk;                 // k_xscan's ticket (zero between launches)
     uint32_t *xg_acc, *xg_tk;      // phase 1: per group the running sums and the ticket (zero between ticks)
     uint32_t *ogrp;                // phase 1 -> 2: this rank's group rows [group][R]
     unsigned long long *xz;        // phase 2: the other launch parity's exchange records, zeroed for the next tick
@@ -455,6 +462,7 @@ void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
 void launch_logscan(const TickArgs &a, int grid, Stream st);
 void launch_plan(const TickArgs &a, Stream st);
+void launch_xscan(const TickArgs &a, Stream st);
 void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);
 void launch_emit_shard(const TickArgs &a, Stream st);

@@ -252,9 +252,18 @@ __device__ __forceinline__ T block_reduce_max(T v, T *lds4) {
 // entries and issues its loads 16 at a time, so the whole array costs one block
 // scan instead of one per 256 entries.  In place (pre == cnt) is allowed: a
 // thread reloads a group of its own run before storing into it.
+template <typename TO, typename LD>
+__device__ __forceinline__ unsigned long long run_excl_scan_ld(const LD &ld, int n, TO *pre, size_t ps,
+                                                               unsigned long long *l4);
 template <typename TO>
 __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt, size_t cs, int n, TO *pre,
                                                             size_t ps, unsigned long long *l4) {
+    return run_excl_scan_ld<TO>([=](int i) -> uint32_t { return cnt[(size_t)i * cs]; }, n, pre, ps, l4);
+}
+// the exclusive scan of n counts ld(0 .. n-1) into pre[i * ps] (one workgroup); returns the total
+template <typename TO, typename LD>
+__device__ __forceinline__ unsigned long long run_excl_scan_ld(const LD &ld, int n, TO *pre, size_t ps,
+                                                               unsigned long long *l4) {
     const int per = (n + kBS - 1) / kBS;
     const int i0 = (int)threadIdx.x * per;
     unsigned long long sum = 0;
@@ -265,7 +274,7 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int i = min(i0 + j, n - 1);
-            v[j] = cnt[(size_t)i * cs];
+            v[j] = ld(i);
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -289,7 +298,7 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int i = min(i0 + j0 + j, n - 1);
-            v[j] = cnt[(size_t)i * cs];
+            v[j] = ld(i);
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) sum += (j0 + j < per && i0 + j0 + j < n) ? v[j] : 0u;
@@ -301,7 +310,7 @@ __device__ __forceinline__ unsigned long long run_excl_scan(const uint32_t *cnt,
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
             const int i = min(i0 + j0 + j, n - 1);
-            v[j] = cnt[(size_t)i * cs];
+            v[j] = ld(i);
         }
 #pragma unroll
         for (int j = 0; j < 16; ++j) {
@@ -2168,6 +2177,99 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
     STAMP(a, SO, 15);
 }
 
+// ------------------------------------------------------------ k_xscan (sharded phase 2, large queues)
+// The per-block prefixes of the exchanged round counts (xrows_mode 2: > kXRowsMaxBlocks
+// queue blocks, R = kXGroupR): one workgroup per chunk of 256 queue blocks, thread t the
+// rows of block 256 ch + t -- every rank's counts from the 4-bit digit row (7 x 16 B) and
+// this rank's own row (8 x 16 B), both coalesced across the wave --, decoded into LDS as a
+// [block][2R] matrix; each wave scans columns (4 rows per lane), the chunk-local exclusive
+// prefixes go out row-major (coalesced), the chunk totals into xct.  The last workgroup (an
+// agent-scope acq_rel ticket) turns the chunk totals into exclusive prefixes over the chunks
+// and writes the totals A(r).  k_plan's one workgroup per column walked 3.5 K rows with a
+// 64-line gather per wave load (13-17 us at configs[3]).
+template <int R>
+__global__ __launch_bounds__(kBS) void k_xscan(TickArgs a) {
+    prefetch_args(a);
+    const int SO = 3 * (a.nbw + a.nbf + a.nbq) + 6000;  // diagnostic stamp rows (stamps builds)
+    STAMP(a, SO, 0);
+    constexpr int C = 2 * R, LD = C + 1, XS = xr_stride(R), NQ = xr_row(R) / 16, NO = R / 4;
+    __shared__ uint32_t xl[kBS * LD];
+    __shared__ int last;
+    const int ch = blockIdx.x, t = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int b = ch * kBS + t;
+    const bool in = b < a.nbq;
+    const int bc = in ? b : a.nbq - 1;
+    uint4 d[NQ], o[NO];
+    const uint4 *dr = reinterpret_cast<const uint4 *>(a.xrows + (size_t)bc * xr_row(R));
+    const uint4 *orw = reinterpret_cast<const uint4 *>(a.ocnt + (size_t)bc * R);
+#pragma unroll
+    for (int k = 0; k < NQ; ++k) d[k] = dr[k];
+#pragma unroll
+    for (int k = 0; k < NO; ++k) o[k] = orw[k];
+    STAMPW(a, SO, 1);
+    // (constant byte / word indices once unrolled: register extracts)
+    auto word = [](const uint4 &v, int i) -> uint32_t { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; };
+    auto byte = [&](int k) -> uint32_t { return (word(d[k >> 4], (k >> 2) & 3) >> (8 * (k & 3))) & 0xffu; };
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        xl[t * LD + r] = in ? byte(r) + (byte(XS + r) << 4) + (byte(2 * XS + r) << 8) : 0u;
+        xl[t * LD + R + r] = in ? word(o[r >> 2], r & 3) : 0u;
+    }
+    __syncthreads();
+    STAMP(a, SO, 2);
+    // columns: wave w takes w, w + 4, ...; lane l rows 4 l .. 4 l + 3
+    for (int col = w; col < C; col += kWaves) {
+        uint32_t v[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = xl[(4 * lane + j) * LD + col];
+        const uint32_t sm = v[0] + v[1] + v[2] + v[3];
+        const uint32_t inc = wave_incl_scan_u32(sm);
+        uint32_t ex = inc - sm;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            xl[(4 * lane + j) * LD + col] = ex;
+            ex += v[j];
+        }
+        if (lane == 63) a.xct[(size_t)ch * C + col] = inc;
+    }
+    __syncthreads();
+    STAMP(a, SO, 3);
+    const int nrow = min(kBS, a.nbq - ch * kBS);
+    uint32_t *const dst = a.xpre + (size_t)ch * kBS * C;
+    for (int e = t; e < nrow * C; e += kBS) dst[e] = xl[(e / C) * LD + e % C];
+    // every wave's chunk-total stores done, then the ticket (release / acquire at agent scope)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    STAMP(a, SO, 4);
+    if (t == 0) last = __hip_atomic_fetch_add(a.xtk, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT) ==
+                           (uint32_t)(gridDim.x - 1);
+    __syncthreads();
+    STAMP(a, SO, 5);
+    if (!last) {
+        STAMP(a, SO, 15);
+        return;
+    }
+    if (t < C) {
+        // 16 chunks' totals per pass, all loads in flight before the running sum (a load per
+        // iteration behind the previous store costs a memory round trip per chunk)
+        uint32_t run = 0;
+        const int nch = (int)gridDim.x;
+        for (int c0 = 0; c0 < nch; c0 += 16) {
+            uint32_t v[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) v[j] = a.xct[(size_t)min(c0 + j, nch - 1) * C + t];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                if (c0 + j < nch) a.xct[(size_t)(c0 + j) * C + t] = run;
+                run += c0 + j < nch ? v[j] : 0u;
+            }
+        }
+        a.xA[t] = run;
+    }
+    if (t == 0) *a.xtk = 0u;
+    STAMP(a, SO, 15);
+}
+
 // ------------------------------------------------------------ k_plan2 (large grids, R <= 128)
 // k_plan for k_emit2 when k_scan's queue blocks also added their counts into
 // group rows (<= 64 groups of 2^gshift blocks): one workgroup per group reads
@@ -3415,14 +3517,18 @@ constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // as digit rows (phase 1, a.xrows), this rank's in its own rows (ocnt); each block sums the
 // rows of all blocks (totals) and of the blocks before it (prefix), and counts its waves'
 // rounds itself; max c and the capacity follow from the totals.
-template <bool GRP, bool XR>
+// XP (large queues, a.xplan): the block rows arrived in the exchange as with XR, but k_plan
+// scanned their columns (every rank's digits, this rank's own rows) into per-block prefixes
+// and totals first; each block reads its own prefix row and counts its waves' rounds itself
+// (no phase-2 k_scan, no segment counts).
+template <bool GRP, bool XR, bool XP = false>
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     prefetch_args(a);
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows (stamps builds)
     STAMP(a, SO, 0);
-    if (XR) {  // the other parity's exchange records, for the next tick's phase 1
+    if (XR || XP) {  // the other parity's exchange records, for the next tick's phase 1
         for (int i = bid * kBS + (int)threadIdx.x; i < a.xz_words; i += (int)gridDim.x * kBS) a.xz[i] = 0ull;
     } else if (GRP) {  // the other parity's group rows, for the next launch's k_scan atomics
         for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
@@ -3747,6 +3853,87 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             maxc = (int)max(max(smx[0], smx[1]), max(smx[2], smx[3]));
             cap = (int64_t)scap[0] + scap[1] + scap[2] + scap[3];
             O = (int64_t)sorf[0] + sorf[1] + sorf[2] + sorf[3];
+        } else if (XP) {
+            // k_xscan's totals, this block's chunk-local prefixes and its chunk's prefix (lanes
+            // r < R of chunk 0: R = kXGroupR), every rank's orphans and max c from the records
+            const int ch = b / kBS;
+            const int rr = min(lane, R - 1);
+            const uint32_t A0 = a.xA[rr], oA0 = a.xA[R + rr];
+            const uint32_t p0 = a.xpre[(size_t)b * 2 * R + rr], op0 = a.xpre[(size_t)b * 2 * R + R + rr];
+            const uint32_t c0 = a.xct[(size_t)ch * 2 * R + rr], oc0 = a.xct[(size_t)ch * 2 * R + R + rr];
+            const int gx = (int)threadIdx.x < a.world * kXRecLines ? (int)threadIdx.x : 0;
+            const unsigned long long xo = a.xrec[(size_t)gx * 16], xm = a.xrec[(size_t)gx * 16 + 1];
+#pragma unroll
+            for (int k = 0; k < kRCh; ++k) {
+                Av[k] = k == 0 ? A0 : 0u;
+                oAv[k] = k == 0 ? oA0 : 0u;
+                pv[k] = k == 0 ? p0 + c0 : 0u;
+                opv[k] = k == 0 ? op0 + oc0 : 0u;
+            }
+            __shared__ uint32_t xred[kWaves][2];
+            {
+                const bool rin = (int)threadIdx.x < a.world * kXRecLines;
+                const uint32_t orf = wave_sum_u32(rin ? (uint32_t)xo : 0u), mxr = wave_max_u32(rin ? (uint32_t)xm : 0u);
+                if (lane == 0) {
+                    xred[w][0] = orf;
+                    xred[w][1] = mxr;
+                }
+            }
+            STAMPW(a, SO, 1);
+            {
+                // the capacity sum_r<R A(r) (= sum of c when max c <= R), and this wave's rounds
+                // (all / own lanes) from histograms of min(c, R): the in-block bases of the
+                // later waves
+                __shared__ uint32_t swc[kWaves][kRFused + 1], sowc[kWaves][kRFused + 1];
+                uint32_t cp = 0;
+#pragma unroll
+                for (int k = 0; k < kRCh; ++k) cp += (64 * k + lane < R) ? (uint32_t)Av[k] : 0u;
+                cap = (int64_t)wave_sum_u32(cp);
+                const int cw_ = pos < a.Qlog ? cq : 0;
+                const int ocw = (cw_ > 0 && sq >= 0 && own_slot(a, sq) >= 0) ? cw_ : 0;
+                uint32_t *ha = swc[w], *ho = sowc[w];
+                for (int i = lane; i <= R; i += 64) {
+                    ha[i] = 0;
+                    ho[i] = 0;
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                atomicAdd(&ha[cw_ < R ? cw_ : R], 1u);
+                atomicAdd(&ho[ocw < R ? ocw : R], 1u);
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                __builtin_amdgcn_wave_barrier();
+                uint32_t ca = 0, co = 0;
+#pragma unroll
+                for (int k = 0; k < 2; ++k) {  // count(c > r) = 64 - #(lanes with min(c, R) <= r)
+                    const int r = 64 * k + lane;
+                    const uint32_t hv = r < R ? ha[r] : 0u, hw = r < R ? ho[r] : 0u;
+                    const uint32_t Pa = ca + wave_incl_scan_u32(hv), Po = co + wave_incl_scan_u32(hw);
+                    ca = (uint32_t)__builtin_amdgcn_readlane((int)Pa, 63);
+                    co = (uint32_t)__builtin_amdgcn_readlane((int)Po, 63);
+                    __builtin_amdgcn_wave_barrier();
+                    if (r < R) {
+                        ha[r] = 64u - Pa;
+                        ho[r] = 64u - Po;
+                    }
+                }
+                __syncthreads();
+#pragma unroll
+                for (int k = 0; k < kRCh; ++k) {
+                    const int rr = min(64 * k + lane, R - 1);
+                    uint32_t sc = 0, osc = 0;
+#pragma unroll
+                    for (int qq = 0; qq < kWaves - 1; ++qq) {
+                        const bool in = qq < w && 64 * k + lane < R;
+                        sc += in ? swc[qq][rr] : 0u;
+                        osc += in ? sowc[qq][rr] : 0u;
+                    }
+                    segc[k] = sc;
+                    osegc[k] = osc;
+                }
+                O = (int64_t)xred[0][0] + xred[1][0] + xred[2][0] + xred[3][0];
+                maxc = (int)max(max(xred[0][1], xred[1][1]), max(xred[2][1], xred[3][1]));
+                STAMP(a, SO, 5);
+            }
         } else {
 #pragma unroll
             for (int k = 0; k < kRCh; ++k) {
@@ -3760,7 +3947,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             cap = a.P->cap_total;
             maxc = a.P->maxc;
         }
-        if (!XR) {
+        if (!XR && !XP) {
             uint32_t sv[kRCh][kWaves - 1], osv[kRCh][kWaves - 1];
 #pragma unroll
             for (int k = 0; k < kRCh; ++k)
@@ -3818,7 +4005,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         const int64_t ALv = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Av[0] : (Lc == 1 ? Av[1] : Av[2])), Ll);
         const int64_t AL = (L < maxc && L < rlim) ? ALv : 0;
         int64_t O_loc = 0, n_ev = 0;
-        if (GRP && b == 0) {
+        if ((GRP || XP) && b == 0) {
             // this rank's orphans and evictions (its phase-1 tile counts) for the host
             __shared__ uint32_t sfo[kWaves], sev[kWaves];
             uint32_t fo = 0, ev = 0;
@@ -3836,8 +4023,8 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         }
         if (b == 0 && threadIdx.x == 0) {
             a.hout->O = O;
-            a.hout->O_local = GRP ? O_loc : a.P->O_local;
-            a.hout->n_evicted = GRP ? n_ev : a.P->n_evicted;
+            a.hout->O_local = (GRP || XP) ? O_loc : a.P->O_local;
+            a.hout->n_evicted = (GRP || XP) ? n_ev : a.P->n_evicted;
             a.hout->cap_total = cap;
             a.hout->maxc = maxc;
             a.hout->L = L;
@@ -4345,6 +4532,9 @@ void launch_plan(const TickArgs &a, Stream st) {
     else
         hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
+void launch_xscan(const TickArgs &a, Stream st) {
+    hipExtLaunchKernelGGL(k_xscan<kXGroupR>, dim3((a.nbq + kBS - 1) / kBS), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+}
 void launch_emit(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
 }
@@ -4376,7 +4566,9 @@ void launch_emit_shard(const TickArgs &a, Stream st) {
         return;
     }
     const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
-    if (a.xrows)
+    if (a.xplan)
+        hipExtLaunchKernelGGL((k_emit_shard<false, false, true>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    else if (a.xrows)
         hipExtLaunchKernelGGL(k_emit_shard<true, true>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
     else if (a.grp_on)
         hipExtLaunchKernelGGL(k_emit_shard<true, false>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

@@ -365,7 +365,7 @@ def test_device_reported_lengths_are_validated(window):
     args = (1000.0, 10.0, [], [], [], [], [], 500)   # fill level 0: the next tick may be a window tick
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
-    g.set_path("fault_qlen", 1 << 40)
+    g.set_path("fault_qlen", 1 << 30)
     args = (1001.0, 10.0, [synth.EV_HEARTBEAT], [5], [0], [1000.5], [-1], 300)
     with pytest.raises(FaasbalError, match="queue length|window"):
         g.tick(*args)

@@ -60,7 +60,9 @@ def main(d, tag):
     allt = json.load(open(tp)) if os.path.exists(tp) else {}
     if "entries" not in allt:
         allt = {"entries": {}}
-    allt["entries"]["%d,%d,%d" % (traffic["workers"], traffic["tasks_per_tick"], traffic["n_gpus"])] = traffic
+    # (the streaming bench's entries carry a "stream," prefix: same workers and tasks, other kernels)
+    pre = "stream," if "events_per_tick" in cfg else ""
+    allt["entries"]["%s%d,%d,%d" % (pre, traffic["workers"], traffic["tasks_per_tick"], traffic["n_gpus"])] = traffic
     json.dump(allt, open(tp, "w"), indent=1)
     print(json.dumps(traffic, indent=1))
 

@@ -1,7 +1,8 @@
 """Diagnostic: phase stamps of k_emit_shard (exchanged block rows) for rank 0 of a
-strong-scaled configs[2] table at world N, every rank context on one GPU
-(libfaasbal_stamps.so, tools/build_all.sh).  Prints per phase the median shader
-cycles over the queue blocks:  python tools/stamps_shard.py [--world 8 --reps 30]"""
+strong-scaled configs[2] table (or configs[3]: --workload cfg3) at world N, every rank
+context on one GPU (libfaasbal_stamps.so, tools/build_all.sh).  Prints per phase the
+median shader cycles over the queue blocks and when the blocks start / end (realtime,
+from the first block's start):  python tools/stamps_shard.py [--world 8 --reps 30]"""
 import argparse
 import os
 import sys
@@ -20,8 +21,9 @@ STAMPS_SO = os.path.join(REPO, "distributed-faas_amd", "faasbal", "libfaasbal_st
 ap = argparse.ArgumentParser()
 ap.add_argument("--world", type=int, default=8)
 ap.add_argument("--reps", type=int, default=30)
+ap.add_argument("--workload", default="tick", choices=("tick", "cfg3"))
 args = ap.parse_args()
-W, T = 65536, 1_000_000
+W, T = (1 << 20, 16_000_000) if args.workload == "cfg3" else (65536, 1_000_000)
 st = synth.zipf_state(W=W, seed=0)
 F = len(st["log"])
 bals = [ShardedBalancer(r, args.world, W, 2 * F // args.world + T + 16, max_events=1, lib_path=STAMPS_SO)
@@ -53,10 +55,28 @@ d = np.stack([r[: (SO + nbq) * 16].reshape(-1, 16).astype(np.int64) for r in row
 print("world %d, rank 0: %d queue blocks (stamp rows from %d)" % (args.world, nbq, SO))
 span = (d[:, :, 14].max(axis=1) - d[:, :, 13].min(axis=1)) / 100.0
 print("queue-block span (realtime) median %.2f us" % np.median(span))
+st0 = (d[:, :, 13] - d[:, :, 13].min(axis=1, keepdims=True)) / 100.0
+en0 = (d[:, :, 14] - d[:, :, 13].min(axis=1, keepdims=True)) / 100.0
+for qq in (10, 50, 90, 100):
+    print("  block start p%d %.2f us, end p%d %.2f us" % (qq, np.median(np.percentile(st0, qq, axis=1)), qq,
+                                                      np.median(np.percentile(en0, qq, axis=1))))
 prev = 0
-for k in (1, 4, 5, 6, 15):
+for k in (1, 4, 5, 6, 15):  # (the k_plan path stamps 1 after its loads, 5 after the histograms)
     ok = (d[:, :, k] > 0) & (d[:, :, prev] > 0)
     if ok.any():
         dc = (d[:, :, k] - d[:, :, prev])[ok]
         print("  %2d -> %2d  median %6d cyc  p90 %6d" % (prev, k, np.median(dc), np.percentile(dc, 90)))
+        prev = k
+# k_xscan (large queues): its stamp rows from 3 (nbw + nbf + nbq) + 6000, one per chunk
+nch = -(-nbq // 256)
+SX = SO + 6000
+dx = np.stack([r[: (SX + nch) * 16].reshape(-1, 16).astype(np.int64) for r in rows])[:, SX:SX + nch, :]
+if (dx[:, :, 13] > 0).all():
+    t0 = dx[:, :, 13].min(axis=1, keepdims=True)
+    print("k_xscan: %d chunks; start max %.2f us, end max %.2f us (realtime)" % (
+        nch, np.median(((dx[:, :, 13] - t0) / 100.0).max(axis=1)), np.median(((dx[:, :, 14] - t0) / 100.0).max(axis=1))))
+    prev = 0
+    for k in (1, 2, 3, 4, 5, 15):
+        dc = (dx[:, :, k] - dx[:, :, prev])
+        print("  %2d -> %2d  median %6d cyc  max %6d" % (prev, k, np.median(dc), np.median(dc.max(axis=1))))
         prev = k
