@@ -288,6 +288,11 @@ struct fb_ctx {
     uint32_t *ocnt = nullptr, *osegcnt = nullptr;
     uint32_t *xg_acc = nullptr, *xg_tk = nullptr, *ogrp = nullptr;  // exchanged group rows (phase 1 -> 2)
     uint32_t *xs_tk = nullptr;                        // k_xscan's ticket
+    int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
+    int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
+    bool l_full = false;                              // ... and the last launch did
+    int32_t *assign_all = nullptr;                    // (its own allocation, grown as ticks need)
+    int64_t assign_cap = 0;
     int64_t *opre = nullptr, *oA = nullptr;
     uint8_t *xbuf = nullptr;                          // bound exchange buffer (device)
     int64_t xcap = 0;
@@ -486,10 +491,11 @@ int ensure_table(fb_ctx *c, int R, int nbq) {
 struct XLayout {
     size_t rec, front, back, evs, c8, rows, grows, total;
 };
-// Exchanged block rows for a tick of this shape: 0 none (phase 2 re-counts the c values:
-// > 16 ranks or a table wider than kRFused rows); 1 a one-launch phase 2 that sums the rows
-// itself (<= kXRowsMaxBlocks queue blocks); 2 the same rows for larger queues, their columns
-// scanned by k_plan before k_emit_shard (configs[3]: 3.5 K blocks)
+// The phase-2 form of a sharded tick of this shape: 0 phase 2 re-counts the exchanged c
+// values (k_scan) -- > 16 ranks or a table wider than kRFused rows; 1 phase 1 exchanges
+// its per-block round counts as digit rows, a one-launch phase 2 sums them (<= kXRowsMaxBlocks
+// queue blocks); 2 (xplan; larger queues, R = kXGroupR, configs[3]: 3.5 K blocks) the same
+// digit rows, whose per-block prefixes k_xscan scans before k_emit_shard
 inline int xrows_mode(int world, int R, int64_t Qlog) {
     const int64_t nbq = std::max<int64_t>(1, cdiv(Qlog, kBS));
     if (world > kXRowsMaxWorld || world * kXRecLines > kBS || R > kRFused) return 0;
@@ -702,7 +708,9 @@ int enqueue_tick(fb_ctx *c) {
     int rc;
     if ((rc = ensure_table(c, R, nbq))) return rc;
     const int cur = c->cur, nxt = 1 - cur;
-    const size_t xrb = c->shard ? xrows_bytes(c->world, R, Qlog) : 0;
+    // (fb_set_path("xplan", 0): large queues re-count in a phase-2 k_scan, no rows)
+    const bool xoff = !c->xplan_on && xrows_mode(c->world, R, Qlog) == 2;
+    const size_t xrb = (c->shard && !xoff) ? xrows_bytes(c->world, R, Qlog) : 0;
     const size_t xgb = c->shard ? xgrows_bytes(c->world, R, Qlog) : 0;
     const XLayout xl = xlayout(c->world, E, Qlog, xc_width(R), xrb, xgb);
     int32_t *front = c->front_list, *back = c->back_list;
@@ -1061,20 +1069,35 @@ int enqueue_tick(fb_ctx *c) {
         const size_t xrw = (size_t)c->world * kXRecWords;
         a.xrec = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)c->xpar * xrw;
         a.xrows = xrb ? c->xbuf + xl.rows : nullptr;
-        a.xplan = (xrb && xrows_mode(c->world, R, Qlog) == 2) ? 1 : 0;
+        a.xplan = (c->xplan_on && xrows_mode(c->world, R, Qlog) == 2) ? 1 : 0;
+        c->l_full = c->full_assign != 0;
+        if (c->l_full && c->phase == 2) {
+            // the whole tick's assignments: at most its pending tasks plus every in-flight entry
+            const int64_t need = std::max<int64_t>(1, c->l_T + head);
+            if (need > c->assign_cap) {
+                const int64_t cap = std::max(need, 2 * c->assign_cap);
+                HIPCHK(c, stream_wait(c));
+                hipFree(c->assign_all);
+                c->assign_all = nullptr;
+                c->assign_cap = 0;
+                if ((rc = dalloc(c, &c->assign_all, (size_t)cap))) return rc;
+                c->assign_cap = cap;
+            }
+            a.assign_all = c->assign_all;
+        }
         if (a.xplan) {
             // k_xscan's outputs in the plan tables (unused on this path): per-block prefixes in
             // qpre's words, the chunk prefixes and totals in opre's
             a.xpre = reinterpret_cast<uint32_t *>(c->qpre);
             a.xct = reinterpret_cast<uint32_t *>(c->opre);
-            a.xA = a.xct + (size_t)cdiv(nbq, kBS) * 2 * R;
+            a.xA = a.xct + (size_t)cdiv(nbq, kXsBlocks) * 2 * R;
             a.xtk = c->xs_tk;
         }
         a.xgrows = xgb ? c->xbuf + xl.grows : nullptr;
         a.xg_acc = c->xg_acc;
         a.xg_tk = c->xg_tk;
         a.ogrp = c->ogrp;
-        if (xrb && c->phase == 2) {
+        if ((xrb || a.xplan) && c->phase == 2) {
             a.xz = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)(c->xpar ^ 1) * xrw;
             a.xz_words = (int)xrw;
         }
@@ -1163,10 +1186,10 @@ int enqueue_tick(fb_ctx *c) {
     }
     if (a.shard == 2) {
         if (R > kShardMaxR) return fail(c, FB_ERANGE, "sharded tick: round table of %d rows (limit %d)", R, kShardMaxR);
-        if (a.xrows) {
+        if (a.xrows || a.xplan) {
             // exchanged block rows: k_emit_shard alone (it also zeroes the other records copy,
-            // which the next tick's phase 1 writes); large queues: k_plan's column scans of the
-            // rows first
+            // which the next tick's phase 1 writes); xplan: k_xscan's counts and prefixes of the
+            // exchanged c bytes first
             if (a.xplan) {
                 Timer t(c, "plan");
                 launch_xscan(a, t.st());
@@ -1484,6 +1507,7 @@ int fb_destroy(fb_ctx *c) {
         hipFree(c->opre);
     }
     if (c->oA_owned) hipFree(c->oA);
+    if (c->assign_all) hipFree(c->assign_all);
     if (c->win_owned) hipFree(c->win_mem);
     if (c->dbg) hipFree(c->dbg);
     if (c->arena) hipFree(c->arena);
@@ -1804,7 +1828,8 @@ int fb_exchange_bytes(fb_ctx *c, int32_t n_events, int64_t *bytes) {
                                             xgrows_bytes(c->world, kXGroupR, Qlog)).total});
     } else {
         const int R = c->launched ? c->l_R : kRFused;
-        *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xrows_bytes(c->world, R, Qlog),
+        const bool xoff = !c->xplan_on && xrows_mode(c->world, R, Qlog) == 2;
+        *bytes = (int64_t)xlayout(c->world, E, Qlog, xc_width(R), xoff ? 0 : xrows_bytes(c->world, R, Qlog),
                                   xgrows_bytes(c->world, R, Qlog)).total;
     }
     return FB_OK;
@@ -2461,8 +2486,10 @@ static int copy_out(fb_ctx *c, void *dst, const void *src, size_t bytes) {
 int fb_get_assignments(fb_ctx *c, int64_t first, int64_t n, int32_t *dst) {
     if (!c || !dst) return FB_EINVAL;
     if (!c->waited) return fail(c, FB_ESTATE, "no waited tick");
-    if (c->shard) return fail(c, FB_ESTATE, "sharded context: use fb_get_local_assignments");
+    if (c->shard && !c->l_full)
+        return fail(c, FB_ESTATE, "sharded context: use fb_get_local_assignments (or fb_set_full_assign)");
     if (first < 0 || n < 0 || first + n > c->last.n_assigned) return fail(c, FB_EINVAL, "assignment range");
+    if (c->shard) return copy_out(c, dst, c->assign_all + first, (size_t)n * 4);
     return copy_out(c, dst, c->log_slot + c->l_head + first, (size_t)n * 4);
 }
 
@@ -2803,6 +2830,14 @@ int fb_device_view_get(fb_ctx *c, fb_device_view *v) {
     return FB_OK;
 }
 
+int fb_set_full_assign(fb_ctx *c, int on) {
+    if (!c) return FB_EINVAL;
+    if (c->launched) return fail(c, FB_ESTATE, "fb_set_full_assign between ticks only");
+    if (!c->shard) return fail(c, FB_ESTATE, "fb_set_full_assign on a one-GPU context (it always has them)");
+    c->full_assign = on ? 1 : 0;
+    return FB_OK;
+}
+
 int fb_set_round_hint(fb_ctx *c, int32_t max_free) {
     if (!c) return FB_EINVAL;
     if (c->launched) return fail(c, FB_ESTATE, "fb_set_round_hint between ticks only");
@@ -2821,6 +2856,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "ev_ll" && (value == 0 || value == 1)) c->ev_ll = value;
     else if (n == "rs_wide" && (value == 0 || value == 1)) c->rs_wide = value;
     else if (n == "fault_qlen") c->fault_qlen = value;
+    else if (n == "xplan" && (value == 0 || value == 1)) c->xplan_on = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }

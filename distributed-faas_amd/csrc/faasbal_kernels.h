@@ -34,7 +34,8 @@ constexpr int kXGroupBlocks = 16;
 constexpr int kXGroupDigits = 4;
 constexpr int kXGroupR = 32;
 __host__ __device__ constexpr int xg_row(int R) { return (kXGroupDigits * xr_stride(R) + 15) & ~15; }
-constexpr int kXgAccStride = 36;  // words per group accumulator row (R + 1 = 33 columns)
+constexpr int kXgAccStride = 36;
+constexpr int kXsBlocks = 64;  // k_xscan: queue blocks per workgroup (chunk): a lane per block  // words per group accumulator row (R + 1 = 33 columns)
 // phase 2: the parts (lanes) per 16-byte load column of the digit rows, a power of two
 // with every column's parts in one workgroup; own rows (R / 4 columns) use kBS / (R / 4)
 __host__ __device__ constexpr int xr_parts(int R) {
@@ -406,11 +407,14 @@ struct TickArgs {
     uint8_t *xgrows;               // exchanged group rows (R = kXGroupR; null: phase 2 sums the block rows)
     int xplan;                     // large queues (> kXRowsMaxBlocks blocks, R = kXGroupR): phase 2 is k_xscan's
                                    // prefix scans of the exchanged digit rows / own rows, then k_emit_shard
-    uint32_t *xpre;                // k_xscan: [block][2R] exclusive prefixes inside the block's 256-block chunk
+    uint32_t *xpre;                // k_xscan: [block][2R] exclusive prefixes inside the block's chunk
                                    // (rounds of all positions, then this rank's)
     uint32_t *xct;                 // [chunk][2R] chunk totals, turned into exclusive prefixes over the chunks
     uint32_t *xA;                  // [2R] totals A(r) (all, then this rank's)
     uint32_t *xtk;                 // k_xscan's ticket (zero between launches)
+    // sharded phase 2 (fb_set_full_assign): this rank also writes the whole tick's task -> slot
+    // array (every rank computes the global water-filling; one rank's copy serves the host)
+    int32_t *assign_all;
     uint32_t *xg_acc, *xg_tk;      // phase 1: per group the running sums and the ticket (zero between ticks)
     uint32_t *ogrp;                // phase 1 -> 2: this rank's group rows [group][R]
     unsigned long long *xz;        // phase 2: the other launch parity's exchange records, zeroed for the next tick

@@ -1356,6 +1356,17 @@ __device__ __forceinline__ TickArgs specialise(TickArgs a) {
     return a;
 }
 
+// Sharded exchange of the effective free counts: one byte per LRU position while the
+// round table has at most 128 rows (every c that matters is below the 255 clamp), two
+// bytes (clamp 65535) for wider tables.  Either way one rank writes each position.
+__device__ __forceinline__ int xc_get(const TickArgs &a, int64_t pos) {
+    return a.xcw == 2 ? (int)reinterpret_cast<const uint16_t *>(a.xc8)[pos] : (int)a.xc8[pos];
+}
+__device__ __forceinline__ void xc_put(const TickArgs &a, int64_t pos, int c) {
+    if (a.xcw == 2) reinterpret_cast<uint16_t *>(a.xc8)[pos] = (uint16_t)(c < 65535 ? c : 65535);
+    else a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
+}
+
 // ------------------------------------------------------------ slot purge
 // Heartbeat purge of every slot (purge_workers, :241-249): liveness, the
 // died-registration bitmap, next free_processes (INT32_MIN = no live record).
@@ -1459,17 +1470,6 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
     const uint8_t rf = a.post_rf[s];
     if ((rf >> 1) & kPfDiedStart) return true;
     return (rf & 1) && ((a.now - a.post[s].hb) > a.tte);
-}
-
-// Sharded exchange of the effective free counts: one byte per LRU position while the
-// round table has at most 128 rows (every c that matters is below the 255 clamp), two
-// bytes (clamp 65535) for wider tables.  Either way one rank writes each position.
-__device__ __forceinline__ int xc_get(const TickArgs &a, int64_t pos) {
-    return a.xcw == 2 ? (int)reinterpret_cast<const uint16_t *>(a.xc8)[pos] : (int)a.xc8[pos];
-}
-__device__ __forceinline__ void xc_put(const TickArgs &a, int64_t pos, int c) {
-    if (a.xcw == 2) reinterpret_cast<uint16_t *>(a.xc8)[pos] = (uint16_t)(c < 65535 ? c : 65535);
-    else a.xc8[pos] = (uint8_t)(c < 255 ? c : 255);
 }
 
 // ------------------------------------------------------------ k_scan
@@ -2179,65 +2179,74 @@ __global__ __launch_bounds__(kBS) void k_plan(TickArgs a) {
 
 // ------------------------------------------------------------ k_xscan (sharded phase 2, large queues)
 // The per-block prefixes of the exchanged round counts (xrows_mode 2: > kXRowsMaxBlocks
-// queue blocks, R = kXGroupR): one workgroup per chunk of 256 queue blocks, thread t the
-// rows of block 256 ch + t -- every rank's counts from the 4-bit digit row (7 x 16 B) and
-// this rank's own row (8 x 16 B), both coalesced across the wave --, decoded into LDS as a
-// [block][2R] matrix; each wave scans columns (4 rows per lane), the chunk-local exclusive
-// prefixes go out row-major (coalesced), the chunk totals into xct.  The last workgroup (an
-// agent-scope acq_rel ticket) turns the chunk totals into exclusive prefixes over the chunks
-// and writes the totals A(r).  k_plan's one workgroup per column walked 3.5 K rows with a
-// 64-line gather per wave load (13-17 us at configs[3]).
+// queue blocks, R = kXGroupR): one workgroup per chunk of kXsBlocks = 64 queue blocks, lane l
+// of every wave the rows of block 64 ch + l; wave w the 16 columns [16 w, 16 w + 16) of the
+// 2R = 64 (waves 0-1: every rank's counts, decoded from the block's 4-bit digit row; waves
+// 2-3: this rank's own row), each column one DPP scan across the wave's lanes -- no LDS
+// transpose.  The chunk-local exclusive prefixes go out as 64 contiguous bytes per lane, the
+// chunk totals into xct.  The last workgroup (an agent-scope acq_rel ticket) turns the chunk
+// totals into exclusive prefixes over the chunks -- four parts per column, each part's chunks
+// loaded at once -- and writes the totals A(r).  (k_plan's one workgroup per column walked
+// 3.5 K rows with a 64-line gather per wave load: 13-17 us at configs[3]; an LDS transpose per
+// 256-block chunk 11-14 us; counting the exchanged c bytes here instead of in phase 1 -- a
+// phase 1 without a queue role -- 20-31 us: NOTES_r05.md.)
 template <int R>
 __global__ __launch_bounds__(kBS) void k_xscan(TickArgs a) {
     prefetch_args(a);
     const int SO = 3 * (a.nbw + a.nbf + a.nbq) + 6000;  // diagnostic stamp rows (stamps builds)
     STAMP(a, SO, 0);
-    constexpr int C = 2 * R, LD = C + 1, XS = xr_stride(R), NQ = xr_row(R) / 16, NO = R / 4;
-    __shared__ uint32_t xl[kBS * LD];
+    static_assert(2 * R == 4 * 16 && kXsBlocks == 64, "four waves of 16 columns, a lane per block");
+    constexpr int C = 2 * R, XS = xr_stride(R), NQ = xr_row(R) / 16;
     __shared__ int last;
+    __shared__ uint32_t psum[kWaves][C];
     const int ch = blockIdx.x, t = threadIdx.x, lane = lane_id(), w = wave_id();
-    const int b = ch * kBS + t;
+    const int b = ch * kXsBlocks + lane;
     const bool in = b < a.nbq;
     const int bc = in ? b : a.nbq - 1;
-    uint4 d[NQ], o[NO];
-    const uint4 *dr = reinterpret_cast<const uint4 *>(a.xrows + (size_t)bc * xr_row(R));
-    const uint4 *orw = reinterpret_cast<const uint4 *>(a.ocnt + (size_t)bc * R);
+    uint32_t v[16];
+    auto word = [](const uint4 &q, int i) -> uint32_t { return i == 0 ? q.x : i == 1 ? q.y : i == 2 ? q.z : q.w; };
+    if (w < 2) {
+        // every rank's counts of rounds 16 w .. 16 w + 15: digit bytes r, XS + r, 2 XS + r
+        uint4 d[NQ];
+        const uint4 *dr = reinterpret_cast<const uint4 *>(a.xrows + (size_t)bc * xr_row(R));
 #pragma unroll
-    for (int k = 0; k < NQ; ++k) d[k] = dr[k];
+        for (int k = 0; k < NQ; ++k) d[k] = dr[k];
+        auto byte = [&](int k) -> uint32_t { return (word(d[k >> 4], (k >> 2) & 3) >> (8 * (k & 3))) & 0xffu; };
 #pragma unroll
-    for (int k = 0; k < NO; ++k) o[k] = orw[k];
-    STAMPW(a, SO, 1);
-    // (constant byte / word indices once unrolled: register extracts)
-    auto word = [](const uint4 &v, int i) -> uint32_t { return i == 0 ? v.x : i == 1 ? v.y : i == 2 ? v.z : v.w; };
-    auto byte = [&](int k) -> uint32_t { return (word(d[k >> 4], (k >> 2) & 3) >> (8 * (k & 3))) & 0xffu; };
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-        xl[t * LD + r] = in ? byte(r) + (byte(XS + r) << 4) + (byte(2 * XS + r) << 8) : 0u;
-        xl[t * LD + R + r] = in ? word(o[r >> 2], r & 3) : 0u;
-    }
-    __syncthreads();
-    STAMP(a, SO, 2);
-    // columns: wave w takes w, w + 4, ...; lane l rows 4 l .. 4 l + 3
-    for (int col = w; col < C; col += kWaves) {
-        uint32_t v[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) v[j] = xl[(4 * lane + j) * LD + col];
-        const uint32_t sm = v[0] + v[1] + v[2] + v[3];
-        const uint32_t inc = wave_incl_scan_u32(sm);
-        uint32_t ex = inc - sm;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            xl[(4 * lane + j) * LD + col] = ex;
-            ex += v[j];
+        for (int j = 0; j < 16; ++j) {
+            // (w is wave-uniform: both forms unrolled with constant byte indices)
+            const uint32_t x0 = byte(j) + (byte(XS + j) << 4) + (byte(2 * XS + j) << 8);
+            const uint32_t x1 = byte(16 + j) + (byte(XS + 16 + j) << 4) + (byte(2 * XS + 16 + j) << 8);
+            v[j] = in ? (w == 0 ? x0 : x1) : 0u;
         }
-        if (lane == 63) a.xct[(size_t)ch * C + col] = inc;
+    } else {
+        // this rank's own counts of rounds 16 (w - 2) .. +15: words of its own row
+        const uint4 *orw = reinterpret_cast<const uint4 *>(a.ocnt + (size_t)bc * R) + 4 * (w - 2);
+        uint4 o[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) o[k] = orw[k];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) v[j] = in ? word(o[j >> 2], j & 3) : 0u;
     }
-    __syncthreads();
-    STAMP(a, SO, 3);
-    const int nrow = min(kBS, a.nbq - ch * kBS);
-    uint32_t *const dst = a.xpre + (size_t)ch * kBS * C;
-    for (int e = t; e < nrow * C; e += kBS) dst[e] = xl[(e / C) * LD + e % C];
-    // every wave's chunk-total stores done, then the ticket (release / acquire at agent scope)
+    STAMPW(a, SO, 1);
+    uint32_t tot[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+        const uint32_t inc = wave_incl_scan_u32(v[j]);
+        tot[j] = (uint32_t)__builtin_amdgcn_readlane((int)inc, 63);
+        v[j] = inc - v[j];
+    }
+    STAMP(a, SO, 2);
+    if (in) {
+        uint4 *dst = reinterpret_cast<uint4 *>(a.xpre + (size_t)b * C + 16 * w);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dst[k] = make_uint4(v[4 * k], v[4 * k + 1], v[4 * k + 2], v[4 * k + 3]);
+    }
+    uint32_t my = 0;  // lane j < 16: column 16 w + j's chunk total
+#pragma unroll
+    for (int j = 0; j < 16; ++j) my = lane == j ? tot[j] : my;
+    if (lane < 16) a.xct[(size_t)ch * C + 16 * w + lane] = my;
+    // every wave's stores done, then the ticket (release / acquire at agent scope)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     STAMP(a, SO, 4);
@@ -2249,19 +2258,47 @@ __global__ __launch_bounds__(kBS) void k_xscan(TickArgs a) {
         STAMP(a, SO, 15);
         return;
     }
-    if (t < C) {
-        // 16 chunks' totals per pass, all loads in flight before the running sum (a load per
-        // iteration behind the previous store costs a memory round trip per chunk)
+    // exclusive prefixes over the chunks: column col = t % C, part t / C of kBS / C, each
+    // part's chunks loaded at once (up to 64 in registers), then the parts' offsets
+    constexpr int NP = kBS / C;
+    const int col = t % C, part = t / C;
+    const int nch = (int)gridDim.x, per = (nch + NP - 1) / NP;
+    const int c0 = part * per;
+    if (per <= 64) {
+        uint32_t x[64];
+        uint32_t sum = 0;
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            x[k] = a.xct[(size_t)min(c0 + k, nch - 1) * C + col];
+            x[k] = (k < per && c0 + k < nch) ? x[k] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 64; ++k) sum += x[k];
+        psum[part][col] = sum;
+        __syncthreads();
+        uint32_t run = 0, all = 0;
+#pragma unroll
+        for (int q = 0; q < NP; ++q) {
+            run += q < part ? psum[q][col] : 0u;
+            all += psum[q][col];
+        }
+#pragma unroll
+        for (int k = 0; k < 64; ++k) {
+            if (k < per && c0 + k < nch) a.xct[(size_t)(c0 + k) * C + col] = run;
+            run += x[k];
+        }
+        if (part == 0) a.xA[col] = all;
+    } else if (t < C) {
+        // (past 64 x NP chunks: one thread per column, 16 chunks in flight per pass)
         uint32_t run = 0;
-        const int nch = (int)gridDim.x;
-        for (int c0 = 0; c0 < nch; c0 += 16) {
-            uint32_t v[16];
+        for (int b0 = 0; b0 < nch; b0 += 16) {
+            uint32_t x[16];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) v[j] = a.xct[(size_t)min(c0 + j, nch - 1) * C + t];
+            for (int k = 0; k < 16; ++k) x[k] = a.xct[(size_t)min(b0 + k, nch - 1) * C + t];
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                if (c0 + j < nch) a.xct[(size_t)(c0 + j) * C + t] = run;
-                run += c0 + j < nch ? v[j] : 0u;
+            for (int k = 0; k < 16; ++k) {
+                if (b0 + k < nch) a.xct[(size_t)(b0 + k) * C + t] = run;
+                run += b0 + k < nch ? x[k] : 0u;
             }
         }
         a.xA[t] = run;
@@ -3856,7 +3893,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         } else if (XP) {
             // k_xscan's totals, this block's chunk-local prefixes and its chunk's prefix (lanes
             // r < R of chunk 0: R = kXGroupR), every rank's orphans and max c from the records
-            const int ch = b / kBS;
+            const int ch = b / kXsBlocks;
             const int rr = min(lane, R - 1);
             const uint32_t A0 = a.xA[rr], oA0 = a.xA[R + rr];
             const uint32_t p0 = a.xpre[(size_t)b * 2 * R + rr], op0 = a.xpre[(size_t)b * 2 * R + R + rr];
@@ -4058,7 +4095,9 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         uint32_t *const lseq = a.lseq_out + a.head_local;
         const uint32_t hin = (uint32_t)a.head_in;
         // ---- full rounds r < min(L, max own c of the wave): own lanes append their task
-        const int owmx = (int)wave_max_u32((uint32_t)oc);
+        // (assign_all: every lane's task into the whole-tick array, rounds < min(L, max c))
+        int32_t *const aall = a.assign_all;
+        const int owmx = (int)wave_max_u32((uint32_t)(aall ? c : oc));
         const int rfull = L < owmx ? L : owmx;
         // (32-bit byte offsets from the arena base when it spans < 4 GB: a saddr store per
         // array, as k_emit2's rounds; four rounds per step)
@@ -4082,6 +4121,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                             *reinterpret_cast<int32_t *>(ab + (so + lp4)) = s;
                             *reinterpret_cast<uint32_t *>(ab + (qo + lp4)) = hin + base + popc_lt(m);
                         }
+                        if (aall && c > r) aall[base + popc_lt(m)] = s;
                     }
                 }
             }
@@ -4096,6 +4136,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
                     lslot[lp] = s;
                     lseq[lp] = hin + (uint32_t)(base + popc_lt(m));
                 }
+                if (aall && c > r) aall[base + popc_lt(m)] = s;
             }
         }
         // ---- round L (partial: ranks < p) and round L + 1 (ranks for the next queue)
@@ -4112,6 +4153,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             lslot[lp] = s;
             lseq[lp] = hin + (uint32_t)(S_L + rankL);
         }
+        if (aall && c > L && rankL < p) aall[S_L + rankL] = s;
         const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
         if (c > 0) {
             int64_t n_q = c < L ? c : L;
@@ -4147,7 +4189,7 @@ __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid) {
     // the tile's offset: k_plan's scan of the tile counts, or (no k_plan: group rows) the
     // wave's own sum of the earlier tiles' counts
     auto tile_pre = [&](const uint32_t *cnt, const int64_t *pre) -> int64_t {
-        if (!a.grp_on && !a.xrows) return pre[t];
+        if (!a.grp_on && !a.xrows && !a.xplan) return pre[t];
         uint32_t v = 0;
         for (int i = lane; i < t; i += 64) v += cnt[i];
         return (int64_t)wave_sum_u32(v);
@@ -4281,7 +4323,8 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
     uint32_t *const lseq = a.lseq_out + a.head_local;
     const uint32_t hin = (uint32_t)a.head_in;
     // ---- full rounds r < min(L, max own c of the wave), a 64-round chunk at a time
-    const int owmx = (int)wave_max_u32((uint32_t)oc);
+    int32_t *const aall = a.assign_all;  // (fb_set_full_assign: every lane's task too)
+    const int owmx = (int)wave_max_u32((uint32_t)(aall ? c : oc));
     const int rfull = L < owmx ? L : owmx;
     for (int k = 0; 64 * k < rfull; ++k) {
         const int r = 64 * k + lane;
@@ -4304,6 +4347,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
                 lslot[lp] = s;
                 lseq[lp] = hin + (uint32_t)(base + popc_lt(m));
             }
+            if (aall && c > rr) aall[base + popc_lt(m)] = s;
         }
     }
     // ---- round L (partial: ranks < p) and round L + 1 (ranks for the next queue)
@@ -4319,6 +4363,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_wide(TickArgs a) {
         lslot[lp] = s;
         lseq[lp] = hin + (uint32_t)(S_L + rankL);
     }
+    if (aall && c > L && rankL < p) aall[S_L + rankL] = s;
     const int64_t exL1 = rbL1 + popc_lt(__ballot(c > L + 1));
     if (c > 0) {
         int64_t n_q = c < L ? c : L;
@@ -4533,7 +4578,8 @@ void launch_plan(const TickArgs &a, Stream st) {
         hipExtLaunchKernelGGL(k_plan, dim3(3 + (a.shard ? 2 : 1) * a.R), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_xscan(const TickArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_xscan<kXGroupR>, dim3((a.nbq + kBS - 1) / kBS), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    hipExtLaunchKernelGGL(k_xscan<kXGroupR>, dim3((a.nbq + kXsBlocks - 1) / kXsBlocks), dim3(kBS), 0, st.s, st.e0,
+                          st.e1, 0, a);
 }
 void launch_emit(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);

@@ -27,7 +27,7 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign", "fb_get_outputs",
            "fb_read_inflight", "fb_set_compact", "fb_get_outputs_compact", "fb_expand_compact",
            "fb_set_window", "fb_window_stats", "fb_set_compact_out", "fb_set_eager_commit", "fb_set_path",
-           "fb_set_round_hint")
+           "fb_set_round_hint", "fb_set_full_assign")
 
 
 class TickResult(C.Structure):
@@ -132,6 +132,7 @@ def load(path=None):
         "fb_expand_compact": (C.c_int, [_P, _P, _P, i64, _P]),
         "fb_set_path": (C.c_int, [_P, C.c_char_p, C.c_int]),
         "fb_set_round_hint": (C.c_int, [_P, C.c_int32]),
+        "fb_set_full_assign": (C.c_int, [_P, C.c_int]),
     }
     for name, (res, args) in proto.items():
         fn = getattr(lib, name, None)

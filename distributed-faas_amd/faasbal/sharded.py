@@ -122,8 +122,16 @@ class ShardedBalancer(GpuBalancer):
     def cont(self):
         self._chk(self.lib.fb_tick_continue(self.h))
 
+    def set_full_assign(self, on=True):
+        """fb_set_full_assign: this rank's phase 2 also writes the whole tick's task -> slot
+        array (assignments() then works here; the dispatcher's rank gathers no tasks)."""
+        self._chk(self.lib.fb_set_full_assign(self.h, 1 if on else 0))
+        self.full_assign = bool(on)
+
     def assignments(self, first=0, n=None):
-        raise FaasbalError(_lib.FB_ESTATE, "sharded context: use local_assignments()")
+        if not getattr(self, "full_assign", False):
+            raise FaasbalError(_lib.FB_ESTATE, "sharded context: use local_assignments() (or set_full_assign)")
+        return super().assignments(first, n)
 
     def _allreduce(self, allreduce):
         n = C.c_int64()
@@ -170,9 +178,14 @@ class ShardedBalancer(GpuBalancer):
                                allreduce)
         out = dict(result=res)
         if outputs:
-            task, slot = self.local_assignments()
-            out.update(reconnect=self.event_status(), task=task, slot=slot, orphans=self.orphans(),
-                       evicted=self.evicted())
+            # the whole tick's assignments where this rank writes them (set_full_assign), else
+            # this rank's own (task, slot) pairs
+            if getattr(self, "full_assign", False):
+                out.update(assign=self.assignments())
+            else:
+                task, slot = self.local_assignments()
+                out.update(task=task, slot=slot)
+            out.update(reconnect=self.event_status(), orphans=self.orphans(), evicted=self.evicted())
         if commit:
             self.commit()
         return out
@@ -376,8 +389,10 @@ def _gather_results(dist, dev, op, guarded):
     payload = np.zeros(0, np.uint8)
     if ok:
         r = val["result"]
-        task = np.asarray(val.get("task", np.zeros(0)), np.int64)
-        slot = np.asarray(val.get("slot", np.zeros(0)), np.int32)
+        # (rank 0 writes the whole assignment array itself, fb_set_full_assign: the other
+        # ranks send only their orphans and evicted slots, a few KB)
+        task = np.zeros(0, np.int64)
+        slot = np.zeros(0, np.int32)
         orph = np.asarray(val["orphans"], np.int64)
         evic = np.asarray(val["evicted"], np.int32)
         h[0] = 1
@@ -413,15 +428,11 @@ def _gather_results(dist, dev, op, guarded):
                 res = dict(n_local=int(hs[i][2]), n_orphans_local=int(hs[i][3]), n_evicted=int(hs[i][4]))
                 d = dict(result=res, orphans=b[o[2]:o[3]].view(np.int64).copy(),
                          evicted=b[o[3]:o[4]].view(np.int32).copy(), reconnect=None)
-                if op == "tick":
-                    d.update(task=b[o[0]:o[1]].view(np.int64).copy(), slot=b[o[1]:o[2]].view(np.int32).copy())
                 outs[i] = (True, d)
     elif rank == 0:
         for i in range(1, world):
             res = dict(n_local=int(hs[i][2]), n_orphans_local=int(hs[i][3]), n_evicted=int(hs[i][4]))
             d = dict(result=res, orphans=np.zeros(0, np.int64), evicted=np.zeros(0, np.int32), reconnect=None)
-            if op == "tick":
-                d.update(task=np.zeros(0, np.int64), slot=np.zeros(0, np.int32))
             outs[i] = (True, d)
     return outs
 
@@ -442,6 +453,8 @@ class DistShardGroup(ShardGroup):
         if dist.get_rank() != 0:
             raise FaasbalError(_lib.FB_ESTATE, "DistShardGroup lives on rank 0; run serve_shard() on the others")
         self.dev = _dev(dist)
+        # rank 0's phase 2 writes the whole assignment array (the per-task gather is gone)
+        balancer.set_full_assign(True)
 
     def _each(self, op, **kw):
         _bcast_call(self.dist, self.dev, op, kw)
@@ -553,10 +566,16 @@ class LocalShardGroup(ShardGroup):
 
 
 def merge_outputs(outs, n_assigned):
-    """Whole-table outputs from every rank's tick outputs (test / host-side helper)."""
-    assign = np.full(n_assigned, -1, np.int32)
-    for o in outs:
-        assign[o["task"]] = o["slot"]
+    """Whole-table outputs from every rank's tick outputs (test / host-side helper): the
+    assignment array of a rank that wrote it whole (set_full_assign), else the union of
+    the ranks' (task, slot) pairs."""
+    full = next((o["assign"] for o in outs if o.get("assign") is not None), None)
+    if full is not None:
+        assign = np.asarray(full, np.int32)
+    else:
+        assign = np.full(n_assigned, -1, np.int32)
+        for o in outs:
+            assign[o["task"]] = o["slot"]
     orphans = np.sort(np.concatenate([o["orphans"] for o in outs])) if outs else np.zeros(0, np.int64)
     evicted = np.sort(np.concatenate([o["evicted"] for o in outs])) if outs else np.zeros(0, np.int32)
     return dict(reconnect=outs[0]["reconnect"], assign=assign, orphans=orphans.astype(np.int64),

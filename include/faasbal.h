@@ -322,6 +322,12 @@ int fb_read_shard_log(fb_ctx *ctx, uint32_t *log_seq, int64_t *log_len, int64_t 
  * starts narrow and a wider fill level costs one FB_ERERUN relaunch.  Replaces nothing in
  * the reference (it sizes a buffer, task_dispatcher.py:393-419 has none). */
 int fb_set_round_hint(fb_ctx *ctx, int32_t max_free);
+/* Sharded, between ticks: on != 0 makes this rank's phase 2 also write the whole tick's
+ * task -> slot array (every rank computes the global water-filling anyway), so
+ * fb_get_assignments works on it and the host needs no per-task gather from the other
+ * ranks (the rank that serves the dispatcher loop turns it on).  Replaces the gather of
+ * task_dispatcher.py:409-413's decisions onto the loop's process. */
+int fb_set_full_assign(fb_ctx *ctx, int on);
 /* Exchange buffer size for a tick of n_events events (n_events < 0: the maximum). */
 int fb_exchange_bytes(fb_ctx *ctx, int32_t n_events, int64_t *bytes);
 /* Device buffer (same size on every rank) the ranks all-reduce between phases. */

@@ -158,6 +158,7 @@ def phase2(rs, ctx, x, redist=True):
     p = N_eff - S[L]
     AL = int((c > L).sum())
     tasks, slots = [], []
+    assign_all = np.full(N_eff, -1, np.int32)  # the whole tick's task -> slot (fb_set_full_assign)
     for r in range(L + 1):
         act = np.nonzero(c > r)[0]
         lim = len(act) if r < L else p
@@ -165,6 +166,7 @@ def phase2(rs, ctx, x, redist=True):
         sel_own = np.nonzero(own[sel])[0]
         tasks.append(S[r] + sel_own)
         slots.append(lq[sel[sel_own]])
+        assign_all[S[r]:S[r] + lim] = lq[sel]
     tasks = np.concatenate(tasks) if tasks else np.zeros(0, np.int64)
     slots = np.concatenate(slots) if slots else np.zeros(0, np.int64)
     rankL = np.cumsum(c > L) - 1
@@ -195,5 +197,5 @@ def phase2(rs, ctx, x, redist=True):
                log_seq=np.concatenate([rs["log_seq"], head + tasks]), head=head + N_eff)
     out = dict(task=tasks, slot=slots.astype(np.int32), orphans=ctx["orphans"].astype(np.int64),
                evicted=(np.nonzero(evicted)[0] + base).astype(np.int32),
-               reconnect=x[lay["evs"]:lay["c8"]].copy(), n_assigned=N_eff)
+               reconnect=x[lay["evs"]:lay["c8"]].copy(), n_assigned=N_eff, assign_all=assign_all)
     return out, nxt

@@ -14,6 +14,10 @@ class ModelRankBalancer:
     def __init__(self, rank, world, n_workers):
         self.rank, self.world, self.W = rank, world, int(n_workers)
         self.rs = None
+        self.full_assign = False
+
+    def set_full_assign(self, on=True):
+        self.full_assign = bool(on)
 
     def close(self):
         pass
@@ -40,6 +44,9 @@ class ModelRankBalancer:
         x, ctx = sm.phase1(self.rs, self.world, self.rank, now, tte, k, s, v, t, q, T)
         out, self._next = sm.phase2(self.rs, ctx, self._exchange(x, allreduce), redist=redist)
         n = int(out["n_assigned"])
+        full = out.pop("assign_all")
+        if self.full_assign:
+            out["assign"] = full
         out["result"] = dict(n_assigned=n, log_head=head + n, n_local=len(out["task"]),
                              n_orphans_local=len(out["orphans"]), n_evicted=len(out["evicted"]))
         if commit:

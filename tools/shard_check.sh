@@ -5,7 +5,7 @@
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}; cd $R; mkdir -p gpurun_out
 T=${1:-sh}
-timeout -k 10 900 python -u -m pytest tests/test_gpu_sharded.py tests/test_gpu_shard_dist.py tests/test_shard_dispatcher.py \
+timeout -k 10 1000 python -u -m pytest tests/test_gpu_sharded.py tests/test_gpu_shard_dist.py tests/test_shard_dispatcher.py \
     "tests/test_full_size.py::test_gpu_sharded_16m_x_1m_matches_oracle" -m gpu -x -q --timeout 300 --timeout-method thread \
     > gpurun_out/${T}_pytest.log 2>&1 || { tail -40 gpurun_out/${T}_pytest.log; exit 1; }
 tail -2 gpurun_out/${T}_pytest.log

@@ -68,15 +68,15 @@ for k in (1, 4, 5, 6, 15):  # (the k_plan path stamps 1 after its loads, 5 after
         print("  %2d -> %2d  median %6d cyc  p90 %6d" % (prev, k, np.median(dc), np.percentile(dc, 90)))
         prev = k
 # k_xscan (large queues): its stamp rows from 3 (nbw + nbf + nbq) + 6000, one per chunk
-nch = -(-nbq // 256)
+nch = -(-nbq // 64)
 SX = SO + 6000
 dx = np.stack([r[: (SX + nch) * 16].reshape(-1, 16).astype(np.int64) for r in rows])[:, SX:SX + nch, :]
-if (dx[:, :, 13] > 0).all():
+if dx.size and (dx[:, :, 13] > 0).all():
     t0 = dx[:, :, 13].min(axis=1, keepdims=True)
     print("k_xscan: %d chunks; start max %.2f us, end max %.2f us (realtime)" % (
         nch, np.median(((dx[:, :, 13] - t0) / 100.0).max(axis=1)), np.median(((dx[:, :, 14] - t0) / 100.0).max(axis=1))))
     prev = 0
-    for k in (1, 2, 3, 4, 5, 15):
+    for k in (1, 2, 4, 5, 15):
         dc = (dx[:, :, k] - dx[:, :, prev])
         print("  %2d -> %2d  median %6d cyc  max %6d" % (prev, k, np.median(dc), np.median(dc.max(axis=1))))
         prev = k
