@@ -2318,6 +2318,30 @@ __global__ __launch_bounds__(kBS) void k_xscan(TickArgs a) {
 // eviction tile counts.  Group 0 publishes the totals (A, P).
 constexpr int kGrpLd = 4;     // group / block row loads per thread per batch (k_plan2, k_emit2)
 constexpr int kP2Rows = kBS;  // rows per pass of a group's scan (one per thread)
+// k_plan2's group scan for groups of <= 64 blocks (one wave; lane l = block b0 + l)
+template <int R>
+__device__ __forceinline__ void plan2_group_rows(const TickArgs &a, int g, int b0, int b1, int nr,
+                                                 const uint32_t *gp_r) {
+    const int lane = lane_id();
+    const int b = b0 + lane;
+    const bool in = b < b1;
+    const uint4 *rp = reinterpret_cast<const uint4 *>(a.qcnt + (size_t)min(b, b1 - 1) * R);
+    uint32_t v[R];
+#pragma unroll
+    for (int k = 0; k < R / 4; ++k) {
+        const uint4 q = rp[k];
+        v[4 * k] = q.x;
+        v[4 * k + 1] = q.y;
+        v[4 * k + 2] = q.z;
+        v[4 * k + 3] = q.w;
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+        const uint32_t x = (in && r < nr) ? v[r] : 0u;
+        const uint32_t inc = wave_incl_scan_u32(x);
+        if (in && r < nr) a.qpre[(size_t)b * R + r] = (int64_t)gp_r[r] + (int64_t)(inc - x);
+    }
+}
 __global__ __launch_bounds__(kBS) void k_plan2(TickArgs a) {
     prefetch_args(a);
     __shared__ unsigned long long l4[kWaves];
@@ -2421,6 +2445,17 @@ __global__ __launch_bounds__(kBS) void k_plan2(TickArgs a) {
     const int nr = nr_s;
     // ---- this group's rows, rounds r < nr: prefix = earlier groups + earlier rows
     const int gsz = 1 << a.gshift, b0 = g * gsz, b1 = min(b0 + gsz, a.nbq);
+    if (gsz <= 64 && (R == 32 || R == 64)) {
+        // a group of <= 64 blocks (configs[3]: 56 groups of 64): wave 0, lane l = block b0 + l,
+        // its whole row in one load round (16-byte loads), then one DPP scan across the lanes
+        // per round -- instead of a load round and a block barrier per 4 rounds (8.6 us at
+        // configs[3])
+        if (w == 0) {
+            if (R == 32) plan2_group_rows<32>(a, g, b0, b1, nr, gp_r);
+            else plan2_group_rows<64>(a, g, b0, b1, nr, gp_r);
+        }
+        return;
+    }
     for (int r0 = 0; r0 < nr; r0 += 4) {
         uint32_t carry4[4] = {0u, 0u, 0u, 0u};
         for (int c0 = b0; c0 < b1; c0 += kP2Rows) {
@@ -3554,18 +3589,15 @@ constexpr int kRCh = 3;  // 64-round chunks: rounds 0 .. L+1 <= 129
 // as digit rows (phase 1, a.xrows), this rank's in its own rows (ocnt); each block sums the
 // rows of all blocks (totals) and of the blocks before it (prefix), and counts its waves'
 // rounds itself; max c and the capacity follow from the totals.
-// XP (large queues, a.xplan): the block rows arrived in the exchange as with XR, but k_plan
-// scanned their columns (every rank's digits, this rank's own rows) into per-block prefixes
-// and totals first; each block reads its own prefix row and counts its waves' rounds itself
-// (no phase-2 k_scan, no segment counts).
-template <bool GRP, bool XR, bool XP = false>
+// (Large queues, a.xplan: k_emit_shard_xp below.)
+template <bool GRP, bool XR>
 __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
     prefetch_args(a);
     const int bid = blockIdx.x;
     const int lane = lane_id(), w = wave_id();
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows (stamps builds)
     STAMP(a, SO, 0);
-    if (XR || XP) {  // the other parity's exchange records, for the next tick's phase 1
+    if (XR) {  // the other parity's exchange records, for the next tick's phase 1
         for (int i = bid * kBS + (int)threadIdx.x; i < a.xz_words; i += (int)gridDim.x * kBS) a.xz[i] = 0ull;
     } else if (GRP) {  // the other parity's group rows, for the next launch's k_scan atomics
         for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
@@ -3890,87 +3922,6 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             maxc = (int)max(max(smx[0], smx[1]), max(smx[2], smx[3]));
             cap = (int64_t)scap[0] + scap[1] + scap[2] + scap[3];
             O = (int64_t)sorf[0] + sorf[1] + sorf[2] + sorf[3];
-        } else if (XP) {
-            // k_xscan's totals, this block's chunk-local prefixes and its chunk's prefix (lanes
-            // r < R of chunk 0: R = kXGroupR), every rank's orphans and max c from the records
-            const int ch = b / kXsBlocks;
-            const int rr = min(lane, R - 1);
-            const uint32_t A0 = a.xA[rr], oA0 = a.xA[R + rr];
-            const uint32_t p0 = a.xpre[(size_t)b * 2 * R + rr], op0 = a.xpre[(size_t)b * 2 * R + R + rr];
-            const uint32_t c0 = a.xct[(size_t)ch * 2 * R + rr], oc0 = a.xct[(size_t)ch * 2 * R + R + rr];
-            const int gx = (int)threadIdx.x < a.world * kXRecLines ? (int)threadIdx.x : 0;
-            const unsigned long long xo = a.xrec[(size_t)gx * 16], xm = a.xrec[(size_t)gx * 16 + 1];
-#pragma unroll
-            for (int k = 0; k < kRCh; ++k) {
-                Av[k] = k == 0 ? A0 : 0u;
-                oAv[k] = k == 0 ? oA0 : 0u;
-                pv[k] = k == 0 ? p0 + c0 : 0u;
-                opv[k] = k == 0 ? op0 + oc0 : 0u;
-            }
-            __shared__ uint32_t xred[kWaves][2];
-            {
-                const bool rin = (int)threadIdx.x < a.world * kXRecLines;
-                const uint32_t orf = wave_sum_u32(rin ? (uint32_t)xo : 0u), mxr = wave_max_u32(rin ? (uint32_t)xm : 0u);
-                if (lane == 0) {
-                    xred[w][0] = orf;
-                    xred[w][1] = mxr;
-                }
-            }
-            STAMPW(a, SO, 1);
-            {
-                // the capacity sum_r<R A(r) (= sum of c when max c <= R), and this wave's rounds
-                // (all / own lanes) from histograms of min(c, R): the in-block bases of the
-                // later waves
-                __shared__ uint32_t swc[kWaves][kRFused + 1], sowc[kWaves][kRFused + 1];
-                uint32_t cp = 0;
-#pragma unroll
-                for (int k = 0; k < kRCh; ++k) cp += (64 * k + lane < R) ? (uint32_t)Av[k] : 0u;
-                cap = (int64_t)wave_sum_u32(cp);
-                const int cw_ = pos < a.Qlog ? cq : 0;
-                const int ocw = (cw_ > 0 && sq >= 0 && own_slot(a, sq) >= 0) ? cw_ : 0;
-                uint32_t *ha = swc[w], *ho = sowc[w];
-                for (int i = lane; i <= R; i += 64) {
-                    ha[i] = 0;
-                    ho[i] = 0;
-                }
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_wave_barrier();
-                atomicAdd(&ha[cw_ < R ? cw_ : R], 1u);
-                atomicAdd(&ho[ocw < R ? ocw : R], 1u);
-                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-                __builtin_amdgcn_wave_barrier();
-                uint32_t ca = 0, co = 0;
-#pragma unroll
-                for (int k = 0; k < 2; ++k) {  // count(c > r) = 64 - #(lanes with min(c, R) <= r)
-                    const int r = 64 * k + lane;
-                    const uint32_t hv = r < R ? ha[r] : 0u, hw = r < R ? ho[r] : 0u;
-                    const uint32_t Pa = ca + wave_incl_scan_u32(hv), Po = co + wave_incl_scan_u32(hw);
-                    ca = (uint32_t)__builtin_amdgcn_readlane((int)Pa, 63);
-                    co = (uint32_t)__builtin_amdgcn_readlane((int)Po, 63);
-                    __builtin_amdgcn_wave_barrier();
-                    if (r < R) {
-                        ha[r] = 64u - Pa;
-                        ho[r] = 64u - Po;
-                    }
-                }
-                __syncthreads();
-#pragma unroll
-                for (int k = 0; k < kRCh; ++k) {
-                    const int rr = min(64 * k + lane, R - 1);
-                    uint32_t sc = 0, osc = 0;
-#pragma unroll
-                    for (int qq = 0; qq < kWaves - 1; ++qq) {
-                        const bool in = qq < w && 64 * k + lane < R;
-                        sc += in ? swc[qq][rr] : 0u;
-                        osc += in ? sowc[qq][rr] : 0u;
-                    }
-                    segc[k] = sc;
-                    osegc[k] = osc;
-                }
-                O = (int64_t)xred[0][0] + xred[1][0] + xred[2][0] + xred[3][0];
-                maxc = (int)max(max(xred[0][1], xred[1][1]), max(xred[2][1], xred[3][1]));
-                STAMP(a, SO, 5);
-            }
         } else {
 #pragma unroll
             for (int k = 0; k < kRCh; ++k) {
@@ -3984,7 +3935,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
             cap = a.P->cap_total;
             maxc = a.P->maxc;
         }
-        if (!XR && !XP) {
+        if (!XR) {
             uint32_t sv[kRCh][kWaves - 1], osv[kRCh][kWaves - 1];
 #pragma unroll
             for (int k = 0; k < kRCh; ++k)
@@ -4042,7 +3993,7 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         const int64_t ALv = (int64_t)__builtin_amdgcn_readlane((int)(Lc == 0 ? Av[0] : (Lc == 1 ? Av[1] : Av[2])), Ll);
         const int64_t AL = (L < maxc && L < rlim) ? ALv : 0;
         int64_t O_loc = 0, n_ev = 0;
-        if ((GRP || XP) && b == 0) {
+        if (GRP && b == 0) {
             // this rank's orphans and evictions (its phase-1 tile counts) for the host
             __shared__ uint32_t sfo[kWaves], sev[kWaves];
             uint32_t fo = 0, ev = 0;
@@ -4060,8 +4011,8 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         }
         if (b == 0 && threadIdx.x == 0) {
             a.hout->O = O;
-            a.hout->O_local = (GRP || XP) ? O_loc : a.P->O_local;
-            a.hout->n_evicted = (GRP || XP) ? n_ev : a.P->n_evicted;
+            a.hout->O_local = GRP ? O_loc : a.P->O_local;
+            a.hout->n_evicted = GRP ? n_ev : a.P->n_evicted;
             a.hout->cap_total = cap;
             a.hout->maxc = maxc;
             a.hout->L = L;
@@ -4176,6 +4127,237 @@ __global__ __launch_bounds__(kBS) void k_emit_shard(TickArgs a) {
         return;
     }
     shard_compact(a, bid);
+}
+
+// k_emit_shard for xplan ticks (R = kXGroupR, > kXRowsMaxBlocks queue blocks), NSB queue
+// blocks per workgroup: every sub-block's loads in one round, the fill level once per
+// workgroup, then each sub-block's in-block ranks, emission and next state in turn.  At
+// configs[3] the 3 547 blocks of one position per thread made about two generations of
+// resident workgroups of ~7 us of dependent phases each (profiles/r05a_stamps_*); NSB = 2
+// makes one.
+template <int NSB>
+__global__ __launch_bounds__(kBS) void k_emit_shard_xp(TickArgs a) {
+    prefetch_args(a);
+    constexpr int R = kXGroupR;
+    static_assert(R < 64, "one 64-round chunk");
+    const int bid = blockIdx.x, t = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows (stamps builds)
+    STAMP(a, SO, 0);
+    // the other parity's exchange records, for the next tick's phase 1
+    for (int i = bid * kBS + t; i < a.xz_words; i += (int)gridDim.x * kBS) a.xz[i] = 0ull;
+    const int nqw = (a.nbq + NSB - 1) / NSB;
+    if (bid >= nqw) {
+        shard_compact(a, a.nbq + (bid - nqw));
+        return;
+    }
+    __shared__ uint32_t swc[NSB][kWaves][R + 1], sowc[NSB][kWaves][R + 1];
+    __shared__ uint32_t xred[kWaves][2], sfo[kWaves], sev[kWaves];
+    const int rr = min(lane, R - 1);
+    // ---- every load in flight at once: NSB positions per thread, their blocks' prefix rows
+    // (k_xscan: chunk-local + the chunk's), the totals and every rank's records
+    int cq[NSB], sq[NSB];
+    int32_t rq[NSB];
+    uint32_t pre[NSB], opre[NSB];
+#pragma unroll
+    for (int j = 0; j < NSB; ++j) {
+        const int b = min(bid * NSB + j, a.nbq - 1), ch = b / kXsBlocks;
+        const int64_t pos = (int64_t)(bid * NSB + j) * kBS + t;
+        const int64_t pq = pos < a.Qlog ? pos : (a.Qlog > 0 ? a.Qlog - 1 : 0);
+        cq[j] = xc_get(a, pq);
+        sq[j] = lq_slot(a, pq);
+        rq[j] = a.c_arr[pq];
+        pre[j] = a.xpre[(size_t)b * 2 * R + rr] + a.xct[(size_t)ch * 2 * R + rr];
+        opre[j] = a.xpre[(size_t)b * 2 * R + R + rr] + a.xct[(size_t)ch * 2 * R + R + rr];
+    }
+    const uint32_t A0 = a.xA[rr], oA0 = a.xA[R + rr];
+    const bool rin = t < a.world * kXRecLines;
+    const int gx = rin ? t : 0;
+    const unsigned long long xo = a.xrec[(size_t)gx * 16], xm = a.xrec[(size_t)gx * 16 + 1];
+#pragma unroll
+    for (int j = 0; j < NSB; ++j)
+        if ((int64_t)(bid * NSB + j) * kBS + t >= a.Qlog) cq[j] = 0;
+    {
+        const uint32_t orf = wave_sum_u32(rin ? (uint32_t)xo : 0u), mxr = wave_max_u32(rin ? (uint32_t)xm : 0u);
+        if (lane == 0) {
+            xred[w][0] = orf;
+            xred[w][1] = mxr;
+        }
+    }
+    STAMPW(a, SO, 1);
+    // ---- per sub-block and wave: counts of c > r (all / own lanes) from histograms of
+    // min(c, R) -- the in-block bases of the later waves
+#pragma unroll
+    for (int j = 0; j < NSB; ++j) {
+        const int c = cq[j];
+        const int oc = (c > 0 && own_slot(a, sq[j]) >= 0) ? c : 0;
+        uint32_t *ha = swc[j][w], *ho = sowc[j][w];
+        for (int i = lane; i <= R; i += 64) {
+            ha[i] = 0;
+            ho[i] = 0;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        atomicAdd(&ha[c < R ? c : R], 1u);
+        atomicAdd(&ho[oc < R ? oc : R], 1u);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        const uint32_t hv = lane < R ? ha[lane] : 0u, hw = lane < R ? ho[lane] : 0u;
+        const uint32_t Pa = wave_incl_scan_u32(hv), Po = wave_incl_scan_u32(hw);
+        __builtin_amdgcn_wave_barrier();
+        if (lane < R) {
+            ha[lane] = 64u - Pa;  // count(c > r) = 64 - #(lanes with min(c, R) <= r)
+            ho[lane] = 64u - Po;
+        }
+    }
+    int64_t O_loc = 0, n_ev = 0;
+    if (bid == 0) {
+        // this rank's orphans and evictions (its phase-1 tile counts) for the host
+        uint32_t fo = 0, ev = 0;
+        for (int i = t; i < a.nbf; i += kBS) fo += a.fcnt[i];
+        for (int i = t; i < a.nbw; i += kBS) ev += a.wcnt[i];
+        fo = wave_sum_u32(fo);
+        ev = wave_sum_u32(ev);
+        if (lane == 0) {
+            sfo[w] = fo;
+            sev[w] = ev;
+        }
+    }
+    __syncthreads();
+    if (bid == 0) {
+        O_loc = (int64_t)sfo[0] + sfo[1] + sfo[2] + sfo[3];
+        n_ev = (int64_t)sev[0] + sev[1] + sev[2] + sev[3];
+    }
+    STAMP(a, SO, 5);
+    // ---- the fill level (every wave alike; lane r = round r, one chunk)
+    const int64_t O = (int64_t)xred[0][0] + xred[1][0] + xred[2][0] + xred[3][0];
+    const int maxc = (int)max(max(xred[0][1], xred[1][1]), max(xred[2][1], xred[3][1]));
+    const int rlim = maxc < R ? maxc : R;
+    int64_t cap = (int64_t)wave_sum_u32(lane < R ? A0 : 0u);  // sum of c when max c <= R
+    if (maxc > R) cap = INT64_MAX;
+    const int64_t N = (a.redist ? O : 0) + a.T;
+    const int64_t N_eff = N < cap ? N : cap;
+    const uint32_t v = lane < rlim ? A0 : 0u, ov = lane < rlim ? oA0 : 0u;
+    const uint32_t incl = wave_incl_scan_u32(v), oincl = wave_incl_scan_u32(ov);
+    const int32_t Sv = (int32_t)(incl - v), Sov = (int32_t)(oincl - ov);  // S(r), So(r)
+    const int L = __popcll(__ballot(lane < rlim && (int64_t)incl <= N_eff));
+    const int64_t S_L = (int64_t)(uint32_t)__builtin_amdgcn_readlane(Sv, L);
+    const int64_t oSL = (int64_t)(uint32_t)__builtin_amdgcn_readlane(Sov, L);
+    int status = 0;
+    if (maxc > R && L >= R - 1) status = 1;
+    else if (a.head_local + N_eff > a.log_cap) status = 2;
+    const int64_t p = N_eff - S_L;
+    const int64_t AL = (L < maxc && L < rlim) ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)A0, L) : 0;
+    if (bid == 0 && t == 0) {
+        a.hout->O = O;
+        a.hout->O_local = O_loc;
+        a.hout->n_evicted = n_ev;
+        a.hout->cap_total = cap;
+        a.hout->maxc = maxc;
+        a.hout->L = L;
+        a.hout->status = status;
+        a.hout->N_eff = status ? 0 : N_eff;
+        a.hout->p = p;
+        a.hout->AL = AL;
+        if (!status && AL == 0) {
+            a.hout->new_qlen = 0;
+            a.hout->n_local = oSL;  // every worker saturated: all own capacity used
+        }
+    }
+    STAMP(a, SO, 6);
+    if (status) return;
+    int32_t *const lslot = a.log_slot + a.head_local;
+    uint32_t *const lseq = a.lseq_out + a.head_local;
+    const uint32_t hin = (uint32_t)a.head_in;
+    int32_t *const aall = a.assign_all;
+    char *const ab = a.arena;
+    const uint32_t so = (uint32_t)((char *)lslot - ab), qo = (uint32_t)((char *)lseq - ab);
+    const int L1 = L + 1;
+#pragma unroll
+    for (int j = 0; j < NSB; ++j) {
+        if (bid * NSB + j >= a.nbq) break;  // (uniform)
+        const int c = cq[j], s = sq[j];
+        const int ls = s >= 0 ? own_slot(a, s) : -1;
+        const bool own = c > 0 && ls >= 0;
+        const int oc = own ? c : 0;
+        // rank bases in A_r (global and own) and the task / own-log index bases per round
+        uint32_t sc = 0, osc = 0;
+#pragma unroll
+        for (int qq = 0; qq < kWaves - 1; ++qq) {
+            const bool in = qq < w && lane < R;
+            sc += in ? swc[j][qq][rr] : 0u;
+            osc += in ? sowc[j][qq][rr] : 0u;
+        }
+        const int32_t rbv = (int32_t)((lane < rlim ? pre[j] : 0u) + sc);
+        const int32_t orbv = (int32_t)((lane < rlim ? opre[j] : 0u) + osc);
+        const int32_t basev = Sv + rbv, obasev = Sov + orbv;
+        // ---- full rounds r < min(L, max own c of the wave) (assign_all: max c)
+        const int owmx = (int)wave_max_u32((uint32_t)(aall ? c : oc));
+        const int rfull = L < owmx ? L : owmx;
+        int i = 0;
+        if (a.arena32) {
+            for (; i + 3 < rfull; i += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = i + u;
+                    const uint64_t m = __ballot(c > r);
+                    const uint64_t om = __ballot(oc > r);
+                    const uint32_t base = (uint32_t)__builtin_amdgcn_readlane(basev, r);
+                    const uint32_t obase = (uint32_t)__builtin_amdgcn_readlane(obasev, r);
+                    if (oc > r) {
+                        const uint32_t lp4 = 4u * (obase + popc_lt(om));
+                        *reinterpret_cast<int32_t *>(ab + (so + lp4)) = s;
+                        *reinterpret_cast<uint32_t *>(ab + (qo + lp4)) = hin + base + popc_lt(m);
+                    }
+                    if (aall && c > r) aall[base + popc_lt(m)] = s;
+                }
+            }
+        }
+        for (; i < rfull; ++i) {
+            const uint64_t m = __ballot(c > i);
+            const uint64_t om = __ballot(oc > i);
+            const int base = __builtin_amdgcn_readlane(basev, i);
+            const int obase = __builtin_amdgcn_readlane(obasev, i);
+            if (oc > i) {
+                const int lp = obase + popc_lt(om);
+                lslot[lp] = s;
+                lseq[lp] = hin + (uint32_t)(base + popc_lt(m));
+            }
+            if (aall && c > i) aall[base + popc_lt(m)] = s;
+        }
+        // ---- round L (partial: ranks < p) and round L + 1 (ranks for the next queue)
+        const int rbL = __builtin_amdgcn_readlane(rbv, L);
+        const int orbL = __builtin_amdgcn_readlane(orbv, L);
+        const int rbL1 = __builtin_amdgcn_readlane(rbv, L1);
+        const uint64_t mL = __ballot(c > L);
+        const uint64_t omL = __ballot(oc > L);
+        const int64_t rankL = (int64_t)rbL + popc_lt(mL);
+        const int64_t orankL = (int64_t)orbL + popc_lt(omL);
+        if (oc > L && rankL < p) {
+            const int64_t lp = oSL + orankL;
+            lslot[lp] = s;
+            lseq[lp] = hin + (uint32_t)(S_L + rankL);
+        }
+        if (aall && c > L && rankL < p) aall[S_L + rankL] = s;
+        const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
+        if (c > 0) {
+            int64_t n_q = c < L ? c : L;
+            if (c > L && rankL < p) n_q += 1;
+            int64_t np = -1;
+            if (c > L) {
+                if (rankL >= p) np = rankL - p;
+                else if (c > L1) np = (AL - p) + exL1;
+                if (rankL == p) {
+                    // first position of round L left without a task: both queue and own-log lengths
+                    a.hout->new_qlen = (AL - p) + exL1;
+                    a.hout->n_local = oSL + orankL;
+                }
+            }
+            // the owned worker's next {free, queued} in one 8-byte store (the purge wrote {., 0})
+            if (own) a.free_out[ls] = make_int2(rq[j] - (int32_t)n_q, np >= 0 ? 1 : 0);
+            if (np >= 0) a.queue_out[np] = s;  // the next queue is replicated on every rank
+        }
+    }
+    STAMP(a, SO, 15);
 }
 
 // ---- compaction roles of k_emit_shard*, as in k_emit2: one wave per tile (a phase-1
@@ -4612,9 +4794,13 @@ void launch_emit_shard(const TickArgs &a, Stream st) {
         return;
     }
     const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
-    if (a.xplan)
-        hipExtLaunchKernelGGL((k_emit_shard<false, false, true>), g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
-    else if (a.xrows)
+    if (a.xplan) {
+        // two queue blocks per workgroup (k_emit_shard_xp)
+        const dim3 g2((a.nbq + 1) / 2 + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
+        hipExtLaunchKernelGGL(k_emit_shard_xp<2>, g2, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+        return;
+    }
+    if (a.xrows)
         hipExtLaunchKernelGGL(k_emit_shard<true, true>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
     else if (a.grp_on)
         hipExtLaunchKernelGGL(k_emit_shard<true, false>, g, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);

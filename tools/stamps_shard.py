@@ -52,7 +52,8 @@ nbw = max(1, -(-int(p0["n"]) // 256))
 nbf = -(-len(p0["log_slot"]) // 2048)
 SO = 3 * (nbw + nbf + nbq)
 d = np.stack([r[: (SO + nbq) * 16].reshape(-1, 16).astype(np.int64) for r in rows])[:, SO:SO + nbq, :]
-print("world %d, rank 0: %d queue blocks (stamp rows from %d)" % (args.world, nbq, SO))
+d = d[:, d[0, :, 13] > 0, :]  # (k_emit_shard_xp: one row per workgroup of 2 queue blocks)
+print("world %d, rank 0: %d queue blocks, %d stamped workgroups (stamp rows from %d)" % (args.world, nbq, d.shape[1], SO))
 span = (d[:, :, 14].max(axis=1) - d[:, :, 13].min(axis=1)) / 100.0
 print("queue-block span (realtime) median %.2f us" % np.median(span))
 st0 = (d[:, :, 13] - d[:, :, 13].min(axis=1, keepdims=True)) / 100.0
