@@ -9,6 +9,7 @@ block (:393-419), plus redistribution of the dead workers' in-flight tasks.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import weakref
 
 import numpy as np
@@ -22,6 +23,11 @@ _NONE = None
 # launch sequences of other table sizes on small, oracle-checkable inputs.  Test
 # fixtures set them (tests/test_gpu_parity.py); production code leaves this empty.
 TEST_PATHS = {}
+# ... or from the environment for same-box A/B runs (tools/ab_stream.sh):
+# FAASBAL_PATHS="spec_purge=0,xplan=1"
+for _kv in filter(None, os.environ.get("FAASBAL_PATHS", "").split(",")):
+    _k, _v = _kv.split("=")
+    TEST_PATHS[_k.strip()] = int(_v)
 
 
 def _p(a):
