@@ -329,8 +329,11 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
     tp = os.path.join(REPO, "profiles", "traffic.json")
     if os.path.exists(tp):
         tj = json.load(open(tp)).get("entries", {}).get("stream,%d,%d,%d" % (W, T, world))
-        if tj and dom in tj["kernels"]:
-            traffic = tj["kernels"][dom]["hbm_bytes"]
+        # (timer names -> the kernel symbols the PMC summary keys: the window tick's emit is
+        # k_emit_win, its apply k_ev_apply_ll)
+        dk = {"ev_apply": "ev_apply_ll", "emit": "emit_win"}.get(dom, dom)
+        if tj and dk in tj["kernels"]:
+            traffic = tj["kernels"][dk]["hbm_bytes"]
             traffic_src = ("profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch, separate rocprofv3 --pmc "
                            "passes; the x2 FETCH_SIZE correction is calibrated for streaming reads, so for random "
                            "gathers it is an upper bound)" % tj["tag"])
