@@ -412,6 +412,10 @@ struct TickArgs {
     uint32_t *xct;                 // [chunk][2R] chunk totals, turned into exclusive prefixes over the chunks
     uint32_t *xA;                  // [2R] totals A(r) (all, then this rank's)
     uint32_t *xtk;                 // k_xscan's ticket (zero between launches)
+    // one-GPU large tables with k_logscan (gp): no k_plan2 -- k_emit2's queue blocks reduce the
+    // group rows themselves and its compaction workgroups sum the tile counts before theirs
+    // (as the fused path does)
+    int gp;
     // sharded phase 2 (fb_set_full_assign): this rank also writes the whole tick's task -> slot
     // array (every rank computes the global water-filling; one rank's copy serves the host)
     int32_t *assign_all;

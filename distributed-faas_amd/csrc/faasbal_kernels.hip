@@ -1317,22 +1317,23 @@ __device__ __forceinline__ void wave_round_counts2(int c, uint64_t own, int r0, 
 
 // Sum of cnt[i] over i < n with all loads in flight at once (n <= kPeel*256 on
 // the fused path; a tail loop covers larger n); also the sum over i < lim.
+template <int PEEL = kPeel>
 __device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int n, int lim,
                                            unsigned long long &tot, unsigned long long &pre) {
-    uint32_t v[kPeel];
+    uint32_t v[PEEL];
 #pragma unroll
-    for (int k = 0; k < kPeel; ++k) {
+    for (int k = 0; k < PEEL; ++k) {
         const int i = threadIdx.x + k * kBS;
         v[k] = i < n ? cnt[i] : 0u;
     }
     tot = pre = 0;
 #pragma unroll
-    for (int k = 0; k < kPeel; ++k) {
+    for (int k = 0; k < PEEL; ++k) {
         const int i = threadIdx.x + k * kBS;
         tot += v[k];
         pre += i < lim ? v[k] : 0u;
     }
-    for (int i = threadIdx.x + kPeel * kBS; i < n; i += kBS) {
+    for (int i = threadIdx.x + PEEL * kBS; i < n; i += kBS) {
         const uint32_t x = cnt[i];
         tot += x;
         pre += i < lim ? x : 0u;
@@ -2877,10 +2878,14 @@ __device__ __forceinline__ int xcd_block(int i, int n) {
     return x * q + (x < r ? x : r) + y;
 }
 
-// PLAN: large tables (round table beyond the fused limit, R <= 128) -- the same
-// emission with this block's prefixes and the totals from k_plan.
-template <int MODE, bool PLAN, int NCH>
+// PM 1 (PLAN): large tables (round table beyond the fused limit, R <= 128) -- the same
+// emission with this block's prefixes and the totals from k_plan2.  PM 2 (gp): large tables
+// without k_plan2 -- the prefixes from the group rows as the fused path (PM 0) reads them,
+// the rest as PLAN's (segment counts in LDS, compaction offsets from fpre / wpre).
+template <int MODE, int PM, int NCH>
 __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
+    constexpr bool PLAN = PM == 1;  // prefixes and totals from k_plan2
+    constexpr bool BIG = PM != 0;   // large tables
     STAMP_TOP(a_, a_.nbw + a_.nbf + a_.nbq + (a_.slots_in_scan ? a_.nbw : 0));
     prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
@@ -2924,7 +2929,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         uint32_t segc[NCH];
         // large tables only: on the fused (configs[2]) path the histogram sits on the
         // critical path between the loads and the barrier (11.13 -> 11.45 us per tick)
-        constexpr bool kSegLds = PLAN;
+        constexpr bool kSegLds = BIG;
         __shared__ uint32_t shist[kWaves][kRFused + 1];
         __shared__ uint32_t sseg[kWaves][kRFused];
         if constexpr (kSegLds)
@@ -2996,6 +3001,23 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             const int g = b >> a.gshift, gsz = 1 << a.gshift, ng = a.ngrp;
             const int gs = a.gstride;
             uint32_t pre = 0, tot = 0;
+            const int nb_in = b - g * gsz;
+            if (PM == 2 && NCH == 1) {
+                // gp, R = 32 (P = 8): the <= 64 group rows and <= 63 earlier block rows in one
+                // load round, 8 + 8 per thread
+                uint32_t vg[8], vb[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    vg[j] = a.grp[min(p + P * j, ng - 1) * gs + r];
+                    vb[j] = a.qcnt[(size_t)(g * gsz + min(p + P * j, nb_in > 0 ? nb_in - 1 : 0)) * R + r];
+                }
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    const int gg = p + P * j;
+                    tot += gg < ng ? vg[j] : 0u;
+                    pre += (gg < g ? vg[j] : 0u) + (gg < nb_in ? vb[j] : 0u);
+                }
+            } else {
             // group rows g' = p + P j: totals, and the prefix of the groups before g
             for (int j0 = 0; j0 * P < ng; j0 += kGrpLd) {
                 uint32_t v[kGrpLd];
@@ -3009,7 +3031,6 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 }
             }
             // rows of the blocks of group g before b
-            const int nb_in = b - g * gsz;
             for (int j0 = 0; j0 * P < nb_in; j0 += kGrpLd) {
                 uint32_t v[kGrpLd];
 #pragma unroll
@@ -3019,6 +3040,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                 }
 #pragma unroll
                 for (int j = 0; j < kGrpLd; ++j) pre += p + P * (j0 + j) < nb_in ? v[j] : 0u;
+            }
             }
             // max c, orphans and evictions: columns R, R + 1, R + 2 of the group rows
             // (ngrp <= 64: wave 0 holds them)
@@ -3194,7 +3216,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // (one 1 KB trash row per block, 1024 rows: no line shared between blocks)
             int32_t *const tr = a.trash + (size_t)(blockIdx.x & (kTrashRows - 1)) * kBS + threadIdx.x;
             if (kDiagNow & 2) i = r1;
-            if (!PLAN && a.arena32) {
+            if (!BIG && a.arena32) {
                 // every buffer lies in the context's arena (< 4 GB): 32-bit byte offsets from
                 // one scalar base -- a select and a saddr store per round, no 64-bit math
                 char *const ab = a.arena;
@@ -3220,7 +3242,7 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
                     const bool act = c > r;
                     const uint64_t m = __ballot(act);
                     const int base = __builtin_amdgcn_readlane(basev[k], i + u);
-                    if constexpr (!PLAN) {
+                    if constexpr (!BIG) {
                         // select by mask arithmetic: a ?: on the pointers becomes an exec-masked block
                         const uint64_t pa = (uint64_t)(out + (base + (int)popc_lt(m))), pt = (uint64_t)tr;
                         wt_store((int32_t *)(pt ^ ((pa ^ pt) & (0ull - (uint64_t)act))), s);
@@ -3265,8 +3287,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         const int64_t *pre = frole ? a.fpre : a.wpre;
         off = pre[t < ntile ? t : ntile - 1];
     } else {
+        // the workgroup sums the counts of the tiles before its own (gp: up to 4096 tiles,
+        // 16 loads per thread in flight at once)
         unsigned long long tot, pre;
-        peeled_sum(cnt, t0, t0, tot, pre);
+        if constexpr (PM == 2) peeled_sum<16>(cnt, t0, t0, tot, pre);
+        else peeled_sum<kPeel>(cnt, t0, t0, tot, pre);
         const uint32_t ws = wave_sum_u32((uint32_t)pre);
         if (lane == 0) red[w][0] = ws;
         lds_barrier();
@@ -4766,25 +4791,28 @@ void launch_xscan(const TickArgs &a, Stream st) {
 void launch_emit(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_emit, dim3(a.nbq + a.nbf + a.nbw), 0, st, a);
 }
-template <bool PLAN, int NCH>
+template <int PM, int NCH>
 static void launch_emit2_t(const TickArgs &a, Stream st) {
     const dim3 g(a.nbq + (a.f_emit ? a.nbf : (a.nbf + 3) / 4) + (a.nbw + 3) / 4);
     // f_emit: the log workgroups stage the died bitmap in LDS (rounded to whole int4)
     const size_t lds = a.f_emit ? (size_t)(((a.W + 63) / 64 + 1) / 2) * 16 : 0;
     switch (tick_mode(a)) {
-    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PLAN, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
-    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PLAN, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
-    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PLAN, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    case kModeIdle: hipExtLaunchKernelGGL((k_emit2<kModeIdle, PM, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    case kModeEvents: hipExtLaunchKernelGGL((k_emit2<kModeEvents, PM, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    default: hipExtLaunchKernelGGL((k_emit2<kModeDeque, PM, NCH>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
     }
 }
 void launch_emit2(const TickArgs &a, Stream st) {
     // one 64-round chunk while rounds 0 .. L+1 <= R+1 fit in a wave's lanes (R = 32)
     if (a.fused) {
-        if (a.R <= 32) launch_emit2_t<false, 1>(a, st);
-        else launch_emit2_t<false, 3>(a, st);
+        if (a.R <= 32) launch_emit2_t<0, 1>(a, st);
+        else launch_emit2_t<0, 3>(a, st);
+    } else if (a.gp) {
+        if (a.R <= 32) launch_emit2_t<2, 1>(a, st);
+        else launch_emit2_t<2, 3>(a, st);
     } else {
-        if (a.R <= 32) launch_emit2_t<true, 1>(a, st);
-        else launch_emit2_t<true, 3>(a, st);
+        if (a.R <= 32) launch_emit2_t<1, 1>(a, st);
+        else launch_emit2_t<1, 3>(a, st);
     }
 }
 void launch_emit_shard(const TickArgs &a, Stream st) {

@@ -472,7 +472,21 @@ def test_random_multitick_logscan(logscan, seed):
 
 @pytest.mark.parametrize("seed", range(6))
 def test_random_multitick_logscan_plan(logscan, force_plan, seed):
+    """Large-table path with k_logscan: no k_plan2 (k_emit2 reduces the group rows, the last
+    k_logscan workgroup writes the tile prefixes -- the configs[3] default)."""
     test_random_multitick_vs_oracle(seed + 20)
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_multitick_logscan_plan2(logscan, force_plan, monkeypatch, seed):
+    """... and the same ticks through k_plan2 (fb_set_path("gp", 0))."""
+    monkeypatch.setitem(TEST_PATHS, "gp", 0)
+    test_random_multitick_vs_oracle(seed + 20)
+
+
+def test_config3_logscan_plan2(logscan, force_plan, monkeypatch):
+    monkeypatch.setitem(TEST_PATHS, "gp", 0)
+    test_config3_full_size()
 
 
 def test_config3_logscan(logscan):

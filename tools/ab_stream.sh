@@ -9,6 +9,6 @@ for rep in 1 2; do
   for e in "$@"; do
     i=$((i+1))
     env $e timeout -k 10 300 python -u bench.py --workload stream $AB_ARGS > gpurun_out/${TAG}_${i}_${rep}.json 2>/dev/null || exit 1
-    python -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_${i}_${rep}.json')); print('%-28s %.1f us/tick, kernels %.1f' % ('$e', d['ms_per_step']*1e3, d['tick']['device_us_per_tick']))"
+    python -c "import json,sys; d=json.load(open('gpurun_out/${TAG}_${i}_${rep}.json')); print('%-28s %.1f us/tick, kernels %.1f' % ('$e', d['ms_per_step']*1e3, d['tick'].get('device_us_per_tick', d['tick'].get('device_ms', 0) * 1e3)))"
   done
 done
