@@ -138,6 +138,12 @@ def report(d, nbw, nbf, nbq, split, fsep, femit=False):
         span = (ext.max(axis=1) - ent.min(axis=1)) / 100.0
         spread = (ent.max(axis=1) - ent.min(axis=1)) / 100.0
         print("%-6s span %.2f us (median), entry spread %.2f us" % (kern, np.median(span), np.median(spread)))
+        # resident blocks: mean (block-time / span) and the peak, first rep
+        e0, x0 = ent[0], ext[0]
+        ev = np.concatenate([np.stack([e0, np.ones_like(e0)], 1), np.stack([x0, -np.ones_like(x0)], 1)])
+        ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
+        print("       resident blocks: mean %.0f, peak %d" % ((x0 - e0).sum() / max(1, x0.max() - e0.min()),
+                                                              int(np.cumsum(ev[:, 1]).max())))
         top = d[:, lo:hi, 12]
         if (top > 0).all():
             # realtime at the top of the kernel, before the argument copy
