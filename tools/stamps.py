@@ -144,6 +144,12 @@ def report(d, nbw, nbf, nbq, split, fsep, femit=False):
         ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
         print("       resident blocks: mean %.0f, peak %d" % ((x0 - e0).sum() / max(1, x0.max() - e0.min()),
                                                               int(np.cumsum(ev[:, 1]).max())))
+        # blocks entering / leaving per microsecond (first rep)
+        nb = int((x0.max() - e0.min()) // 100) + 1
+        hin = np.bincount(((e0 - e0.min()) // 100).astype(int), minlength=nb)
+        hout = np.bincount(((x0 - e0.min()) // 100).astype(int), minlength=nb)
+        print("       entering per us:", " ".join(str(int(v)) for v in hin))
+        print("       leaving  per us:", " ".join(str(int(v)) for v in hout))
         top = d[:, lo:hi, 12]
         if (top > 0).all():
             # realtime at the top of the kernel, before the argument copy
