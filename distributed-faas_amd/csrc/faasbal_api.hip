@@ -289,6 +289,7 @@ struct fb_ctx {
     uint32_t *xg_acc = nullptr, *xg_tk = nullptr, *ogrp = nullptr;  // exchanged group rows (phase 1 -> 2)
     uint32_t *xs_tk = nullptr;                        // k_xscan's ticket
     int gp_on = 1;                                    // fb_set_path("gp", 0): large one-GPU tables run k_plan2
+    int gpcheck = 0;                                  // fb_set_path("gpcheck", 1): diagnostic (stamps builds)
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
     bool l_full = false;                              // ... and the last launch did
@@ -1235,8 +1236,10 @@ int enqueue_tick(fb_ctx *c) {
     // large one-GPU tables (<= 64 group rows): no k_plan2 -- k_emit2's queue blocks reduce
     // the group rows, its compaction workgroups the tile counts before theirs
     if (!a.fused && a.segw && a.grp_on && !c->shard && !c->deque && !c->l_win && c->gp_on && nbf <= 4096 * 4 &&
-        nbw <= 4096 * 4)
+        nbw <= 4096 * 4) {
         a.gp = 1;
+        a.gpcheck = c->gpcheck;
+    }
     if (!a.slots_in_scan && !a.slots_in_apply) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
@@ -1249,7 +1252,7 @@ int enqueue_tick(fb_ctx *c) {
         Timer t(c, "logscan");
         launch_logscan(a, ls_grid, t.st());
     }
-    if (!a.fused && !a.gp) {
+    if (!a.fused && (!a.gp || a.gpcheck)) {
         Timer t(c, "plan");
         launch_plan(a, t.st());
     }
@@ -2864,6 +2867,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "fault_qlen") c->fault_qlen = value;
     else if (n == "xplan" && (value == 0 || value == 1)) c->xplan_on = value;
     else if (n == "gp" && (value == 0 || value == 1)) c->gp_on = value;
+    else if (n == "gpcheck" && (value == 0 || value == 1)) c->gpcheck = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }

@@ -416,6 +416,7 @@ struct TickArgs {
     // group rows themselves and its compaction workgroups sum the tile counts before theirs
     // (as the fused path does)
     int gp;
+    int gpcheck;  // (stamps builds: k_plan2 runs too, k_emit2 records both prefixes)
     // sharded phase 2 (fb_set_full_assign): this rank also writes the whole tick's task -> slot
     // array (every rank computes the global water-filling; one rank's copy serves the host)
     int32_t *assign_all;

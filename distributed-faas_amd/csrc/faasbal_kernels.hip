@@ -3002,9 +3002,9 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             const int gs = a.gstride;
             uint32_t pre = 0, tot = 0;
             const int nb_in = b - g * gsz;
-            if (PM == 2 && NCH == 1) {
-                // gp, R = 32 (P = 8): the <= 64 group rows and <= 63 earlier block rows in one
-                // load round, 8 + 8 per thread
+            if (PM == 2 && NCH == 1 && gsz <= 64) {
+                // gp, R = 32 (P = 8), groups of <= 64 blocks: the <= 64 group rows and <= 63
+                // earlier block rows in one load round, 8 + 8 per thread
                 uint32_t vg[8], vb[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
@@ -3090,6 +3090,21 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             }
         }
         STAMP(a, SO, 1);
+#ifdef FAASBAL_STAMPS
+        if constexpr (PM == 2) {
+            // (diagnostic, fb_set_path("gpcheck", 1): k_plan2 ran too; this block's round-0
+            // prefix beside k_plan2's)
+            if (a.gpcheck && threadIdx.x == 0) {
+                unsigned long long *row = a.dbg + (size_t)(3 * (a.nbw + a.nbf + a.nbq) + 1024 + b) * 16;
+                row[0] = (unsigned long long)b + 1;
+                row[1] = prev[0];
+                row[2] = (uint32_t)a.qpre[(size_t)b * R];
+                row[3] = (unsigned long long)(b >> a.gshift);
+                row[4] = totv[0];
+                row[5] = (unsigned long long)a.gshift;
+            }
+        }
+#endif
 #pragma unroll
         for (int k = 0; k < NCH && kSegLds; ++k) {
             const int r = min(64 * k + lane, kRFused - 1);
