@@ -359,14 +359,17 @@ def test_device_reported_lengths_are_validated(window):
     copy uses it: a queue length past the buffer (injected into the results) fails the
     tick with FB_EHIP naming the number; the tick is not committed and the next one runs
     against the oracle as if it never happened."""
-    st = synth.zipf_state(W=2048, seed=3)
+    # nobody dead and a frozen clock: both ticks stay at fill level 0, so with window ticks
+    # on the second one is a window tick (a death's orphans would lift it to level 1: a
+    # general tick after the window attempt)
+    st = synth.zipf_state(W=2048, seed=3, dead_frac=0.0)
     g, o = _pair(st, len(st["log"]) * 2 + 100_000)
     g.set_window(window)
-    args = (1000.0, 10.0, [], [], [], [], [], 500)   # fill level 0: the next tick may be a window tick
+    args = (1000.0, 10.0, [], [], [], [], [], 500)
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)
     g.set_path("fault_qlen", 1 << 30)
-    args = (1001.0, 10.0, [synth.EV_HEARTBEAT], [5], [0], [1000.5], [-1], 300)
+    args = (1000.0, 10.0, [synth.EV_HEARTBEAT], [5], [0], [1000.0], [-1], 300)
     with pytest.raises(FaasbalError, match="queue length|window"):
         g.tick(*args)
     a, b = g.tick(*args), o.tick(*args)
