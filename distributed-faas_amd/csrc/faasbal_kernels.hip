@@ -771,6 +771,14 @@ __global__ __launch_bounds__(kBS) void k_ev_apply(EvArgs a) {
 // One slot's commit: t = the slot got messages this tick.
 __device__ __forceinline__ void commit_slot(const CommitArgs &a, int s, bool t, int64_t wq_head) {
     const uint8_t stt = a.st[s];
+    // the second load round at once, branch-free (clamped addresses: an untouched slot
+    // reads slot 0's line, a slot not queued at tick start slot 0's position): the
+    // post-message record and flags of a touched slot, the committed position of a queued one
+    const int sc = t ? s : 0;
+    const PostRec pr = a.post[sc];
+    const uint8_t rf = a.win ? a.post_rf[sc] : (uint8_t)0;
+    const int32_t p = a.win ? a.pos[(stt & kStQ0) ? s : 0] : -1;  // exact for a queued slot
+    const int32_t bn = a.bud ? a.bud_next[sc] : 0;
     if (a.win) {
         // window tick: the committed position of a slot queued at tick start that the tick
         // did not serve -- tombstoned when the slot died or its messages took it out of the
@@ -779,14 +787,12 @@ __device__ __forceinline__ void commit_slot(const CommitArgs &a, int s, bool t, 
         // moved to the front or the back were recorded by k_emit_win (the tomb list above):
         // they may also be appended, so their pos is rewritten in this launch.
         if ((stt & kStQ0) && (t || !(stt & kStAlive))) {
-            const int qs = t ? (a.post_rf[s] >> 2) & 3 : kQsKeep;
+            const int qs = t ? (rf >> 2) & 3 : kQsKeep;
             if (!(stt & kStAlive) || qs == kQsOut || qs == kQsKeep) {
-                const int32_t p = a.pos[s];  // exact for a queued slot
                 if (p >= wq_head && p < a.wq_tail) {
                     if (!(stt & kStAlive) || qs == kQsOut) {
                         a.wqf[p] = kTomb;
                     } else {
-                        const PostRec pr = a.post[s];
                         a.wqf[p] = pr.free;
                         a.wqh[p] = pr.hb;
                     }
@@ -797,11 +803,10 @@ __device__ __forceinline__ void commit_slot(const CommitArgs &a, int s, bool t, 
     // committed hb is NaN for slots without a record (k_scan's log role relies on it)
     if (t) {
         const bool alive = (stt & kStAlive) != 0;
-        const PostRec pr = a.post[s];
         a.reg[s] = alive ? 1 : 0;
         a.hb[s] = alive ? pr.hb : __builtin_nan("");
         a.epoch[s] = pr.epoch;
-        if (a.bud) a.bud[s] = a.bud_next[s];
+        if (a.bud) a.bud[s] = bn;
     } else if (stt & kStEvicted) {
         a.reg[s] = 0;
         a.hb[s] = __builtin_nan("");
@@ -1972,12 +1977,14 @@ __device__ __forceinline__ WinEl win_elem(const TickArgs &a, int reg, int64_t i,
         const int sq = a.wq_buf[ic];
         const int32_t fq = a.wqf_buf[ic];
         const double hq = a.wqh_buf[ic];
+        // the touched bit and the post-message record in one load round (the record of an
+        // untouched slot is loaded and ignored: a dependent round costs more than the line)
         const bool tq = got_msg(a, sq);
+        const uint8_t rf = a.post_rf[sq];
+        const PostRec pr = a.post[sq];
         int32_t raw = ((a.now - hq) > a.tte) ? INT32_MIN : fq;
         double hb = hq;
         if (tq) {
-            const uint8_t rf = a.post_rf[sq];
-            const PostRec pr = a.post[sq];
             hb = pr.hb;
             raw = ((rf & 1) && !((a.now - pr.hb) > a.tte) && ((rf >> 2) & 3) == kQsKeep) ? pr.free : INT32_MIN;
         }
