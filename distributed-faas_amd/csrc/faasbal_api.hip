@@ -289,6 +289,7 @@ struct fb_ctx {
     uint32_t *xg_acc = nullptr, *xg_tk = nullptr, *ogrp = nullptr;  // exchanged group rows (phase 1 -> 2)
     uint32_t *xs_tk = nullptr;                        // k_xscan's ticket
     int gp_on = 1;                                    // fb_set_path("gp", 0): large one-GPU tables run k_plan2
+    int win_direct = 1;                               // fb_set_path("win_direct", 0): k_emit_win chunks by ticket
     int gpcheck = 0;                                  // fb_set_path("gpcheck", 1): diagnostic (stamps builds)
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
@@ -1152,6 +1153,9 @@ int enqueue_tick(fb_ctx *c) {
         a.tomb = c->tomb;
         a.lstamp = c->lstamp;
         const int nch = a.nchB + a.nchF + a.nchW;
+        // few enough chunks to be resident together (k_emit_win holds 6 workgroups per CU):
+        // chunk = workgroup index, no ticket round before the element loads
+        a.win_direct = (c->win_direct && nch <= 4 * c->ncu) ? 1 : 0;
         a.lpart = c->lpart;
         a.died_tag = c->died_tag;
         a.n_lpart = head > 0 ? ls_grid : 0;
@@ -2867,6 +2871,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "fault_qlen") c->fault_qlen = value;
     else if (n == "xplan" && (value == 0 || value == 1)) c->xplan_on = value;
     else if (n == "gp" && (value == 0 || value == 1)) c->gp_on = value;
+    else if (n == "win_direct" && (value == 0 || value == 1)) c->win_direct = value;
     else if (n == "gpcheck" && (value == 0 || value == 1)) c->gpcheck = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;

@@ -3437,12 +3437,14 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
     __shared__ uint32_t xs[8];
     const int tid = threadIdx.x, lane = lane_id(), w = wave_id();
     STAMP(a, kWinStampRow, 0);
-    if (tid == 0) xs[0] = atomicAdd(a.wticket, 1u);  // chunk = ticket: predecessors already run
+    // chunk = ticket (predecessors already run), or the workgroup index when every chunk is
+    // resident at once (win_direct: no atomic round before the element loads)
+    if (!a.win_direct && tid == 0) xs[0] = atomicAdd(a.wticket, 1u);
     // the orphan partials of the log workgroups and the purge's eviction / queued partials
     const uint32_t op = tid < a.n_lpart ? a.lpart[tid] : 0u;
     const uint32_t e0 = tid < 64 ? a.wpart[(size_t)tid * 32] : 0u, q0 = tid < 64 ? a.wpart[(size_t)tid * 32 + 1] : 0u;
-    lds_barrier();
-    const int ch = (int)xs[0];
+    if (!a.win_direct) lds_barrier();
+    const int ch = a.win_direct ? (int)blockIdx.x : (int)xs[0];
     int64_t i0, i1;
     const int reg = win_region(a, ch, i0, i1);
     // ---- this chunk's elements: classification (loads in flight), in-chunk ranks

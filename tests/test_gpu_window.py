@@ -327,3 +327,12 @@ def test_large_table_window_stream_vs_oracle(eager):
     wt, fb = g.window_stats()
     assert wt >= 3 and n_orph > 0, (wt, fb, n_orph)
     g.close()
+
+
+@pytest.mark.parametrize("seed", range(0, 24, 4))
+def test_window_random_ticketed_chunks_vs_oracle(monkeypatch, seed):
+    """k_emit_win with its chunks taken by ticket (fb_set_path("win_direct", 0): the form
+    for grids too large to be resident at once) instead of by workgroup index."""
+    from faasbal.balancer import TEST_PATHS
+    monkeypatch.setitem(TEST_PATHS, "win_direct", 0)
+    test_window_random_vs_oracle(seed)
