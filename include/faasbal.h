@@ -265,7 +265,15 @@ int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_to
  *   "logscan"     -1 auto, 0 never, 1 the log role as its own k_logscan launch;
  *   "split_slots" -1 auto, 0 never, 1 the slot purge as its own k_slots launch;
  *   "ev_ll"       1 per-slot linked lists (one GPU), 0 the radix sort of messages;
- *   "rs_wide"     1 digits up to 11 bits while a batch has <= 4096 sort tiles, 0 8-bit.
+ *   "rs_wide"     1 digits up to 11 bits while a batch has <= 4096 sort tiles, 0 8-bit;
+ *   "xplan"       sharded: 1 large queues exchange digit rows scanned by k_xscan, 0 a
+ *                 phase-2 k_scan re-counts them;
+ *   "gp"          one GPU, large tables: 1 k_emit2 reduces the group rows itself, 0 k_plan2;
+ *   "win_direct"  window ticks: 1 k_emit_win chunk = workgroup index when every chunk is
+ *                 resident at once, 0 always by ticket;
+ *   "fault_qlen"  test hook: the next waited tick reports this queue length (checked and
+ *                 refused by fb_tick_wait when it exceeds the buffer; -1 off);
+ *   "gpcheck"     diagnostic (stamps builds): k_plan2 runs beside a gp tick for comparison.
  * Between ticks only; FB_EINVAL for an unknown name or value. */
 int fb_set_path(fb_ctx *ctx, const char *name, int value);
 
