@@ -3009,21 +3009,29 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             const int gs = a.gstride;
             uint32_t pre = 0, tot = 0;
             const int nb_in = b - g * gsz;
-            if (PM == 2 && NCH == 1 && gsz <= 64) {
-                // gp, R = 32 (P = 8), groups of <= 64 blocks: the <= 64 group rows and <= 63
-                // earlier block rows in one load round, 8 + 8 per thread
+            // gp, R = 32, groups of <= 64 blocks: the <= 64 group rows and <= 63 earlier block
+            // rows in one load round, 8 + 8 per thread, a column per lane (c = t & 31) and a
+            // row class per half wave (rows q + 8 j, q = t >> 5): every wave load covers two
+            // whole rows; the 8 row classes of a column are summed by a cross-half shuffle and
+            // the 4 waves' partials after the block barrier
+            const bool trp = PM == 2 && NCH == 1 && gsz <= 64;
+            if (trp) {
+                const int cc = (int)threadIdx.x & 31, q = (int)threadIdx.x >> 5;
                 uint32_t vg[8], vb[8];
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    vg[j] = a.grp[min(p + P * j, ng - 1) * gs + r];
-                    vb[j] = a.qcnt[(size_t)(g * gsz + min(p + P * j, nb_in > 0 ? nb_in - 1 : 0)) * R + r];
+                    const int i = q + 8 * j;
+                    vg[j] = a.grp[min(i, ng - 1) * gs + cc];
+                    vb[j] = a.qcnt[(size_t)(g * gsz + min(i, nb_in > 0 ? nb_in - 1 : 0)) * R + cc];
                 }
 #pragma unroll
                 for (int j = 0; j < 8; ++j) {
-                    const int gg = p + P * j;
-                    tot += gg < ng ? vg[j] : 0u;
-                    pre += (gg < g ? vg[j] : 0u) + (gg < nb_in ? vb[j] : 0u);
+                    const int i = q + 8 * j;
+                    tot += i < ng ? vg[j] : 0u;
+                    pre += (i < g ? vg[j] : 0u) + (i < nb_in ? vb[j] : 0u);
                 }
+                pre += (uint32_t)__shfl_xor((int)pre, 32);
+                tot += (uint32_t)__shfl_xor((int)tot, 32);
             } else {
             // group rows g' = p + P j: totals, and the prefix of the groups before g
             for (int j0 = 0; j0 * P < ng; j0 += kGrpLd) {
@@ -3053,19 +3061,26 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             // (ngrp <= 64: wave 0 holds them)
             const int gi = min((int)threadIdx.x, ng - 1) * gs + R;
             const uint32_t mg = a.grp[gi], og = a.grp[gi + 1], eg = a.grp[gi + 2];
-            if (P == 8) {
-                pre = group_sum<8>(pre);
-                tot = group_sum<8>(tot);
-            } else if (P == 4) {
-                pre = group_sum<4>(pre);
-                tot = group_sum<4>(tot);
+            if (trp) {
+                if (lane < 32) {
+                    gpre[w * 32 + lane] = pre;
+                    gtot[w * 32 + lane] = tot;
+                }
             } else {
-                pre = group_sum<2>(pre);
-                tot = group_sum<2>(tot);
-            }
-            if (p == 0) {
-                gpre[r] = pre;
-                gtot[r] = tot;
+                if (P == 8) {
+                    pre = group_sum<8>(pre);
+                    tot = group_sum<8>(tot);
+                } else if (P == 4) {
+                    pre = group_sum<4>(pre);
+                    tot = group_sum<4>(tot);
+                } else {
+                    pre = group_sum<2>(pre);
+                    tot = group_sum<2>(tot);
+                }
+                if (p == 0) {
+                    gpre[r] = pre;
+                    gtot[r] = tot;
+                }
             }
 #pragma unroll
             for (int k = 0; k < NCH; ++k)
@@ -3092,8 +3107,14 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
 #pragma unroll
             for (int k = 0; k < NCH; ++k) {
                 const int rr = 64 * k + lane;
-                prev[k] = rr < R ? gpre[rr] : 0u;
-                totv[k] = rr < R ? gtot[rr] : 0u;
+                if (trp) {
+                    const int rc = rr < 32 ? rr : 31;
+                    prev[k] = rr < R ? gpre[rc] + gpre[32 + rc] + gpre[64 + rc] + gpre[96 + rc] : 0u;
+                    totv[k] = rr < R ? gtot[rc] + gtot[32 + rc] + gtot[64 + rc] + gtot[96 + rc] : 0u;
+                } else {
+                    prev[k] = rr < R ? gpre[rr] : 0u;
+                    totv[k] = rr < R ? gtot[rr] : 0u;
+                }
             }
         }
         STAMP(a, SO, 1);
