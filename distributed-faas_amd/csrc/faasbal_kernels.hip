@@ -3520,6 +3520,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
     if (w == 0) {
         uint32_t elv, eg1, emx, LB = 0, bmax = 0;
         bool ok = gr_lookback(gch, ci, reg == 0 ? tl : tl, reg == 0 ? 0u : tg, bmx, elv, eg1, emx);
+        STAMP(a, kWinStampRow, 4);
         // front / window chunks append after the live backs: the back chain's total
         if (ok && reg != 0) ok = gr_wait_incl(a.wlb, a.nchB - 1, LB, bmax);
         if (lane == 0) {

@@ -22,6 +22,7 @@ g = GpuBalancer(W, len(st["log"]) + (K + 8) * 2 * T, max_events=E,
 g.load(st)
 carried = 0
 res = []
+split = []
 for i, tk in enumerate(ticks):
     n = carried + tk["n_new"]
     g.tick(tk["now"], 10.0, tk["ev_kind"], tk["ev_slot"], tk["ev_val"], tk["ev_ts"], tk["ev_seq"], n_pending=n,
@@ -36,8 +37,21 @@ for i, tk in enumerate(ticks):
         res.append([len(rows), np.median(full[:, 1] - full[:, 0]), np.median(full[:, 2] - full[:, 1]),
                     np.percentile(rows[:, 15] - rows[:, 2], 90), np.percentile((rows[:, 13] - e0) / 100.0, 100),
                     np.percentile((rows[:, 14] - e0) / 100.0, 50), np.percentile((rows[:, 14] - e0) / 100.0, 100)])
+        nb = -(-len(tk["ev_kind"]) // 1024)  # back chunks come first (chunk = row)
+        ix = np.nonzero((d[:, 13] > 0) & (d[:, 14] > newest - 10000) & (d[:, 15] > 0))[0]
+        back, rest = rows[ix < nb], rows[ix >= nb]
+        fr = rest[rest[:, 4] > 0]
+        split.append([np.median(back[:, 4] - back[:, 1]) if len(back) else 0,
+                      np.median(fr[:, 4] - fr[:, 1]) if len(fr) else 0,
+                      np.median(fr[:, 2] - fr[:, 4]) if len(fr) else 0,
+                      (back[:, 14].max() - e0) / 100.0 if len(back) else 0,
+                      (rest[:, 14].max() - e0) / 100.0 if len(rest) else 0])
     g.commit()
     carried = n + int(r["n_orphans"]) - int(r["n_assigned"])
 m = np.median(np.array(res), axis=0)
 print("k_emit_win: %d chunks; classify %d cyc, look-back %d cyc, emission p90 %d cyc (medians); "
       "entry max +%.2f us, exit p50 +%.2f / max +%.2f us" % tuple(m))
+if split:
+    m2 = np.median(np.array(split), axis=0)
+    print("  back chunks: own chain %d cyc, last exit +%.2f us; front / window chunks: own chain %d cyc, "
+          "wait for the back total %d cyc, last exit +%.2f us" % (m2[0], m2[3], m2[1], m2[2], m2[4]))
