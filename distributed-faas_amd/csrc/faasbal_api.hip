@@ -290,6 +290,7 @@ struct fb_ctx {
     uint32_t *xs_tk = nullptr;                        // k_xscan's ticket
     int gp_on = 1;                                    // fb_set_path("gp", 0): large one-GPU tables run k_plan2
     int win_direct = 1;                               // fb_set_path("win_direct", 0): k_emit_win chunks by ticket
+    int xself_on = 1;                                 // fb_set_path("xself", 0): k_xscan's last workgroup prefixes the chunks
     int gpcheck = 0;                                  // fb_set_path("gpcheck", 1): diagnostic (stamps builds)
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
@@ -1073,6 +1074,8 @@ int enqueue_tick(fb_ctx *c) {
         a.xrec = (unsigned long long *)(c->xbuf + xl.rec) + (size_t)c->xpar * xrw;
         a.xrows = xrb ? c->xbuf + xl.rows : nullptr;
         a.xplan = (c->xplan_on && xrows_mode(c->world, R, Qlog) == 2) ? 1 : 0;
+        // (<= 64 chunks of kXsBlocks queue blocks: 16 loads per k_emit_shard_xp thread)
+        a.xself = (a.xplan && c->xself_on && cdiv(Qlog, kBS) <= 64 * kXsBlocks) ? 1 : 0;
         c->l_full = c->full_assign != 0;
         if (c->l_full && c->phase == 2) {
             // the whole tick's assignments: at most its pending tasks plus every in-flight entry
@@ -2872,6 +2875,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "xplan" && (value == 0 || value == 1)) c->xplan_on = value;
     else if (n == "gp" && (value == 0 || value == 1)) c->gp_on = value;
     else if (n == "win_direct" && (value == 0 || value == 1)) c->win_direct = value;
+    else if (n == "xself" && (value == 0 || value == 1)) c->xself_on = value;
     else if (n == "gpcheck" && (value == 0 || value == 1)) c->gpcheck = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;

@@ -357,7 +357,8 @@ struct TickArgs {
     int32_t *wq_buf, *wqf_buf;
     double *wqh_buf;
     int nchB, nchF, nchW;
-    int win_direct;  // k_emit_win: chunk = workgroup index (every chunk resident at once), else a ticket
+    int win_direct;
+    int xself;       // xplan ticks with <= 64 chunks: k_emit_shard_xp prefixes the chunk totals itself  // k_emit_win: chunk = workgroup index (every chunk resident at once), else a ticket
     unsigned long long *wlb;     // look-back granules: [0, nchB) the back chain, then the front / window chain
     uint32_t *wticket;           // chunk tickets (zeroed by k_ev_link)
     int64_t *cw;                 // commit word {failed, window head, window length} (eager commits)

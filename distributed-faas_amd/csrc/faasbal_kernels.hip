@@ -2254,6 +2254,10 @@ __global__ __launch_bounds__(kBS) void k_xscan(TickArgs a) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) my = lane == j ? tot[j] : my;
     if (lane < 16) a.xct[(size_t)ch * C + 16 * w + lane] = my;
+    if (a.xself) {  // k_emit_shard_xp sums the chunk totals itself
+        STAMP(a, SO, 15);
+        return;
+    }
     // every wave's stores done, then the ticket (release / acquire at agent scope)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -4229,6 +4233,30 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_xp(TickArgs a) {
     int cq[NSB], sq[NSB];
     int32_t rq[NSB];
     uint32_t pre[NSB], opre[NSB];
+    // xself (<= 64 chunks): k_xscan left the chunks' raw totals; this workgroup sums them
+    // itself -- column col = t & 63 of the 2R, chunks part + 4 i (part = t >> 6), 16 loads in
+    // flight per thread -- into its chunks' prefixes and the totals (no ticket, no serial
+    // last workgroup in k_xscan)
+    __shared__ uint32_t cps[3][4][2 * R];
+    const int nch = (a.nbq + kXsBlocks - 1) / kXsBlocks;
+    const int ch0 = min(bid * NSB, a.nbq - 1) / kXsBlocks, ch1 = min(bid * NSB + NSB - 1, a.nbq - 1) / kXsBlocks;
+    uint32_t xt = 0, xp0 = 0, xp1 = 0;
+    if (a.xself) {
+        const int col = t & (2 * R - 1), part = t >> 6;
+        uint32_t x[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) x[i] = a.xct[(size_t)min(part + 4 * i, nch - 1) * 2 * R + col];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int k = part + 4 * i;
+            xt += k < nch ? x[i] : 0u;
+            xp0 += k < ch0 ? x[i] : 0u;
+            xp1 += k < ch1 ? x[i] : 0u;
+        }
+        cps[0][part][col] = xt;
+        cps[1][part][col] = xp0;
+        cps[2][part][col] = xp1;
+    }
 #pragma unroll
     for (int j = 0; j < NSB; ++j) {
         const int b = min(bid * NSB + j, a.nbq - 1), ch = b / kXsBlocks;
@@ -4237,10 +4265,10 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_xp(TickArgs a) {
         cq[j] = xc_get(a, pq);
         sq[j] = lq_slot(a, pq);
         rq[j] = a.c_arr[pq];
-        pre[j] = a.xpre[(size_t)b * 2 * R + rr] + a.xct[(size_t)ch * 2 * R + rr];
-        opre[j] = a.xpre[(size_t)b * 2 * R + R + rr] + a.xct[(size_t)ch * 2 * R + R + rr];
+        pre[j] = a.xpre[(size_t)b * 2 * R + rr] + (a.xself ? 0u : a.xct[(size_t)ch * 2 * R + rr]);
+        opre[j] = a.xpre[(size_t)b * 2 * R + R + rr] + (a.xself ? 0u : a.xct[(size_t)ch * 2 * R + R + rr]);
     }
-    const uint32_t A0 = a.xA[rr], oA0 = a.xA[R + rr];
+    uint32_t A0 = a.xself ? 0u : a.xA[rr], oA0 = a.xself ? 0u : a.xA[R + rr];
     const bool rin = t < a.world * kXRecLines;
     const int gx = rin ? t : 0;
     const unsigned long long xo = a.xrec[(size_t)gx * 16], xm = a.xrec[(size_t)gx * 16 + 1];
@@ -4297,6 +4325,17 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_xp(TickArgs a) {
     if (bid == 0) {
         O_loc = (int64_t)sfo[0] + sfo[1] + sfo[2] + sfo[3];
         n_ev = (int64_t)sev[0] + sev[1] + sev[2] + sev[3];
+    }
+    if (a.xself) {
+        A0 = cps[0][0][rr] + cps[0][1][rr] + cps[0][2][rr] + cps[0][3][rr];
+        oA0 = cps[0][0][R + rr] + cps[0][1][R + rr] + cps[0][2][R + rr] + cps[0][3][R + rr];
+#pragma unroll
+        for (int j = 0; j < NSB; ++j) {
+            const int ch = min(bid * NSB + j, a.nbq - 1) / kXsBlocks;
+            const int q = ch == ch0 ? 1 : 2;
+            pre[j] += cps[q][0][rr] + cps[q][1][rr] + cps[q][2][rr] + cps[q][3][rr];
+            opre[j] += cps[q][0][R + rr] + cps[q][1][R + rr] + cps[q][2][R + rr] + cps[q][3][R + rr];
+        }
     }
     STAMP(a, SO, 5);
     // ---- the fill level (every wave alike; lane r = round r, one chunk)
