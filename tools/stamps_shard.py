@@ -81,3 +81,24 @@ if dx.size and (dx[:, :, 13] > 0).all():
         dc = (dx[:, :, k] - dx[:, :, prev])
         print("  %2d -> %2d  median %6d cyc  max %6d" % (prev, k, np.median(dc), np.median(dc.max(axis=1))))
         prev = k
+# phase 1 (k_scan, rank 0): rows from nbw -- queue blocks, then log tiles, then slot tiles
+full = np.stack([r[: (nbw + nbq + nbf + nbw) * 16].reshape(-1, 16).astype(np.int64) for r in rows])
+S1 = nbw
+roles = {"Q": (S1, S1 + nbq), "F": (S1 + nbq, S1 + nbq + nbf), "W": (S1 + nbq + nbf, S1 + nbq + nbf + nbw)}
+e_all = full[:, S1:S1 + nbq + nbf + nbw, 13]
+ok = (e_all > 0).all(axis=0)
+if ok.any():
+    t0 = np.where(e_all > 0, e_all, np.iinfo(np.int64).max).min(axis=1, keepdims=True)
+    print("phase-1 k_scan: span %.2f us" % np.median((full[:, S1:S1 + nbq + nbf + nbw, 14].max(axis=1) - t0[:, 0]) / 100.0))
+    for name, (lo, hi) in roles.items():
+        x = full[:, lo:hi, :]
+        live = (x[..., 13] > 0).all(axis=0)
+        if hi <= lo or not live.any():
+            continue
+        x = x[:, live, :]
+        ent = (x[..., 13] - t0) / 100.0
+        dur = (x[..., 14] - x[..., 13]) / 100.0
+        print("  %s %5d blocks: entry p50 +%.2f p90 +%.2f us, duration p50 %.2f p90 %.2f us, 0->1 %d cyc, 1->15 %d cyc"
+              % (name, x.shape[1], np.median(ent), np.percentile(ent, 90), np.median(dur), np.percentile(dur, 90),
+                 np.median(x[..., 1] - x[..., 0]) if (x[..., 1] > 0).all() else -1,
+                 np.median(x[..., 15] - x[..., 1]) if (x[..., 1] > 0).all() else -1))
