@@ -291,6 +291,7 @@ struct fb_ctx {
     int gp_on = 1;                                    // fb_set_path("gp", 0): large one-GPU tables run k_plan2
     int win_direct = 1;                               // fb_set_path("win_direct", 0): k_emit_win chunks by ticket
     int xself_on = 1;                                 // fb_set_path("xself", 0): k_xscan's last workgroup prefixes the chunks
+    int wfirst_on = 1;                                // fb_set_path("wfirst", 0): phase-1 k_scan queue blocks first
     int gpcheck = 0;                                  // fb_set_path("gpcheck", 1): diagnostic (stamps builds)
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
@@ -1061,6 +1062,9 @@ int enqueue_tick(fb_ctx *c) {
     a.hout = c->hout_dev;
     if (c->shard) {
         a.shard = c->phase == 2 ? 2 : 1;
+        // (only while the log role is fused into k_scan: with k_logscan the slot blocks are
+        // the short ones)
+        a.wfirst = (a.shard == 1 && !a.f_sep && c->wfirst_on) ? 1 : 0;
         a.slot_base = c->slot_base;
         a.rank = c->rank;
         a.world = c->world;
@@ -2876,6 +2880,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "gp" && (value == 0 || value == 1)) c->gp_on = value;
     else if (n == "win_direct" && (value == 0 || value == 1)) c->win_direct = value;
     else if (n == "xself" && (value == 0 || value == 1)) c->xself_on = value;
+    else if (n == "wfirst" && (value == 0 || value == 1)) c->wfirst_on = value;
     else if (n == "gpcheck" && (value == 0 || value == 1)) c->gpcheck = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;

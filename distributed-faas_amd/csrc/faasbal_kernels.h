@@ -358,7 +358,8 @@ struct TickArgs {
     double *wqh_buf;
     int nchB, nchF, nchW;
     int win_direct;
-    int xself;       // xplan ticks with <= 64 chunks: k_emit_shard_xp prefixes the chunk totals itself  // k_emit_win: chunk = workgroup index (every chunk resident at once), else a ticket
+    int xself;
+    int wfirst;      // k_scan: log and slot blocks ahead of the queue blocks in the grid (sharded phase 1)       // xplan ticks with <= 64 chunks: k_emit_shard_xp prefixes the chunk totals itself  // k_emit_win: chunk = workgroup index (every chunk resident at once), else a ticket
     unsigned long long *wlb;     // look-back granules: [0, nchB) the back chain, then the front / window chain
     uint32_t *wticket;           // chunk tickets (zeroed by k_ev_link)
     int64_t *cw;                 // commit word {failed, window head, window length} (eager commits)

@@ -1493,11 +1493,18 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     __shared__ unsigned long long s4[kWaves];
     __shared__ uint32_t wc[kWaves][kBS];
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
-    const int bid = blockIdx.x;
+    // grid: queue blocks first (the critical path: their loads go out before the log
+    // role's gathers fill the memory queues), then log blocks, then slot blocks.  Sharded
+    // phase 1 (a.wfirst): the log and slot blocks first -- there they are the longer ones
+    // (4-5 us against the queue blocks' 3 at configs[3], N = 8) and nothing waits on the
+    // queue role before the exchange
+    const int nfw = (int)gridDim.x - a.nbq - (a.cm_fold ? a.cm_blocks : 0);
+    const int bid = !a.wfirst ? (int)blockIdx.x
+                              : ((int)blockIdx.x < nfw ? a.nbq + (int)blockIdx.x
+                                                       : ((int)blockIdx.x < nfw + a.nbq ? (int)blockIdx.x - nfw
+                                                                                         : (int)blockIdx.x));
     const int SO = a.nbw;
     STAMP(a, SO, 0);
-    // grid: queue blocks first (the critical path: their loads go out before the log
-    // role's gathers fill the memory queues), then log blocks, then slot blocks
     if (bid >= a.nbq && bid - a.nbq < nbf) {
         // ---- F-role: orphan flags of log entries [b*2048 + t*8, +8)
         const int b = bid - a.nbq;
