@@ -1322,23 +1322,23 @@ __device__ __forceinline__ void wave_round_counts2(int c, uint64_t own, int r0, 
 
 // Sum of cnt[i] over i < n with all loads in flight at once (n <= kPeel*256 on
 // the fused path; a tail loop covers larger n); also the sum over i < lim.
-template <int PEEL = kPeel>
+template <int PEEL = kPeel, int BS = kBS>
 __device__ __forceinline__ void peeled_sum(const uint32_t *__restrict__ cnt, int n, int lim,
                                            unsigned long long &tot, unsigned long long &pre) {
     uint32_t v[PEEL];
 #pragma unroll
     for (int k = 0; k < PEEL; ++k) {
-        const int i = threadIdx.x + k * kBS;
+        const int i = threadIdx.x + k * BS;
         v[k] = i < n ? cnt[i] : 0u;
     }
     tot = pre = 0;
 #pragma unroll
     for (int k = 0; k < PEEL; ++k) {
-        const int i = threadIdx.x + k * kBS;
+        const int i = threadIdx.x + k * BS;
         tot += v[k];
         pre += i < lim ? v[k] : 0u;
     }
-    for (int i = threadIdx.x + PEEL * kBS; i < n; i += kBS) {
+    for (int i = threadIdx.x + PEEL * BS; i < n; i += BS) {
         const uint32_t x = cnt[i];
         tot += x;
         pre += i < lim ? x : 0u;
@@ -2896,6 +2896,238 @@ __device__ __forceinline__ int xcd_block(int i, int n) {
     return x * q + (x < r ? x : r) + y;
 }
 
+// k_emit2's compaction roles (workgroup rel of them): one wave per tile (a k_scan block's
+// 2048 log entries or 256 slots), four tiles per workgroup -- a quarter of the blocks of one
+// thread per flag byte / slot, so they do not queue behind the queue role.  PLAN: the
+// tiles' offsets from k_plan2's scans, else summed here.  NW waves (tiles) per workgroup.
+template <bool PLAN, int PEEL, int NW = kWaves>
+__device__ __forceinline__ void emit2_compact(const TickArgs &a, int rel, int nbf4, uint32_t (*red)[4]) {
+    const int lane = lane_id(), w = wave_id();
+    const bool frole = rel < nbf4;
+    const int t0 = NW * (frole ? rel : rel - nbf4);
+    const int t = t0 + w;
+    const int ntile = frole ? a.nbf : a.nbw;
+    const uint32_t *cnt = frole ? a.fcnt : a.wcnt;
+    int64_t off;  // entries of the tiles before t
+    if constexpr (PLAN) {
+        const int64_t *pre = frole ? a.fpre : a.wpre;
+        off = pre[t < ntile ? t : ntile - 1];
+    } else {
+        // the workgroup sums the counts of the tiles before its own (PEEL x 256 tiles with
+        // every load in flight; a tail loop past that)
+        unsigned long long tot, pre;
+        peeled_sum<PEEL, 64 * NW>(cnt, t0, t0, tot, pre);
+        const uint32_t ws = wave_sum_u32((uint32_t)pre);
+        if (lane == 0) red[w][0] = ws;
+        lds_barrier();
+        off = 0;
+#pragma unroll
+        for (int q = 0; q < NW; ++q) off += red[q][0];
+        for (int q = 0; q < w; ++q) off += t0 + q < ntile ? cnt[t0 + q] : 0u;
+    }
+    if (t >= ntile) return;
+    if (frole) {
+        // orphans, ascending sequence: lane l holds flag bytes 4l .. 4l+3 of tile t
+        // (k_scan's thread j flagged entries t*2048 + 8j .. +8)
+        const uint32_t f4 = reinterpret_cast<const uint32_t *>(a.ofl + (size_t)t * kBS)[lane];
+        const uint32_t n = (uint32_t)__popc(f4);
+        int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
+        const int64_t base = (int64_t)t * kFTile + (int64_t)lane * 4 * kFItems;
+        for (uint32_t m = f4; m; m &= m - 1) wt_store(a.orphans + o++, (int64_t)(base + __builtin_ctz(m)));
+    } else {
+        // evicted slots, ascending: lane l holds slots t*256 + 4l .. +4
+        const int s0 = t * kBS + 4 * lane;
+        const int wl = a.W > 0 ? a.W - 1 : 0;
+        uint32_t e = 0;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint8_t sv = a.st[min(s0 + q, wl)];
+            e |= ((s0 + q < a.W) && (sv & kStEvicted)) ? (1u << q) : 0u;
+        }
+        const uint32_t n = (uint32_t)__popc(e);
+        int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
+        for (uint32_t m = e; m; m &= m - 1) wt_store(a.evicted + o++, (int32_t)(s0 + __builtin_ctz(m)));
+    }
+}
+
+// k_emit2's queue role from the per-round prefixes on: the fill level, the partial round
+// L and the next state of every position (finish), the full rounds' stores.  Lane i holds
+// round 64 k + i of chunk k: prev = the tasks of round r taken by earlier blocks, totv =
+// A(r), segc = by the earlier waves of this block.
+template <int NCH, bool BIG, bool PLAN>
+__device__ __forceinline__ void emit2_rounds(const TickArgs &a, int SO, int b, int64_t pos, int32_t raw0, int s0,
+                                             double hb0, const uint32_t (&prev)[NCH], const uint32_t (&totv)[NCH],
+                                             const uint32_t (&segc)[NCH], int maxc, int64_t O, int64_t nev,
+                                             int64_t cap) {
+    const int lane = lane_id();
+    const int R = a.R;
+    const int rlim = maxc < R ? maxc : R;
+    // ---- per wave: S(r) (lane i of chunk k: round 64 k + i), capacity, fill level L
+    int64_t Sv[NCH], S1v[NCH];
+    {
+        int64_t carry = 0;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k) {
+            const int r = 64 * k + lane;
+            const uint32_t v = r < rlim ? totv[k] : 0u;
+            const uint32_t incl = wave_incl_scan_u32(v);
+            S1v[k] = carry + (int64_t)incl;  // S(r + 1)
+            Sv[k] = S1v[k] - (int64_t)v;     // S(r)
+            carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        }
+        // fused: sum_r A(r) over r < max c = sum of c (PLAN: k_plan's capacity)
+        if constexpr (!PLAN) cap = carry;
+    }
+    if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
+    const int64_t N = (a.redist ? O : 0) + a.T;  // purge-only ticks report orphans, dispatch none
+    const int64_t N_eff = N < cap ? N : cap;
+    int L = 0;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) L += __popcll(__ballot(64 * k + lane < rlim && S1v[k] <= N_eff));
+    const int Lc = L >> 6, Ll = L & 63;
+    const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(Sv, Lc), Ll);
+    int status = 0;
+    if (maxc > R && L >= R - 1) status = 1;   // rows beyond the table needed: rerun wider
+    else if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log (N_eff exact once R is)
+    const int64_t pL = N_eff - S_L;
+    const int64_t AL =
+        (L < maxc && L < rlim) ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(totv, Lc), Ll) : 0;
+    if (b == 0 && threadIdx.x == 0) {
+        a.hout->O = O;
+        a.hout->n_evicted = nev;
+        a.hout->cap_total = cap;
+        a.hout->maxc = maxc;
+        a.hout->L = L;
+        a.hout->status = status;
+        a.hout->N_eff = status ? 0 : N_eff;
+        a.hout->p = pL;
+        a.hout->AL = AL;
+        if (AL == 0) a.hout->new_qlen = 0;
+    }
+    if (status) return;
+    // ---- rank base (in A_r) and task index base of this wave's segment, per round
+    const int32_t raw = pos < a.Qlog ? raw0 : INT32_MIN;
+    const int s = s0;
+    // free <= 0 still takes one task; deque mode: c_arr holds the token's c itself
+    const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
+    if (a.rb_slot && pos < a.Qlog) compact_out(a, pos, s, c, L);
+    int32_t rbv[NCH], basev[NCH];
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+        const int r = 64 * k + lane;
+        rbv[k] = (int32_t)((r < rlim ? prev[k] : 0u) + segc[k]);
+        basev[k] = (int32_t)Sv[k] + rbv[k];  // valid for r <= rlim
+    }
+    STAMP(a, SO, 2);
+    int32_t *const out = a.log_slot + a.head_in;
+    // ---- round L (partial: ranks < pL) and round L + 1 (ranks for the next queue)
+    const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
+    const int rbL = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, Lc), Ll);
+    const int rbL1 = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, L1c), L1l);
+    const uint64_t mL = __ballot(c > L);
+    const int64_t rankL = (int64_t)rbL + popc_lt(mL);
+    const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
+    // round L's stores and the position's next state (free count, next queue)
+    auto finish = [&]() {
+        if (!(kDiagNow & 32) && c > L && rankL < pL) wt_store(out + S_L + rankL, s);
+        if (c > 0) {
+            int64_t n_q = c < L ? c : L;
+            if (c > L && rankL < pL) n_q += 1;
+            int64_t np = -1;
+            if (c > L) {
+                if (rankL >= pL) np = rankL - pL;
+                else if (c > L1) np = (AL - pL) + exL1;
+                // the one position of rank pL in A_L knows the next queue's length
+                if (rankL == pL) a.hout->new_qlen = (AL - pL) + exL1;
+            }
+            if (a.deque) {
+                deque_finish(a, pos, s, c, L, n_q, c > L && rankL < pL, np);
+                return;
+            }
+            // the worker's next {free, queued}: one 8-byte store, only for the workers served
+            // this tick -- the slot role already wrote {free, 1} for every queued one (a
+            // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
+            // (free_pre: the purge wrote {raw - c, 0}, this position's value when c <= L)
+            if (!(kDiagNow & 4) && (a.free_pre ? c > L : (n_q != 0 || np < 0))) {
+                wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
+            }
+
+            if (!(kDiagNow & 8) && np >= 0) {
+                wt_store(a.queue_out + np, s);
+                wt_store(a.qfree_out + np, raw - (int32_t)n_q);
+                wt_store(a.qhb_out + np, hb0);
+            }
+        }
+    };
+    // heartbeat loop: issued before the full rounds, so the scattered free-count stores
+    // are under way while the rounds store (configs[2]: 10.30 -> 10.16 us per tick; as
+    // agent-scope stores no change, as nontemporal stores +0.7 us)
+    const bool fin_first = !a.deque;
+    if (fin_first) finish();
+    // ---- full rounds r < min(L, max c of the wave): every active lane takes one task
+    const int wmx = (int)wave_max_u32((uint32_t)c);
+    const int rfull = L < wmx ? L : wmx;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+        const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
+        int i = 0;
+        // fused (small) ticks branch-free: every lane stores, inactive ones into the
+        // trash words (an `if (act)` store costs an exec save / branch / restore per
+        // round; configs[2]: tick 13.4 -> 13.0 us).  (A buffer store predicated by its
+        // range check instead -- inactive lanes given an out-of-range offset -- took
+        // the 19 rounds from 2.0 K to 3.6 K cycles: rejected.)
+        // (one 1 KB trash row per block, 1024 rows: no line shared between blocks)
+        int32_t *const tr = a.trash + (size_t)(blockIdx.x & (kTrashRows - 1)) * kBS + threadIdx.x;
+        if (kDiagNow & 2) i = r1;
+        if (!BIG && a.arena32) {
+            // every buffer lies in the context's arena (< 4 GB): 32-bit byte offsets from
+            // one scalar base -- a select and a saddr store per round, no 64-bit math
+            char *const ab = a.arena;
+            const uint32_t oo = (uint32_t)((char *)out - ab), to = (uint32_t)((char *)tr - ab);
+            const uint32_t bo = oo + 4u * (uint32_t)basev[k];  // byte offset of each round's first store
+            for (; i + 3 < r1; i += 4) {
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int r = 64 * k + i + u;
+                    const bool act = c > r;
+                    const uint64_t m = __ballot(act);
+                    const uint32_t po = __builtin_amdgcn_readlane(bo, i + u) + 4u * popc_lt(m);
+                    const uint32_t off = to + ((po - to) & (0u - (uint32_t)act));
+                    if (!(kDiagNow & 1)) wt_store((int32_t *)(ab + off), s);
+                    else if (act) wt_store((int32_t *)(ab + po), s);
+                }
+            }
+        }
+        for (; i + 3 < r1; i += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int r = 64 * k + i + u;
+                const bool act = c > r;
+                const uint64_t m = __ballot(act);
+                const int base = __builtin_amdgcn_readlane(basev[k], i + u);
+                if constexpr (!BIG) {
+                    // select by mask arithmetic: a ?: on the pointers becomes an exec-masked block
+                    const uint64_t pa = (uint64_t)(out + (base + (int)popc_lt(m))), pt = (uint64_t)tr;
+                    wt_store((int32_t *)(pt ^ ((pa ^ pt) & (0ull - (uint64_t)act))), s);
+                } else {
+                    // large tables (after k_plan): thousands of blocks, where the trash
+                    // stores cost more than the branches they save (16M x 1M: +1.2 us)
+                    if (act) wt_store(out + base + popc_lt(m), s);
+                }
+            }
+        }
+        for (; i < r1; ++i) {
+            const int r = 64 * k + i;
+            const bool act = c > r;
+            const uint64_t m = __ballot(act);
+            const int base = __builtin_amdgcn_readlane(basev[k], i);
+            if (act) wt_store(out + base + popc_lt(m), s);
+        }
+    }
+    STAMP(a, SO, 3);
+    if (!fin_first) finish();
+}
+
 // PM 1 (PLAN): large tables (round table beyond the fused limit, R <= 128) -- the same
 // emission with this block's prefixes and the totals from k_plan2.  PM 2 (gp): large tables
 // without k_plan2 -- the prefixes from the group rows as the fused path (PM 0) reads them,
@@ -3152,177 +3384,11 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
             for (int q = 0; q < kWaves - 1; ++q) sc += (q < w && 64 * k + lane < R) ? sseg[q][r] : 0u;
             segc[k] = sc;
         }
-        const int rlim = maxc < R ? maxc : R;
-        // ---- per wave: S(r) (lane i of chunk k: round 64 k + i), capacity, fill level L
-        int64_t Sv[NCH], S1v[NCH];
-        {
-            int64_t carry = 0;
-#pragma unroll
-            for (int k = 0; k < NCH; ++k) {
-                const int r = 64 * k + lane;
-                const uint32_t v = r < rlim ? totv[k] : 0u;
-                const uint32_t incl = wave_incl_scan_u32(v);
-                S1v[k] = carry + (int64_t)incl;  // S(r + 1)
-                Sv[k] = S1v[k] - (int64_t)v;     // S(r)
-                carry += (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
-            }
-            // fused: sum_r A(r) over r < max c = sum of c (PLAN: k_plan's capacity)
-            if constexpr (!PLAN) cap = carry;
-        }
-        if (maxc > R) cap = INT64_MAX;  // capacity beyond the table: only S(R) is known
-        const int64_t N = (a.redist ? O : 0) + a.T;  // purge-only ticks report orphans, dispatch none
-        const int64_t N_eff = N < cap ? N : cap;
-        int L = 0;
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) L += __popcll(__ballot(64 * k + lane < rlim && S1v[k] <= N_eff));
-        const int Lc = L >> 6, Ll = L & 63;
-        const int64_t S_L = (int64_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(Sv, Lc), Ll);
-        int status = 0;
-        if (maxc > R && L >= R - 1) status = 1;   // rows beyond the table needed: rerun wider
-        else if (a.head_in + N_eff > a.log_cap) status = 2;  // never write past the in-flight log (N_eff exact once R is)
-        const int64_t pL = N_eff - S_L;
-        const int64_t AL =
-            (L < maxc && L < rlim) ? (int64_t)(uint32_t)__builtin_amdgcn_readlane((int)chunk_pick<NCH>(totv, Lc), Ll) : 0;
-        if (b == 0 && threadIdx.x == 0) {
-            a.hout->O = O;
-            a.hout->n_evicted = nev;
-            a.hout->cap_total = cap;
-            a.hout->maxc = maxc;
-            a.hout->L = L;
-            a.hout->status = status;
-            a.hout->N_eff = status ? 0 : N_eff;
-            a.hout->p = pL;
-            a.hout->AL = AL;
-            if (AL == 0) a.hout->new_qlen = 0;
-        }
-        if (status) return;
-        // ---- rank base (in A_r) and task index base of this wave's segment, per round
-        const int32_t raw = pos < a.Qlog ? raw0 : INT32_MIN;
-        const int s = s0;
-        // free <= 0 still takes one task; deque mode: c_arr holds the token's c itself
-        const int c = raw != INT32_MIN ? (a.deque ? raw : (raw > 1 ? raw : 1)) : 0;
-        if (a.rb_slot && pos < a.Qlog) compact_out(a, pos, s, c, L);
-        int32_t rbv[NCH], basev[NCH];
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) {
-            const int r = 64 * k + lane;
-            rbv[k] = (int32_t)((r < rlim ? prev[k] : 0u) + segc[k]);
-            basev[k] = (int32_t)Sv[k] + rbv[k];  // valid for r <= rlim
-        }
-        STAMP(a, SO, 2);
-        int32_t *const out = a.log_slot + a.head_in;
-        // ---- round L (partial: ranks < pL) and round L + 1 (ranks for the next queue)
-        const int L1 = L + 1, L1c = L1 >> 6, L1l = L1 & 63;
-        const int rbL = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, Lc), Ll);
-        const int rbL1 = __builtin_amdgcn_readlane(chunk_pick<NCH>(rbv, L1c), L1l);
-        const uint64_t mL = __ballot(c > L);
-        const int64_t rankL = (int64_t)rbL + popc_lt(mL);
-        const int64_t exL1 = (int64_t)rbL1 + popc_lt(__ballot(c > L1));
-        // round L's stores and the position's next state (free count, next queue)
-        auto finish = [&]() {
-            if (!(kDiagNow & 32) && c > L && rankL < pL) wt_store(out + S_L + rankL, s);
-            if (c > 0) {
-                int64_t n_q = c < L ? c : L;
-                if (c > L && rankL < pL) n_q += 1;
-                int64_t np = -1;
-                if (c > L) {
-                    if (rankL >= pL) np = rankL - pL;
-                    else if (c > L1) np = (AL - pL) + exL1;
-                    // the one position of rank pL in A_L knows the next queue's length
-                    if (rankL == pL) a.hout->new_qlen = (AL - pL) + exL1;
-                }
-                if (a.deque) {
-                    deque_finish(a, pos, s, c, L, n_q, c > L && rankL < pL, np);
-                    return;
-                }
-                // the worker's next {free, queued}: one 8-byte store, only for the workers served
-                // this tick -- the slot role already wrote {free, 1} for every queued one (a
-                // streaming tick serves 64 K of 1 M queued workers: 64 K scattered stores, not 1 M)
-                // (free_pre: the purge wrote {raw - c, 0}, this position's value when c <= L)
-                if (!(kDiagNow & 4) && (a.free_pre ? c > L : (n_q != 0 || np < 0))) {
-                    wt_store(a.free_out + s, make_int2(raw - (int32_t)n_q, np >= 0 ? 1 : 0));
-                }
-
-                if (!(kDiagNow & 8) && np >= 0) {
-                    wt_store(a.queue_out + np, s);
-                    wt_store(a.qfree_out + np, raw - (int32_t)n_q);
-                    wt_store(a.qhb_out + np, hb0);
-                }
-            }
-        };
-        // heartbeat loop: issued before the full rounds, so the scattered free-count stores
-        // are under way while the rounds store (configs[2]: 10.30 -> 10.16 us per tick; as
-        // agent-scope stores no change, as nontemporal stores +0.7 us)
-        const bool fin_first = !a.deque;
-        if (fin_first) finish();
-        // ---- full rounds r < min(L, max c of the wave): every active lane takes one task
-        const int wmx = (int)wave_max_u32((uint32_t)c);
-        const int rfull = L < wmx ? L : wmx;
-#pragma unroll
-        for (int k = 0; k < NCH; ++k) {
-            const int r1 = rfull - 64 * k < 64 ? rfull - 64 * k : 64;
-            int i = 0;
-            // fused (small) ticks branch-free: every lane stores, inactive ones into the
-            // trash words (an `if (act)` store costs an exec save / branch / restore per
-            // round; configs[2]: tick 13.4 -> 13.0 us).  (A buffer store predicated by its
-            // range check instead -- inactive lanes given an out-of-range offset -- took
-            // the 19 rounds from 2.0 K to 3.6 K cycles: rejected.)
-            // (one 1 KB trash row per block, 1024 rows: no line shared between blocks)
-            int32_t *const tr = a.trash + (size_t)(blockIdx.x & (kTrashRows - 1)) * kBS + threadIdx.x;
-            if (kDiagNow & 2) i = r1;
-            if (!BIG && a.arena32) {
-                // every buffer lies in the context's arena (< 4 GB): 32-bit byte offsets from
-                // one scalar base -- a select and a saddr store per round, no 64-bit math
-                char *const ab = a.arena;
-                const uint32_t oo = (uint32_t)((char *)out - ab), to = (uint32_t)((char *)tr - ab);
-                const uint32_t bo = oo + 4u * (uint32_t)basev[k];  // byte offset of each round's first store
-                for (; i + 3 < r1; i += 4) {
-#pragma unroll
-                    for (int u = 0; u < 4; ++u) {
-                        const int r = 64 * k + i + u;
-                        const bool act = c > r;
-                        const uint64_t m = __ballot(act);
-                        const uint32_t po = __builtin_amdgcn_readlane(bo, i + u) + 4u * popc_lt(m);
-                        const uint32_t off = to + ((po - to) & (0u - (uint32_t)act));
-                        if (!(kDiagNow & 1)) wt_store((int32_t *)(ab + off), s);
-                        else if (act) wt_store((int32_t *)(ab + po), s);
-                    }
-                }
-            }
-            for (; i + 3 < r1; i += 4) {
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int r = 64 * k + i + u;
-                    const bool act = c > r;
-                    const uint64_t m = __ballot(act);
-                    const int base = __builtin_amdgcn_readlane(basev[k], i + u);
-                    if constexpr (!BIG) {
-                        // select by mask arithmetic: a ?: on the pointers becomes an exec-masked block
-                        const uint64_t pa = (uint64_t)(out + (base + (int)popc_lt(m))), pt = (uint64_t)tr;
-                        wt_store((int32_t *)(pt ^ ((pa ^ pt) & (0ull - (uint64_t)act))), s);
-                    } else {
-                        // large tables (after k_plan): thousands of blocks, where the trash
-                        // stores cost more than the branches they save (16M x 1M: +1.2 us)
-                        if (act) wt_store(out + base + popc_lt(m), s);
-                    }
-                }
-            }
-            for (; i < r1; ++i) {
-                const int r = 64 * k + i;
-                const bool act = c > r;
-                const uint64_t m = __ballot(act);
-                const int base = __builtin_amdgcn_readlane(basev[k], i);
-                if (act) wt_store(out + base + popc_lt(m), s);
-            }
-        }
-        STAMP(a, SO, 3);
-        if (!fin_first) finish();
+        emit2_rounds<NCH, BIG, PLAN>(a, SO, b, pos, raw0, s0, hb0, prev, totv, segc, maxc, O, nev, cap);
         STAMP(a, SO, 15);
         return;
     }
-    // ---- compaction roles: one wave per tile (a k_scan block's 2048 log entries or
-    // 256 slots), four tiles per workgroup -- a quarter of the blocks of one
-    // thread per flag byte / slot, so they do not queue behind the queue role
+    // ---- compaction roles (emit2_compact)
     if (a.f_emit && bid >= cb0 && bid < cb0 + a.nbf) {  // f_emit: one log workgroup per tile
         extern __shared__ __attribute__((aligned(16))) unsigned long long dynbm[];
         STAMP(a, SO, 0);
@@ -3331,50 +3397,8 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
         return;
     }
     STAMP(a, SO, 0);
-    const bool frole = !a.f_emit && bid < cb0 + nbf4;
-    const int t0 = 4 * (frole ? bid - cb0 : bid - cb0 - nbf4);
-    const int t = t0 + w;
-    const int ntile = frole ? a.nbf : a.nbw;
-    const uint32_t *cnt = frole ? a.fcnt : a.wcnt;
-    int64_t off;  // entries of the tiles before t
-    if constexpr (PLAN) {
-        const int64_t *pre = frole ? a.fpre : a.wpre;
-        off = pre[t < ntile ? t : ntile - 1];
-    } else {
-        // the workgroup sums the counts of the tiles before its own (gp: up to 4096 tiles,
-        // 16 loads per thread in flight at once)
-        unsigned long long tot, pre;
-        if constexpr (PM == 2) peeled_sum<16>(cnt, t0, t0, tot, pre);
-        else peeled_sum<kPeel>(cnt, t0, t0, tot, pre);
-        const uint32_t ws = wave_sum_u32((uint32_t)pre);
-        if (lane == 0) red[w][0] = ws;
-        lds_barrier();
-        off = (int64_t)red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        for (int q = 0; q < w; ++q) off += t0 + q < ntile ? cnt[t0 + q] : 0u;
-    }
-    if (t >= ntile) return;
-    if (frole) {
-        // orphans, ascending sequence: lane l holds flag bytes 4l .. 4l+3 of tile t
-        // (k_scan's thread j flagged entries t*2048 + 8j .. +8)
-        const uint32_t f4 = reinterpret_cast<const uint32_t *>(a.ofl + (size_t)t * kBS)[lane];
-        const uint32_t n = (uint32_t)__popc(f4);
-        int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
-        const int64_t base = (int64_t)t * kFTile + (int64_t)lane * 4 * kFItems;
-        for (uint32_t m = f4; m; m &= m - 1) wt_store(a.orphans + o++, (int64_t)(base + __builtin_ctz(m)));
-    } else {
-        // evicted slots, ascending: lane l holds slots t*256 + 4l .. +4
-        const int s0 = t * kBS + 4 * lane;
-        const int wl = a.W > 0 ? a.W - 1 : 0;
-        uint32_t e = 0;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            const uint8_t sv = a.st[min(s0 + q, wl)];
-            e |= ((s0 + q < a.W) && (sv & kStEvicted)) ? (1u << q) : 0u;
-        }
-        const uint32_t n = (uint32_t)__popc(e);
-        int64_t o = off + (int64_t)(wave_incl_scan_u32(n) - n);
-        for (uint32_t m = e; m; m &= m - 1) wt_store(a.evicted + o++, (int32_t)(s0 + __builtin_ctz(m)));
-    }
+    if (a.f_emit) emit2_compact<PLAN, PM == 2 ? 16 : kPeel>(a, bid - cb0 - a.nbf, 0, red);
+    else emit2_compact<PLAN, PM == 2 ? 16 : kPeel>(a, bid - cb0, nbf4, red);
     STAMP(a, SO, 15);
 }
 
