@@ -293,6 +293,7 @@ struct fb_ctx {
     int xself_on = 1;                                 // fb_set_path("xself", 0): k_xscan's last workgroup prefixes the chunks
     int wfirst_on = 1;                                // fb_set_path("wfirst", 0): phase-1 k_scan queue blocks first
     int gpcheck = 0;                                  // fb_set_path("gpcheck", 1): diagnostic (stamps builds)
+    int cmix_on = 1;                                  // fb_set_path("cmix"): k_emit2 role interleave
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
     bool l_full = false;                              // ... and the last launch did
@@ -1251,6 +1252,7 @@ int enqueue_tick(fb_ctx *c) {
         a.gp = 1;
         a.gpcheck = c->gpcheck;
     }
+    a.cmix = (c->cmix_on && !a.fused && !a.f_emit);
     if (!a.slots_in_scan && !a.slots_in_apply) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
@@ -2882,6 +2884,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "xself" && (value == 0 || value == 1)) c->xself_on = value;
     else if (n == "wfirst" && (value == 0 || value == 1)) c->wfirst_on = value;
     else if (n == "gpcheck" && (value == 0 || value == 1)) c->gpcheck = value;
+    else if (n == "cmix" && (value == 0 || value == 1)) c->cmix_on = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }

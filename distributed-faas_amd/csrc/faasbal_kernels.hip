@@ -3143,15 +3143,32 @@ __global__ __launch_bounds__(kBS) void k_emit2(TickArgs a_) {
     __shared__ uint32_t red[kWaves][4];
     __shared__ uint32_t pre_c[kRFused];        // PLAN: this block's prefix of round r
     __shared__ uint32_t tot_f[kRFused];        // PLAN: A(r)
-    const int bid = blockIdx.x;
     const int SO = a.nbw + a.nbf + a.nbq + (a.slots_in_scan ? a.nbw : 0);
     STAMP(a, SO, 0);
     const int lane = lane_id(), w = wave_id();
     // the other parity's group rows, for the next launch's k_scan atomics
-    for (int i = bid * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS) a.grp_zero[i] = 0;
+    for (int i = (int)blockIdx.x * kBS + (int)threadIdx.x; i < a.zero_words; i += (int)gridDim.x * kBS)
+        a.grp_zero[i] = 0;
     // grid: queue blocks, then compaction blocks -- log workgroups: 4 tiles each (f_emit:
     // one tile each), then the slot tiles 4 per workgroup
     const int nbf4 = a.f_emit ? a.nbf : (a.nbf + 3) >> 2;
+    int bid = blockIdx.x;  // the role index
+    if (a.cmix) {
+        // (fb_set_path("cmix")) the compaction rows of 8 workgroups (one per XCD) spread
+        // evenly among the queue rows, so they run beside the queue blocks' load latency
+        // instead of after them; a queue block keeps its XCD (role index mod 8 = blockIdx mod 8)
+        const int nc = nbf4 + ((a.nbw + 3) >> 2);
+        const int x = (int)blockIdx.x & 7, y = (int)blockIdx.x >> 3;
+        const int nqr = (a.nbq + 7) >> 3, ncr = (nc + 7) >> 3, nr = nqr + ncr;
+        const int cr = (int)((int64_t)y * ncr / nr);
+        if ((int)((int64_t)(y + 1) * ncr / nr) > cr) {
+            if (8 * cr + x >= nc) return;
+            bid = a.nbq + 8 * cr + x;
+        } else {
+            if (8 * (y - cr) + x >= a.nbq) return;
+            bid = 8 * (y - cr) + x;
+        }
+    }
     const int qb0 = 0, cb0 = a.nbq;
     if (bid >= qb0 && bid < qb0 + a.nbq) {
         const int b = xcd_block(bid - qb0, a.nbq);
@@ -4909,7 +4926,8 @@ void launch_emit(const TickArgs &a, Stream st) {
 }
 template <int PM, int NCH>
 static void launch_emit2_t(const TickArgs &a, Stream st) {
-    const dim3 g(a.nbq + (a.f_emit ? a.nbf : (a.nbf + 3) / 4) + (a.nbw + 3) / 4);
+    const int nc = (a.f_emit ? a.nbf : (a.nbf + 3) / 4) + (a.nbw + 3) / 4;
+    const dim3 g(a.cmix ? 8 * ((a.nbq + 7) / 8 + (nc + 7) / 8) : a.nbq + nc);
     // f_emit: the log workgroups stage the died bitmap in LDS (rounded to whole int4)
     const size_t lds = a.f_emit ? (size_t)(((a.W + 63) / 64 + 1) / 2) * 16 : 0;
     switch (tick_mode(a)) {

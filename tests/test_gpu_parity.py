@@ -496,6 +496,14 @@ def test_config3_logscan(logscan):
     test_config3_full_size()
 
 
+@pytest.mark.parametrize("seed", range(3))
+def test_random_multitick_logscan_plan_no_cmix(logscan, force_plan, monkeypatch, seed):
+    """k_emit2's grid in role order (fb_set_path("cmix", 0)): queue blocks, then the
+    compaction workgroups -- the default interleaves their rows."""
+    monkeypatch.setitem(TEST_PATHS, "cmix", 0)
+    test_random_multitick_vs_oracle(seed + 20)
+
+
 def test_churn_logscan(logscan):
     test_churn_stream_vs_oracle()
 
