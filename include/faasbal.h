@@ -273,6 +273,12 @@ int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_to
  *                 resident at once, 0 always by ticket;
  *   "fault_qlen"  test hook: the next waited tick reports this queue length (checked and
  *                 refused by fb_tick_wait when it exceeds the buffer; -1 off);
+ *   "xself"       sharded xplan: 1 k_emit_shard_xp sums the chunk totals itself (<= 64
+ *                 chunks), 0 k_xscan's last workgroup does behind a ticket;
+ *   "wfirst"      sharded phase 1: 1 k_scan's log and slot blocks ahead of its queue blocks
+ *                 (while the log role is fused into k_scan), 0 queue blocks first;
+ *   "cmix"        k_emit2 on unfused ticks: 1 compaction workgroups interleaved with the queue
+ *                 blocks, 0 after them;
  *   "gpcheck"     diagnostic (stamps builds): k_plan2 runs beside a gp tick for comparison.
  * Between ticks only; FB_EINVAL for an unknown name or value. */
 int fb_set_path(fb_ctx *ctx, const char *name, int value);
