@@ -421,6 +421,7 @@ struct TickArgs {
     int gp;
     int gpcheck;  // (stamps builds: k_plan2 runs too, k_emit2 records both prefixes)
     int cmix;     // k_emit2: compaction workgroups interleaved with the queue blocks
+    int wtiles;   // k_scan: slot tiles per W-role workgroup (1, 2 or 4)
     // sharded phase 2 (fb_set_full_assign): this rank also writes the whole tick's task -> slot
     // array (every rank computes the global water-filling; one rank's copy serves the host)
     int32_t *assign_all;

@@ -1377,63 +1377,84 @@ __device__ __forceinline__ void xc_put(const TickArgs &a, int64_t pos, int c) {
 // Heartbeat purge of every slot (purge_workers, :241-249): liveness, the
 // died-registration bitmap, next free_processes (INT32_MIN = no live record).
 // Its own launch (k_slots) or the W-role blocks of k_scan (a.slots_in_scan).
-__device__ __forceinline__ void slots_body(const TickArgs &a, int blk, uint32_t *l4) {
-    const int s = blk * kBS + threadIdx.x;
-    bool died_start = false, evicted = false;
-    uint32_t no = 0;  // orphans: in-flight entries of this slot's dead registration
-    if (s < a.W) {
-        Cur c = cur_slot(a, s);
-        if (a.cm_fold && (a.st[s] & kStEvicted)) {
-            // the previous tick deleted this record (its commit, folded in here):
-            // del self.workers[remove_id] (task_dispatcher.py:246-247)
-            c.reg0 = c.reg = 0;
-            c.hb = __builtin_nan("");
-            const_cast<uint8_t *>(a.reg)[s] = 0;  // (the committed record arrays: read-only elsewhere in a tick)
-            const_cast<double *>(a.hb)[s] = c.hb;
-        }
+// NT tiles of 256 slots per workgroup (k_scan's W role, fb_set_path("wtiles")), every
+// tile's loads issued before the first tile's stores.
+template <int NT = 1>
+__device__ __forceinline__ void slots_body(const TickArgs &a, int blk0, uint32_t (*l4)[kWaves]) {
+    Cur cv[NT];
+    int32_t b0v[NT];
+    uint32_t ipv[NT];
+    uint8_t st0[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int s = (blk0 + j) * kBS + threadIdx.x;
+        const int sc = s < a.W ? s : (a.W > 0 ? a.W - 1 : 0);
+        cv[j] = cur_slot(a, sc);
+        st0[j] = a.cm_fold ? a.st[sc] : (uint8_t)0;
         // in-flight entries after the messages (loaded with the record, selected after)
-        const int32_t b0 = a.bud ? a.bud[s] : 0;
-        const uint32_t ip = (a.bud && a.E > 0) ? a.post_infl[s] : 0u;
-        const bool dead = is_dead(a, c);
-        const bool alive = c.reg && !dead;
-        died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
-        evicted = !a.deque && (c.reg0 || c.t) && !alive;  // start() never deletes a record
-        a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0) |
-                            (c.q0 ? kStQ0 : 0));
-        // queued: a live position of this tick's LRU queue (committed and kept, or a
-        // front / back insertion) -- k_emit2 then rewrites only the slots it serves
-        const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
-        const int32_t cq = c.fr > 1 ? c.fr : 1;  // its position's c
-        a.free_out[s] = (a.free_pre && queued) ? make_int2(c.fr - cq, 0)
-                                               : make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
-        if (a.bud) {
-            // untouched: the committed free count is c.fr; a slot without a record has none
-            const uint32_t pin = c.t ? ip : (c.reg0 ? (uint32_t)(b0 - c.fr) : 0u);
-            no = died_start ? pin : 0u;
-            // a touched slot's budget after the tick (a new registration starts empty);
-            // an untouched one keeps its budget: dispatches move free into in flight
-            if (c.t) a.bud_next[s] = (int32_t)((alive && !died_start) ? pin : 0u) + c.fr;
+        b0v[j] = a.bud ? a.bud[sc] : 0;
+        ipv[j] = (a.bud && a.E > 0) ? a.post_infl[sc] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int blk = blk0 + j;
+        const int s = blk * kBS + threadIdx.x;
+        bool died_start = false, evicted = false;
+        uint32_t no = 0;  // orphans: in-flight entries of this slot's dead registration
+        if (s < a.W) {
+            Cur c = cv[j];
+            if (a.cm_fold && (st0[j] & kStEvicted)) {
+                // the previous tick deleted this record (its commit, folded in here):
+                // del self.workers[remove_id] (task_dispatcher.py:246-247)
+                c.reg0 = c.reg = 0;
+                c.hb = __builtin_nan("");
+                const_cast<uint8_t *>(a.reg)[s] = 0;  // (the committed record arrays: read-only elsewhere in a tick)
+                const_cast<double *>(a.hb)[s] = c.hb;
+            }
+            const int32_t b0 = b0v[j];
+            const uint32_t ip = ipv[j];
+            const bool dead = is_dead(a, c);
+            const bool alive = c.reg && !dead;
+            died_start = c.reg0 && (dead || (c.flags & kPfDiedStart));
+            evicted = !a.deque && (c.reg0 || c.t) && !alive;  // start() never deletes a record
+            a.st[s] = (uint8_t)((alive ? kStAlive : 0) | (died_start ? kStDiedStart : 0) | (evicted ? kStEvicted : 0) |
+                                (c.q0 ? kStQ0 : 0));
+            // queued: a live position of this tick's LRU queue (committed and kept, or a
+            // front / back insertion) -- k_emit2 then rewrites only the slots it serves
+            const bool queued = !a.deque && !a.shard && alive && (c.t ? ((c.flags >> 1) & 3) != kQsOut : c.q0 != 0);
+            const int32_t cq = c.fr > 1 ? c.fr : 1;  // its position's c
+            a.free_out[s] = (a.free_pre && queued) ? make_int2(c.fr - cq, 0)
+                                                   : make_int2(alive ? c.fr : INT32_MIN, queued ? 1 : 0);
+            if (a.bud) {
+                // untouched: the committed free count is c.fr; a slot without a record has none
+                const uint32_t pin = c.t ? ip : (c.reg0 ? (uint32_t)(b0 - c.fr) : 0u);
+                no = died_start ? pin : 0u;
+                // a touched slot's budget after the tick (a new registration starts empty);
+                // an untouched one keeps its budget: dispatches move free into in flight
+                if (c.t) a.bud_next[s] = (int32_t)((alive && !died_start) ? pin : 0u) + c.fr;
+            }
+            if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
+                a.tokcnt_out[s] = 0;
+                a.xw_out[s] = 0;
+            }
         }
-        if (a.deque) {  // the emit kernel counts the surviving tokens per slot into these
-            a.tokcnt_out[s] = 0;
-            a.xw_out[s] = 0;
+        const uint64_t dm = __ballot(died_start);
+        if ((!a.slots_in_scan || a.f_sep || a.f_emit) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) {
+            a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
         }
+        if (a.f_emit) {
+            // O for the fill level: the dead registrations' in-flight counts (k_emit2's log
+            // tiles find the same entries, for the compaction)
+            const uint32_t nw = wave_sum_u32(no);
+            if (lane_id() == 0 && nw) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 1], nw);
+        }
+        const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
+        if (lane_id() == 0) l4[j][wave_id()] = ev;
     }
-    const uint64_t dm = __ballot(died_start);
-    if ((!a.slots_in_scan || a.f_sep || a.f_emit) && lane_id() == 0 && blk * kBS + wave_id() * 64 < a.W) {
-        a.dmask[(blk * kBS) / 64 + wave_id()] = dm;
-    }
-    if (a.f_emit) {
-        // O for the fill level: the dead registrations' in-flight counts (k_emit2's log
-        // tiles find the same entries, for the compaction)
-        const uint32_t nw = wave_sum_u32(no);
-        if (lane_id() == 0 && nw) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 1], nw);
-    }
-    const uint32_t ev = (uint32_t)__popcll(__ballot(evicted));
-    if (lane_id() == 0) l4[wave_id()] = ev;
     lds_barrier();
-    if (threadIdx.x == 0) {
-        const uint32_t n = l4[0] + l4[1] + l4[2] + l4[3];
+    if (threadIdx.x < NT && blk0 + (int)threadIdx.x < a.nbw) {
+        const int j = threadIdx.x, blk = blk0 + j;
+        const uint32_t n = l4[j][0] + l4[j][1] + l4[j][2] + l4[j][3];
         a.wcnt[blk] = n;
         // fused: evictions into column R + 2 of a group row (k_emit2 sums every row)
         if (a.grp_on && n) atomicAdd(&a.grp[(blk % a.ngrp) * a.gstride + a.R + 2], n);
@@ -1444,7 +1465,7 @@ template <int MODE>
 __global__ __launch_bounds__(kBS) void k_slots(TickArgs a_) {
     prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
-    __shared__ uint32_t l4[kWaves];
+    __shared__ uint32_t l4[1][kWaves];
     STAMP(a, 0, 0);
     slots_body(a, blockIdx.x, l4);
     STAMP(a, 0, 15);
@@ -1597,7 +1618,10 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     }
     if (bid >= a.nbq) {
         // ---- W-role: heartbeat purge of slots [b*256, +256)
-        slots_body(a, bid - a.nbq - nbf, l4);
+        __shared__ uint32_t l4w[4][kWaves];
+        if (a.wtiles == 4) slots_body<4>(a, 4 * (bid - a.nbq - nbf), l4w);
+        else if (a.wtiles == 2) slots_body<2>(a, 2 * (bid - a.nbq - nbf), l4w);
+        else slots_body(a, bid - a.nbq - nbf, l4w);
         STAMP(a, SO, 15);
         return;
     }
@@ -4903,7 +4927,7 @@ void launch_slots(const TickArgs &a, Stream st) {
 }
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
-    const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : a.nbw;
+    const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : (a.wtiles > 1 ? (a.nbw + a.wtiles - 1) / a.wtiles : a.nbw);
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;
     FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq + (a.cm_fold ? a.cm_blocks : 0)), nbf ? lds : 0, st, a);
 }

@@ -496,6 +496,15 @@ def test_config3_logscan(logscan):
     test_config3_full_size()
 
 
+@pytest.mark.parametrize("wtiles", [1, 2])
+@pytest.mark.parametrize("seed", range(2))
+def test_random_multitick_logscan_plan_wtiles(logscan, force_plan, monkeypatch, seed, wtiles):
+    """k_scan's slot purge with 1 or 2 tiles per W workgroup (fb_set_path("wtiles"); large
+    tables default to 4, fused ones to 1)."""
+    monkeypatch.setitem(TEST_PATHS, "wtiles", wtiles)
+    test_random_multitick_vs_oracle(seed + 30)
+
+
 @pytest.mark.parametrize("seed", range(3))
 def test_random_multitick_logscan_plan_no_cmix(logscan, force_plan, monkeypatch, seed):
     """k_emit2's grid in role order (fb_set_path("cmix", 0)): queue blocks, then the
