@@ -1067,6 +1067,9 @@ int enqueue_tick(fb_ctx *c) {
         // (only while the log role is fused into k_scan: with k_logscan the slot blocks are
         // the short ones)
         a.wfirst = (a.shard == 1 && !a.f_sep && c->wfirst_on) ? 1 : 0;
+        // sharded phase 1: 4 slot tiles per workgroup while the log role has its own launch
+        // (N = 2 at configs[3]: scan 18.4 -> 17.8 us), 1 behind wfirst (N = 8: no gain)
+        if (a.shard == 1) a.wtiles = c->wtiles ? c->wtiles : (a.wfirst ? 1 : 4);
         a.slot_base = c->slot_base;
         a.rank = c->rank;
         a.world = c->world;
