@@ -881,6 +881,7 @@ int enqueue_tick(fb_ctx *c) {
         // the slot purge (k_scan's W role) runs in k_ev_apply_ll's launch: extra blocks for
         // the untouched slots, each owner thread for its touched slot
         ea.nbw = nbw;
+        ea.wtiles = c->wtiles ? c->wtiles : (nbw >= 1024 ? 4 : 1);
         ea.now = c->l_now;
         ea.st = c->st;
         ea.free_out = c->free_[nxt];

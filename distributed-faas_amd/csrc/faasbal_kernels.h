@@ -243,9 +243,11 @@ struct EvArgs {
     // the previous tick's deferred commit, run by k_ev_link's blocks past the link grid
     int cm_blocks;
     CommitArgs cm;
-    // the slot purge (k_scan's W role) in k_ev_apply_ll's launch: nbw blocks past the
-    // apply grid purge the untouched slots, each owner thread its touched slot
+    // the slot purge (k_scan's W role) in k_ev_apply_ll's launch: nbw tiles of 256 slots,
+    // wtiles per workgroup, past the apply grid purge the untouched slots, each owner
+    // thread its touched slot
     int nbw;
+    int wtiles;
     double now;
     uint8_t *st;
     int2 *free_out;

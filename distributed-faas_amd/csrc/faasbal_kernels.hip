@@ -1011,36 +1011,53 @@ __device__ __forceinline__ bool SlotRun::purge(const EvArgs &a, uint32_t s, int 
 __device__ __forceinline__ bool apply_run(const EvArgs &a, SlotRun &r, uint32_t s, int e, int hidx, int kind0,
                                           int32_t val0, double ts0, int64_t seq0, int reg0, bool &ev);
 
-// k_ev_apply_ll's slot blocks: the purge of untouched slots, one slot per thread, block
-// blk = slots [256 blk, +256)
-__device__ __forceinline__ void apply_slot_block(const EvArgs &a, int blk) {
-    const int s = blk * kBS + (int)threadIdx.x;
-    bool died = false, evicted = false, queued = false;
-    uint32_t no = 0;
-    if (s < a.W) {
+// k_ev_apply_ll's slot blocks: the purge of untouched slots, one slot per thread, NT tiles
+// of 256 slots from tile blk0 (every tile's loads issued before the first tile's purge)
+template <int NT>
+__device__ __forceinline__ void apply_slot_tiles(const EvArgs &a, int blk0) {
+    bool tv[NT];
+    int regv[NT];
+    double hbv[NT];
+    int2 fqv[NT];
+    int32_t bv[NT];
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int s = (blk0 + j) * kBS + (int)threadIdx.x;
+        const int sc = s < a.W ? s : (a.W > 0 ? a.W - 1 : 0);
         // the link stamp says whether the slot got messages (its owner purges it); the
         // committed record loaded with it (no dependent round)
-        const bool t = (uint32_t)(a.ev_head[s] >> 32) == a.link;
-        const int reg0 = a.reg[s];
-        const double hb0 = a.hb[s];
-        const int2 fq0 = a.free_in[s];
-        const int32_t b0 = a.bud ? a.bud[s] : 0;
-        const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(b0 - fq0.x) : 0u;
-        bool alive;
-        if (!t)
-            no = purge_slot(a, s, false, reg0, reg0, hb0, fq0.x, 0, fq0.y != 0, fq0.y, in0, died, evicted, alive,
-                            queued);
+        tv[j] = (uint32_t)(a.ev_head[sc] >> 32) == a.link;
+        regv[j] = a.reg[sc];
+        hbv[j] = a.hb[sc];
+        fqv[j] = a.free_in[sc];
+        bv[j] = a.bud ? a.bud[sc] : 0;
     }
-    const uint64_t dm = __ballot(died);
-    const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
-    const uint32_t nq = (uint32_t)__popcll(__ballot(queued));
-    const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
-    if (lane_id() == 0) {
-        if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
-        if (a.died_tag && dm) *a.died_tag = a.lstamp;
-        if (ne) count_evicted(a, blk, ne);
-        count_orphans(a, blk, nw);
-        if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+        const int blk = blk0 + j;
+        const int s = blk * kBS + (int)threadIdx.x;
+        bool died = false, evicted = false, queued = false;
+        uint32_t no = 0;
+        if (s < a.W) {
+            const int reg0 = regv[j];
+            const int2 fq0 = fqv[j];
+            const uint32_t in0 = (a.bud && reg0) ? (uint32_t)(bv[j] - fq0.x) : 0u;
+            bool alive;
+            if (!tv[j])
+                no = purge_slot(a, s, false, reg0, reg0, hbv[j], fq0.x, 0, fq0.y != 0, fq0.y, in0, died, evicted,
+                                alive, queued);
+        }
+        const uint64_t dm = __ballot(died);
+        const uint32_t ne = (uint32_t)__popcll(__ballot(evicted));
+        const uint32_t nq = (uint32_t)__popcll(__ballot(queued));
+        const uint32_t nw = a.orph_grp ? wave_sum_u32(no) : 0u;
+        if (lane_id() == 0) {
+            if (a.dmask && dm) atomicOr(&a.dmask[s >> 6], (unsigned long long)dm);
+            if (a.died_tag && dm) *a.died_tag = a.lstamp;
+            if (ne) count_evicted(a, blk, ne);
+            count_orphans(a, blk, nw);
+            if (a.wpart) count_wpart(a, blk * kWaves + wave_id(), ne, nq);
+        }
     }
 }
 
@@ -1065,9 +1082,11 @@ __device__ __forceinline__ void apply_slot_block(const EvArgs &a, int blk) {
 __global__ __launch_bounds__(kBS) void k_ev_apply_ll(EvArgs a) {
     prefetch_args(a);
     APPLY_STAMP(0);
-    const int nba = (int)gridDim.x - a.nbw;  // apply blocks; the rest purge untouched slots
+    const int nwb = a.wtiles == 4 ? (a.nbw + 3) / 4 : a.nbw;
+    const int nba = (int)gridDim.x - nwb;  // apply blocks; the rest purge untouched slots
     if ((int)blockIdx.x >= nba) {
-        apply_slot_block(a, (int)blockIdx.x - nba);
+        if (a.wtiles == 4) apply_slot_tiles<4>(a, 4 * ((int)blockIdx.x - nba));
+        else apply_slot_tiles<1>(a, (int)blockIdx.x - nba);
         APPLY_EXIT();
         return;
     }
@@ -4894,7 +4913,8 @@ void launch_ev_link(const EvArgs &a, Stream st) {
     hipExtLaunchKernelGGL(k_ev_link, dim3(grid + a.cm_blocks), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_ev_apply_ll(const EvArgs &a, Stream st) {
-    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + a.nbw), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
+    const int nwb = a.wtiles == 4 ? (a.nbw + 3) / 4 : a.nbw;
+    hipExtLaunchKernelGGL(k_ev_apply_ll, dim3(cdiv(a.E, kBS) + nwb), dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
 }
 void launch_copy_multi(const CopyMulti &m, Stream st) {
     if (m.n <= 0 && m.otiles <= 0) return;

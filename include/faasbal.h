@@ -279,8 +279,9 @@ int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_to
  *                 (while the log role is fused into k_scan), 0 queue blocks first;
  *   "cmix"        k_emit2 on unfused ticks: 1 compaction workgroups interleaved with the queue
  *                 blocks, 0 after them;
- *   "wtiles"      slot tiles (256 slots each) per k_scan slot-purge workgroup: 0 auto (4 on
- *                 unfused tables, 1 fused), or 1, 2, 4;
+ *   "wtiles"      slot tiles (256 slots each) per slot-purge workgroup: 0 auto (k_scan: 4 on
+ *                 unfused tables, 1 fused; k_ev_apply_ll: 4 from 1024 tiles), or 1, 2, 4
+ *                 (k_ev_apply_ll: 2 runs as 1);
  *   "gpcheck"     diagnostic (stamps builds): k_plan2 runs beside a gp tick for comparison.
  * Between ticks only; FB_EINVAL for an unknown name or value. */
 int fb_set_path(fb_ctx *ctx, const char *name, int value);

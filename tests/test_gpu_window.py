@@ -336,3 +336,20 @@ def test_window_random_ticketed_chunks_vs_oracle(monkeypatch, seed):
     from faasbal.balancer import TEST_PATHS
     monkeypatch.setitem(TEST_PATHS, "win_direct", 0)
     test_window_random_vs_oracle(seed)
+
+
+@pytest.mark.parametrize("seed", range(1, 24, 6))
+def test_window_random_four_slot_tiles_vs_oracle(monkeypatch, seed):
+    """The slot purge in k_ev_apply_ll (and k_scan) with four 256-slot tiles per workgroup
+    (fb_set_path("wtiles", 4), the default from 1024 tiles) on small tables."""
+    from faasbal.balancer import TEST_PATHS
+    monkeypatch.setitem(TEST_PATHS, "wtiles", 4)
+    test_window_random_vs_oracle(seed)
+
+
+def test_window_stream_four_slot_tiles_vs_oracle(monkeypatch):
+    """configs[4]'s event mix (20 000 slots: 79 tiles, a partial last group of four) with
+    the four-tile slot purge forced."""
+    from faasbal.balancer import TEST_PATHS
+    monkeypatch.setitem(TEST_PATHS, "wtiles", 4)
+    test_window_stream_vs_oracle(3, 20000, 2048, 0.05, False)
