@@ -322,7 +322,9 @@ def bench_stream(args, dist=None, world=1, rank=0, dev=0):
     # roofline: the dominant kernel's share of SURVEY.md 8(d)'s tick bytes (one GPU: the apply
     # launch carries the slot purge, 24 B per worker, and the messages, 17 B each) over its
     # event-timed launch average; tick_frac: the whole tick's 8(d) bytes on the driver's clock
-    dom = max(kern, key=lambda k: kern[k])
+    # (by time per tick: a kernel of the occasional general tick -- k_scan, ~22 us once in
+    # ~17 ticks -- may take longer per launch than the apply that runs every tick)
+    dom = max(per_tick, key=lambda k: per_tick[k])
     Eavg = stats["events"] / K
     dom_bytes = (24 * W // world + 17 * Eavg) if dom == "ev_apply" else None
     traffic, traffic_src = None, None
