@@ -1522,7 +1522,7 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
 // F-blocks flag orphaned log entries (died bitmap in LDS); Q-blocks compute the
 // effective free count c of every LRU position and the block's count of c > r
 // for every round r (table laid out [block][round]).
-template <int MODE>
+template <int MODE, int WT>
 __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     STAMP_TOP(a_, a_.nbw);
     prefetch_args(a_);
@@ -1637,10 +1637,10 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     }
     if (bid >= a.nbq) {
         // ---- W-role: heartbeat purge of slots [b*256, +256)
-        __shared__ uint32_t l4w[4][kWaves];
-        if (a.wtiles == 4) slots_body<4>(a, 4 * (bid - a.nbq - nbf), l4w);
-        else if (a.wtiles == 2) slots_body<2>(a, 2 * (bid - a.nbq - nbf), l4w);
-        else slots_body(a, bid - a.nbq - nbf, l4w);
+        // WT tiles per workgroup (a.wtiles; its own instance, so the one-tile form -- fused
+        // ticks -- keeps its registers and occupancy)
+        __shared__ uint32_t l4w[WT][kWaves];
+        slots_body<WT>(a, WT * (bid - a.nbq - nbf), l4w);
         STAMP(a, SO, 15);
         return;
     }
@@ -4945,11 +4945,23 @@ static int tick_mode(const TickArgs &a) { return a.deque ? kModeDeque : (a.E == 
 void launch_slots(const TickArgs &a, Stream st) {
     FB_LAUNCH_MODE(k_slots, dim3(a.nbw), 0, st, a);
 }
+template <int WT>
+static void launch_scan_t(const TickArgs &a, dim3 g, size_t lds, Stream st) {
+    switch (tick_mode(a)) {
+    case kModeIdle: hipExtLaunchKernelGGL((k_scan<kModeIdle, WT>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    case kModeEvents: hipExtLaunchKernelGGL((k_scan<kModeEvents, WT>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    default: hipExtLaunchKernelGGL((k_scan<kModeDeque, WT>), g, dim3(kBS), lds, st.s, st.e0, st.e1, 0, a); break;
+    }
+}
 void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
     const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : (a.wtiles > 1 ? (a.nbw + a.wtiles - 1) / a.wtiles : a.nbw);
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;
-    FB_LAUNCH_MODE(k_scan, dim3(nbf + nbw + a.nbq + (a.cm_fold ? a.cm_blocks : 0)), nbf ? lds : 0, st, a);
+    const dim3 g(nbf + nbw + a.nbq + (a.cm_fold ? a.cm_blocks : 0));
+    const int wt = nbw ? a.wtiles : 1;
+    if (wt == 4) launch_scan_t<4>(a, g, nbf ? lds : 0, st);
+    else if (wt == 2) launch_scan_t<2>(a, g, nbf ? lds : 0, st);
+    else launch_scan_t<1>(a, g, nbf ? lds : 0, st);
 }
 void launch_logscan(const TickArgs &a, int grid, Stream st) {
     const size_t lds = (size_t)(((a.W + 63) / 64 + 1) / 2 + 1) * 16;  // + the spare slot
