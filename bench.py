@@ -468,7 +468,31 @@ def host_observed(g, st, T, steps, n_assigned):
                     "pinned arrays, value_with_expand adds the host expansion into one slot per task"}
 
 
-def committed_tick(st, T, reps=10):
+def gated_timing(g, step, K, batch=64):
+    """Per-kernel device times of K steps run back to back on the device: each batch of
+    launches is queued behind a timing gate (fb_timing_gate) and released at once, so the
+    host's enqueue pace cannot stretch them, and the packet events of every launch
+    bracket that kernel's execution (the interval rocprofv3's kernel trace reports).  The
+    kernels of one stream never overlap, so their sum per step cannot exceed the gated
+    span per step (the gate's end to the release point's event), returned beside them."""
+    g.timing_enable(True)
+    span, done, timed_out = 0.0, 0, False
+    while done < K:
+        n = min(batch, K - done)
+        g.timing_gate(True)
+        for _ in range(n):
+            step()
+        g.timing_gate(False)
+        ms, to = g.timing_span()
+        span += ms
+        timed_out |= to
+        done += n
+    kt = g.timing_read()
+    g.timing_enable(False)
+    return {k: (ms / n, n) for k, (ms, n) in kt.items()}, span / K, timed_out
+
+
+def committed_tick(st, T, reps=5):
     """The tick with its commit.  A committed one-GPU tick defers its commit (the evicted
     records' deletion, task_dispatcher.py:246-247, and its orphans' log entries) into the
     next launch; after an idle tick that is k_scan's slot role (the records) and, on fused
@@ -477,23 +501,24 @@ def committed_tick(st, T, reps=10):
     the tick after a committed tick (same state both times): its kernels with the folded
     commit, then relaunched uncommitted without it -- the difference is the commit's
     device cost inside the step.  The commit as its own kernel (what a state read in
-    between forces) is timed beside it.  Packet-event device times, averages of `reps`."""
+    between forces) is timed beside it.  Packet-event device times of gated launches
+    (gated_timing), averages of `reps`."""
     from faasbal import GpuBalancer
     g = GpuBalancer(len(st["reg"]), 2 * len(st["log"]) + 2 * T + 16, max_events=1, device=0)
     d_fold, d_plain, d_sep = [], [], []
+
+    def step():
+        g.launch(1000.0, 10.0, n_pending=T)
+
     for _ in range(reps):
         g.load(st)
         g.launch(1000.0, 10.0, n_pending=T)
         g.wait()
         g.commit()  # deferred: the next launch runs it
-        g.timing_enable(True)
-        g.launch(1000.0, 10.0, n_pending=T)
+        k1, _, _ = gated_timing(g, step, 1)  # with the folded commit
         g.wait()
-        k1 = g.timing_read()
-        g.launch(1000.0, 10.0, n_pending=T)  # same tick, nothing left to fold
+        k2, _, _ = gated_timing(g, step, 1)  # same tick, nothing left to fold
         g.wait()
-        k2 = g.timing_read()
-        g.timing_enable(False)
         if not set(k2) <= set(k1):
             raise SystemExit("committed_tick: different kernels with and without the commit (%s / %s)"
                              % (sorted(k1), sorted(k2)))
@@ -654,6 +679,8 @@ def main():
 
     for _ in range(args.warmup):
         step()
+    if world == 1:
+        g.timing_mark()  # kernel traces: the timed region starts after this launch (tools/prof_summary.py)
     g.sync()
     # timed region: K back-to-back ticks on the device stream
     barrier()
@@ -661,19 +688,29 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
+    t_enq = time.perf_counter() - t0  # host enqueue of the K ticks (device still running)
     g.sync()
     barrier()
     dt = time.perf_counter() - t0
+    if world == 1:
+        g.timing_mark()  # ... and ends before this one
     if dist is not None:
         t = torch.tensor([dt], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
-    # per-kernel device time with HIP events on the balancer's stream (same K)
-    g.timing_enable(True)
-    for _ in range(args.steps):
-        step()
-    kt = g.timing_read()
-    g.timing_enable(False)
+    # per-kernel device time with HIP packet events on the balancer's stream (same K): one
+    # GPU, the K steps gated (run back to back on the device, gated_timing); sharded, the
+    # exchange between the phases syncs with the host (gloo), so those launches are not gated
+    gated_span_ms, gate_timed_out = None, False
+    if world == 1:
+        kern, gated_span_ms, gate_timed_out = gated_timing(g, step, args.steps)
+        g.timing_mark()  # kernel traces: the gated pass (from its gate launch) ends before this one
+    else:
+        g.timing_enable(True)
+        for _ in range(args.steps):
+            step()
+        kern = {k: (ms / n, n) for k, (ms, n) in g.timing_read().items()}
+        g.timing_enable(False)
     g.wait()
     if world > 1:
         # the exchange: all-reduce time per tick, measured alone on the same stream
@@ -688,10 +725,9 @@ def main():
                 dist.all_reduce(xb)
             ev1.record(g.stream)
         ev1.synchronize()
-        kt["exchange_allreduce"] = (ev0.elapsed_time(ev1), args.steps)
+        kern["exchange_allreduce"] = (ev0.elapsed_time(ev1) / args.steps, args.steps)
         kt_x_bytes = xb.numel()
 
-    kern = {k: (ms / n, n) for k, (ms, n) in kt.items()}
     # fused one-GPU heartbeat ticks (scan + emit only, W <= 128K slots): the emit's log
     # workgroups read the in-flight log and flag the orphans, k_scan has no log role
     log_in_emit = world == 1 and not deque and set(kern) == {"scan", "emit"} and W <= 1 << 17
@@ -733,12 +769,15 @@ def main():
         tj = json.load(open(tp)).get("entries", {}).get("%d,%d,%d" % (W, T, world))
         if tj and dom in tj["kernels"]:
             traffic = tj["kernels"][dom]["hbm_bytes"]
-            rocprof_ms = (tj["kernels"][dom].get("trace_avg_ns") or 0) * 1e-6 or None
+            kd = tj["kernels"][dom]
+            # the profile's gated timing pass (the regime kernel_avg_ms is measured in; cut at
+            # bench.py's gate launches), else all launches
+            rocprof_ms = (kd.get("trace_gated_avg_ns") or kd.get("trace_avg_ns") or 0) * 1e-6 or None
             traffic_src = ("profiles/%s_pmc.csv (2*FETCH_SIZE + WRITE_SIZE per launch, separate rocprofv3 --pmc "
                            "passes; the x2 FETCH_SIZE correction is calibrated for 16-B-per-lane streaming reads, "
-                           "so for this kernel's 4-8 B gathers the figure is an upper bound), rocprof average from "
-                           "profiles/%s_kernel_stats.csv; summary profiles/%s_traffic.json"
-                           % (tj["tag"], tj["tag"], tj["tag"]))
+                           "so for this kernel's 4-8 B gathers the figure is an upper bound), rocprof average over the "
+                           "gated timing pass from profiles/%s_kernel_timed.csv (all launches: %s_kernel_stats.csv); "
+                           "summary profiles/%s_traffic.json" % (tj["tag"], tj["tag"], tj["tag"], tj["tag"]))
     line = {
         "metric": "task assignments/sec + % HBM roofline, 1M tasks x 64K workers, 1/2/4/8 GPU",
         "value": value,
@@ -747,6 +786,7 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": dt * 1e3 / args.steps,
+        "host_enqueue_ms_per_step": t_enq * 1e3 / args.steps,
         "higher_is_better": True,
         "scaling": "weak" if args.workload == "weak" else "strong",
         "vs_baseline": None,
@@ -777,13 +817,26 @@ def main():
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes": dom_bytes, "bytes_model": bytes_model,
                      "kernel_avg_ms": dom_ms, "kernel_avg_ms_rocprof": rocprof_ms,
+                     "frac_rocprof": (dom_bytes / (rocprof_ms * 1e-3) / 1e9 / HBM_PEAK_GBS) if rocprof_ms else None,
                      "model_frac": model_frac,
                      # the whole tick on the driver's clock: SURVEY.md 8(d) tick bytes / ms_per_step
                      "tick_frac": B / (dt / args.steps) / 1e9 / HBM_PEAK_GBS},
         "tick": {"algorithmic_bytes": B, "device_ms": tick_dev_ms,
                  "achieved_GBs": B / (tick_dev_ms * 1e-3) / 1e9,
-                 "kernels_avg_ms": {k: v[0] for k, v in kern.items()}},
+                 "kernels_avg_ms": {k: v[0] for k, v in kern.items()},
+                 "kernel_timing": ("packet events of the K steps relaunched behind a timing gate (back to back on the "
+                                   "device, bench.py: gated_timing)" if world == 1 else
+                                   "packet events of K host-paced steps (the exchange syncs with the host)"),
+                 "gate_timed_out": gate_timed_out},
     }
+    # the per-kernel times must fit in the step they were measured for: their sum per step
+    # against the timed region's ms_per_step.  (The gated span itself is not a step time: the
+    # packet events add ~8 us between launches, profiles/r06b_trace_gaps.txt.)
+    lim = dt * 1e3 / args.steps * 1.05
+    line["tick"]["kernels_fit_step"] = bool(tick_dev_ms <= lim) and not gate_timed_out
+    if not line["tick"]["kernels_fit_step"]:
+        line["roofline"]["flag"] = ("per-kernel times (sum %.4f ms) exceed the step (%.4f ms x 1.05) or the gate timed "
+                                    "out: roofline.frac is not a kernel property on this run" % (tick_dev_ms, lim / 1.05))
     if deque:
         line["metric"] = "task assignments/sec, start() loop (no heartbeats), 1M tasks x 64K workers"
         line["data"] = "synthetic (faasbal.synth.zipf_deque_state, seed=0, dup_frac=0.02)"
@@ -802,13 +855,21 @@ def main():
         cm["device_ms_with_commit"] = tick_dev_ms + cm["commit_in_tick_ms"]
         cm["ms_per_step_with_commit"] = dt * 1e3 / args.steps + cm["commit_in_tick_ms"]
         cm["value_with_commit"] = n_assigned / (cm["ms_per_step_with_commit"] * 1e-3)
+        # the headline is the committed tick: value / ms_per_step carry the commit's device cost
+        # (task_dispatcher.py:246-249); the timed region's own figures stay beside them
+        line["uncommitted"] = {"value": value, "ms_per_step": dt * 1e3 / args.steps,
+                               "note": "the K timed steps alone: the functional tick relaunched, its commit not run"}
+        line["value"] = cm["value_with_commit"]
+        line["ms_per_step"] = cm["ms_per_step_with_commit"]
+        line["roofline"]["tick_frac"] = B / (cm["ms_per_step_with_commit"] * 1e-3) / 1e9 / HBM_PEAK_GBS
         cm["note"] = ("the configs[2] tick's commit (its 3277-ish evicted records' deletion and its orphaned log "
                       "entries) folded into the NEXT tick (folded): the records in k_scan's W role, the log entries "
                       "by k_emit2's log workgroup of each tile (fused ticks) or extra k_scan blocks. That next tick "
                       "runs on the committed, depleted state (kernels_ms: fewer queued positions and tasks than the "
                       "timed step's tick.kernels_avg_ms), so only the delta carries over: commit_in_tick_ms = its "
                       "kernels with the fold pending - the same tick relaunched without it (same state); "
-                      "ms_per_step_with_commit = ms_per_step + that delta")
+                      "ms_per_step_with_commit = the timed region's ms_per_step + that delta (the line's value and "
+                      "ms_per_step)")
         line["committed"] = cm
     if world == 1 and not args.no_host_observed:
         line["host_observed"] = host_observed(g, st, T, min(args.steps, 50), n_assigned)

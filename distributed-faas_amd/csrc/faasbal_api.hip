@@ -279,6 +279,12 @@ struct fb_ctx {
     bool timing = false;
     std::vector<TimedLaunch> tl;
     std::vector<hipEvent_t> ev_pool;
+    // fb_timing_gate: a host-mapped word {open sequence, timed out} the gate kernel polls,
+    // the gate's end and the batch's end
+    uint32_t *gate_h = nullptr, *gate_d = nullptr;
+    uint32_t gate_seq = 0;
+    hipEvent_t gate_a = nullptr, gate_b = nullptr;
+    int gate_state = 0;  // 1 held, 2 released (span readable)
     std::string err;
     // sharding (fb_create_sharded): this rank owns global slots [slot_base, slot_base + W)
     int shard = 0, rank = 0, world = 1;
@@ -1551,6 +1557,9 @@ int fb_destroy(fb_ctx *c) {
         if (c->use_ev[h]) hipEventDestroy(c->use_ev[h]);
     }
     if (c->tick_ev) hipEventDestroy(c->tick_ev);
+    if (c->gate_h) hipHostFree(c->gate_h);
+    if (c->gate_a) hipEventDestroy(c->gate_a);
+    if (c->gate_b) hipEventDestroy(c->gate_b);
     if (c->cp_s) hipStreamDestroy(c->cp_s);
     for (auto &t : c->tl) {
         hipEventDestroy(t.a);
@@ -2901,6 +2910,61 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
 int fb_timing_enable(fb_ctx *c, int enable) {
     if (!c) return FB_EINVAL;
     c->timing = enable != 0;
+    return FB_OK;
+}
+
+int fb_timing_gate(fb_ctx *c, int hold) {
+    if (!c) return FB_EINVAL;
+    HIPCHK(c, hipSetDevice(c->device));
+    if (hold) {
+        if (c->gate_state == 1) return fail(c, FB_ESTATE, "fb_timing_gate: the gate is already held");
+        if (!c->gate_h) {
+            if (hipHostMalloc((void **)&c->gate_h, 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess)
+                return fail(c, FB_ENOMEM, "fb_timing_gate: hipHostMalloc failed");
+            memset(c->gate_h, 0, 64);
+            HIPCHK(c, hipHostGetDevicePointer((void **)&c->gate_d, c->gate_h, 0));
+            HIPCHK(c, hipEventCreate(&c->gate_a));
+            HIPCHK(c, hipEventCreate(&c->gate_b));
+        }
+        // (a pending deferred commit stays pending: it rides in the next gated launch as usual)
+        if (++c->gate_seq == 0) c->gate_seq = 1;
+        __atomic_store_n(&c->gate_h[1], 0u, __ATOMIC_RELEASE);
+        // the gate opens by itself after 0.5 s (5e7 ticks of the 100 MHz counter)
+        launch_gate(c->gate_d, c->gate_seq, 50000000ull, Stream(c->stream, nullptr, c->gate_a));
+        HIPCHK(c, hipGetLastError());
+        c->gate_state = 1;
+        return FB_OK;
+    }
+    if (c->gate_state != 1) return fail(c, FB_ESTATE, "fb_timing_gate(0) without a held gate");
+    HIPCHK(c, hipEventRecord(c->gate_b, c->stream));
+    __atomic_store_n(&c->gate_h[0], c->gate_seq, __ATOMIC_RELEASE);
+    c->gate_state = 2;
+    return FB_OK;
+}
+
+int fb_timing_mark(fb_ctx *c) {
+    if (!c) return FB_EINVAL;
+    if (c->gate_state == 1) return fail(c, FB_ESTATE, "fb_timing_mark while the gate is held");
+    HIPCHK(c, hipSetDevice(c->device));
+    if (!c->gate_h) {
+        // (the gate's word, so the mark finds it open)
+        if (int rc_ = fb_timing_gate(c, 1)) return rc_;
+        return fb_timing_gate(c, 0);
+    }
+    launch_gate(c->gate_d, c->gate_seq, 50000000ull, Stream(c->stream));
+    HIPCHK(c, hipGetLastError());
+    return FB_OK;
+}
+
+int fb_timing_span(fb_ctx *c, double *ms, int32_t *timed_out) {
+    if (!c) return FB_EINVAL;
+    if (c->gate_state != 2) return fail(c, FB_ESTATE, "fb_timing_span without a released gate");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, stream_wait(c));
+    float f = 0;
+    HIPCHK(c, hipEventElapsedTime(&f, c->gate_a, c->gate_b));
+    if (ms) *ms = f;
+    if (timed_out) *timed_out = (int32_t)__atomic_load_n(&c->gate_h[1], __ATOMIC_ACQUIRE);
     return FB_OK;
 }
 

@@ -474,6 +474,9 @@ void launch_ev_apply(const EvArgs &a, Stream st);
 void launch_ev_link(const EvArgs &a, Stream st);
 void launch_ev_apply_ll(const EvArgs &a, Stream st);
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
+// a one-lane kernel that holds the stream until flag[0] == want (host-mapped word) or
+// `limit` ticks of the 100 MHz realtime counter pass (then flag[1] = 1)
+void launch_gate(uint32_t *flag, uint32_t want, uint64_t limit, Stream st);
 void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
 void launch_logscan(const TickArgs &a, int grid, Stream st);

@@ -4930,6 +4930,25 @@ void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st)
     const int grid = (int)std::min<int64_t>(std::max<int64_t>(1, (n + 8 * kBS - 1) / (8 * kBS)), 2048);
     hipExtLaunchKernelGGL(k_copy_words, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, dst, src, n);
 }
+// Timing gate (fb_timing_gate): one lane polls a host-mapped word until the host stores
+// `want` into it, so the launches queued behind this kernel run back to back, free of
+// the host's enqueue pace.  Every exit path is bounded: after `limit` ticks of the
+// 100 MHz realtime counter the gate opens by itself and reports it in flag[1].
+__global__ __launch_bounds__(64) void k_gate(uint32_t *flag, uint32_t want, uint64_t limit) {
+    if (threadIdx.x != 0) return;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+        if (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) == want) return;
+        if (__builtin_amdgcn_s_memrealtime() - t0 > limit) {
+            __hip_atomic_store(flag + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            return;
+        }
+        __builtin_amdgcn_s_sleep(8);
+    }
+}
+void launch_gate(uint32_t *flag, uint32_t want, uint64_t limit, Stream st) {
+    hipExtLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st.s, st.e0, st.e1, 0, flag, want, limit);
+}
 void launch_selftest(uint32_t *err, uint32_t seed, Stream st) {
     hipExtLaunchKernelGGL(k_selftest, dim3(64), dim3(kBS), 0, st.s, st.e0, st.e1, 0, err, seed);
 }

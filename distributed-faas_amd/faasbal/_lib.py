@@ -27,7 +27,8 @@ EXPORTS = ("fb_create", "fb_destroy", "fb_last_error", "fb_load_state", "fb_read
            "fb_host_free", "fb_purge_launch", "fb_apply_events", "fb_purge", "fb_assign", "fb_get_outputs",
            "fb_read_inflight", "fb_set_compact", "fb_get_outputs_compact", "fb_expand_compact",
            "fb_set_window", "fb_window_stats", "fb_set_compact_out", "fb_set_eager_commit", "fb_set_path",
-           "fb_set_round_hint", "fb_set_full_assign")
+           "fb_set_round_hint", "fb_set_full_assign", "fb_timing_gate", "fb_timing_span",
+           "fb_timing_mark")
 
 
 class TickResult(C.Structure):
@@ -105,6 +106,9 @@ def load(path=None):
         "fb_timing_enable": (C.c_int, [_P, C.c_int]),
         "fb_timing_read": (C.c_int, [_P, i32, C.POINTER(C.c_char_p), C.POINTER(dbl), C.POINTER(i64),
                                      C.POINTER(i32)]),
+        "fb_timing_gate": (C.c_int, [_P, C.c_int]),
+        "fb_timing_mark": (C.c_int, [_P]),
+        "fb_timing_span": (C.c_int, [_P, C.POINTER(dbl), C.POINTER(i32)]),
         "fb_debug_read": (C.c_int, [_P, _P, i64, C.POINTER(i64)]),
         "fb_selftest": (C.c_int, [_P, C.POINTER(i32)]),
         "fb_sync": (C.c_int, [_P]),

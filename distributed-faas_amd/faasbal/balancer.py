@@ -432,6 +432,21 @@ class GpuBalancer:
         self._chk(self.lib.fb_timing_read(self.h, max_kernels, names, ms, cnt, C.byref(n)))
         return {names[i].decode(): (ms[i], cnt[i]) for i in range(n.value)}
 
+    def timing_gate(self, hold):
+        """hold=True: hold the stream (launches queue up behind a gate kernel); False: release.
+        Measurement only: the gated launches then run back to back on the device."""
+        self._chk(self.lib.fb_timing_gate(self.h, 1 if hold else 0))
+
+    def timing_mark(self):
+        """A marker launch (the open gate kernel) that kernel traces can cut a region at."""
+        self._chk(self.lib.fb_timing_mark(self.h))
+
+    def timing_span(self):
+        """(ms from the gate's end to the release point, gate timed out) after a released gate."""
+        ms, to = C.c_double(), C.c_int32()
+        self._chk(self.lib.fb_timing_span(self.h, C.byref(ms), C.byref(to)))
+        return ms.value, bool(to.value)
+
     def selftest(self):
         e = C.c_int32()
         self._chk(self.lib.fb_selftest(self.h, C.byref(e)))

@@ -251,6 +251,18 @@ int fb_timing_enable(fb_ctx *ctx, int enable);
 int fb_timing_read(fb_ctx *ctx, int32_t max_kernels, const char **names, double *total_ms,
                    int64_t *launches, int32_t *n_kernels);
 
+/* Timing gate (measurement only): hold=1 enqueues a one-lane kernel that holds the
+ * context stream until hold=0 releases it, so the launches queued in between run back
+ * to back on the device whatever the host's enqueue pace (the gate opens by itself
+ * after 0.5 s).  fb_timing_span syncs and returns the device time from the gate's end
+ * to the release point's event, and whether the gate timed out.  Per-kernel times of
+ * the gated launches come from fb_timing_read as usual. */
+int fb_timing_gate(fb_ctx *ctx, int hold);
+int fb_timing_span(fb_ctx *ctx, double *ms, int32_t *timed_out);
+/* A marker launch for profiles: the gate kernel, already open (it returns at once), so a
+ * kernel trace can cut a benchmark's timed region out of the run. */
+int fb_timing_mark(fb_ctx *ctx);
+
 /* Device self-test of the kernels' wave/block scan primitives; *errors = 0 on success. */
 int fb_selftest(fb_ctx *ctx, int32_t *errors);
 

@@ -310,6 +310,39 @@ def test_relaunch_without_commit_is_identical():
             np.testing.assert_array_equal(u, v)
 
 
+def test_timing_gate_keeps_results():
+    """bench.py's measurement hooks change no result: ticks queued behind the timing gate
+    (released at once), marker launches between them, and a committed tick whose deferred
+    commit rides in the gated launch, all against the oracle."""
+    st = synth.zipf_state(W=4096, seed=7)
+    g, o = _pair(st, len(st["log"]) * 2 + 400_000)
+    g.timing_mark()
+    g.timing_enable(True)
+    g.timing_gate(True)
+    for _ in range(3):
+        g.launch(1000.0, 10.0, n_pending=50_000)
+    g.timing_gate(False)
+    ms, timed_out = g.timing_span()
+    kt = g.timing_read()
+    g.timing_enable(False)
+    assert not timed_out and ms > 0 and kt and all(n == 3 for _, n in kt.values())
+    g.wait()
+    b = o.tick(1000.0, 10.0, [], [], [], [], [], 50_000)
+    _cmp_out(dict(reconnect=g.event_status(), assign=g.assignments(), orphans=g.orphans(), evicted=g.evicted()),
+              b, 0)
+    g.commit()  # deferred into the next (gated) launch
+    g.timing_mark()
+    g.timing_gate(True)
+    g.launch(1001.0, 10.0, n_pending=20_000)
+    g.timing_gate(False)
+    g.wait()
+    b = o.tick(1001.0, 10.0, [], [], [], [], [], 20_000)
+    _cmp_out(dict(reconnect=g.event_status(), assign=g.assignments(), orphans=g.orphans(), evicted=g.evicted()),
+              b, 1)
+    g.commit()
+    _cmp_state(g, o, 1)
+
+
 def test_wide_free_counts_rerun():
     """A result pushes free past the launch's round table: the tick reruns wider."""
     W = 3
