@@ -391,15 +391,15 @@ def self_launch(args):
 
 def host_observed(g, st, T, steps, n_assigned):
     """Decisions the Python host can act on, on the path the drop-in dispatcher uses
-    (GpuPushDispatcher._run -> GpuBalancer.tick(pinned=True), dispatcher.py:307-391): per
-    tick launch, wait, the per-message status bytes and one readback of the per-task
-    slots, orphans and evicted slots into reusable pinned arrays.  The tick is relaunched
-    uncommitted (same workload every step); the commit (one kernel, then the host's
-    bookkeeping) is timed separately and added per tick.  Beside it, the compact form
-    (slot and min(c, L + 1) per LRU position, 5 B per queued worker, written into
-    registered pinned arrays by the tick itself) and its host expansion into the per-task
-    array -- a consumer that can walk rounds instead of tasks."""
-    Q = len(st["queue"])
+    (GpuPushDispatcher._run -> GpuBalancer.tick(compact=True), dispatcher.py): per tick
+    launch, wait, the per-message status bytes and the compact assignments -- slot and
+    min(c, L + 1) per LRU position, written by the tick itself into registered pinned
+    arrays, 5 B per queued worker -- with the orphans and evicted slots.  The dispatcher
+    expands the compact form round by round while it sends (CompactAssignments); the
+    whole expansion is timed beside it.  The tick is relaunched uncommitted (same
+    workload every step); the commit (one kernel, then the host's bookkeeping) is timed
+    separately and added per tick.  The per-task readback (4 B per task into pinned
+    arrays, the dispatcher's path until round 5) is timed beside it too."""
 
     def timed(step):
         for _ in range(3):
@@ -410,11 +410,27 @@ def host_observed(g, st, T, steps, n_assigned):
             step()
         return (time.perf_counter() - t0) / steps
 
-    def tick_path():
+    def compact_path():
+        out = g.tick(1000.0, 10.0, n_pending=T, commit=False, compact=True, pinned=True)
+        assert len(out["assign"]) == n_assigned
+
+    def per_task_path():
         out = g.tick(1000.0, 10.0, n_pending=T, commit=False, pinned=True)
         assert len(out["assign"]) == n_assigned
 
-    dt_t = timed(tick_path)
+    dt_c = timed(compact_path)
+    # the whole expansion of one tick's compact form (what the dispatcher's send loop walks)
+    out = g.tick(1000.0, 10.0, n_pending=T, commit=False, compact=True, pinned=True)
+    ca = out["assign"]
+    te = time.perf_counter()
+    for _ in range(5):
+        full = ca.array()
+    t_exp = (time.perf_counter() - te) / 5
+    ref = g.tick(1000.0, 10.0, n_pending=T, commit=False, pinned=True)["assign"]
+    if not np.array_equal(full, ref[:n_assigned]):
+        raise SystemExit("host_observed: the expanded compact form differs from the per-task readback")
+    g.set_compact(False)
+    dt_t = timed(per_task_path)
     # the commit (one kernel + host bookkeeping), averaged over a few ticks, the
     # state reloaded (untimed) after each so every commit is the same tick's
     tc, nc = 0.0, 5
@@ -427,45 +443,19 @@ def host_observed(g, st, T, steps, n_assigned):
         tc += time.perf_counter() - t1
         g.load(st)
     tc /= nc
-    # the compact form, for comparison
-    g.set_compact(True)
-    g.launch(1000.0, 10.0, n_pending=T)
-    g.wait()
-    obuf = g.pinned(max(len(st["log"]), 1), np.int64)  # room for every in-flight entry (fb_set_compact_out)
-    ebuf = g.pinned(max(len(st["reg"]), 1), np.int32)  # room for every worker
-    sbuf, cbuf = g.pinned(Q + 16, np.int32), g.pinned(Q + 16, np.uint8)
-    g.set_compact_out(sbuf, cbuf, obuf, ebuf)
-
-    def compact_path():
-        g.launch(1000.0, 10.0, n_pending=T)
-        g.wait()
-        g.outputs_compact(sbuf, cbuf, obuf, ebuf)
-
-    dt_c = timed(compact_path)
-    g.set_compact_out(None, None, None, None)
-    g.launch(1000.0, 10.0, n_pending=T)
-    g.wait()
-    sl, cc, _, _ = g.outputs_compact(sbuf, cbuf, obuf, ebuf)
-    out = np.zeros(max(n_assigned, 1), np.int32)
-    g.expand(sl, cc, out)
-    te = time.perf_counter()
-    for _ in range(5):
-        g.expand(sl, cc, out)
-    t_exp = (time.perf_counter() - te) / 5
-    ref = g.tick(1000.0, 10.0, n_pending=T, commit=False, pinned=True)["assign"]
-    if not np.array_equal(out[:n_assigned], ref[:n_assigned]):
-        raise SystemExit("host_observed: the expanded compact form differs from the per-task readback")
-    g.set_compact(False)
-    return {"value": n_assigned / (dt_t + tc), "unit": "assignments/s", "ms_per_tick": (dt_t + tc) * 1e3,
-            "readback_ms_per_tick": dt_t * 1e3, "commit_ms": tc * 1e3, "readback_bytes": 4 * n_assigned,
-            "readback_form": "per task: GpuBalancer.tick(pinned=True), the dispatcher's path -- status bytes + "
-                             "slots / orphans / evicted in one readback into reusable pinned arrays",
-            "compact": {"value": n_assigned / (dt_c + tc), "ms_per_tick": (dt_c + tc) * 1e3,
-                        "readback_bytes": 5 * len(sl), "expand_ms": t_exp * 1e3,
-                        "value_with_expand": n_assigned / (dt_c + tc + t_exp)},
+    Q = len(st["queue"])
+    return {"value": n_assigned / (dt_c + tc), "unit": "assignments/s", "ms_per_tick": (dt_c + tc) * 1e3,
+            "readback_ms_per_tick": dt_c * 1e3, "commit_ms": tc * 1e3, "readback_bytes": 5 * Q,
+            "readback_form": "compact, the dispatcher's path: GpuBalancer.tick(compact=True) -- status bytes + slot "
+                             "and min(c, L+1) per LRU position written by the tick into registered pinned arrays, "
+                             "orphans / evicted in the same readback",
+            "expand_ms": t_exp * 1e3, "value_with_expand": n_assigned / (dt_c + tc + t_exp),
+            "per_task": {"value": n_assigned / (dt_t + tc), "ms_per_tick": (dt_t + tc) * 1e3,
+                         "readback_bytes": 4 * n_assigned,
+                         "form": "GpuBalancer.tick(pinned=True): slot per task into reusable pinned arrays"},
             "note": "launch + wait + readback of the tick's decisions (uncommitted relaunch), plus the commit "
-                    "(average of 5); compact: the tick writes slot + min(c, L+1) per LRU position into registered "
-                    "pinned arrays, value_with_expand adds the host expansion into one slot per task"}
+                    "(average of 5); the dispatcher expands the compact form round by round as it sends "
+                    "(faasbal.balancer.CompactAssignments), value_with_expand adds the whole expansion in numpy"}
 
 
 def gated_timing(g, step, K, batch=64):

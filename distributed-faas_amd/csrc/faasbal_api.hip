@@ -246,6 +246,7 @@ struct fb_ctx {
     int rs_wide = 1;       // "rs_wide": 0 8-bit sort digits only (the path past kRsWideMaxBlocks tiles)
     int logscan = -1;      // "logscan": -1 auto (k_logscan for large tables when the bitmap fits in LDS)
     int ncu = 0, max_lds = 0;
+    int win_occ = 0;       // k_emit_win workgroups resident per CU (occupancy calculator)
     int split_slots = -1;  // "split_slots": -1 auto (separate k_slots launch once the records outgrow L2)
     // "fault_qlen": the next fb_tick_wait overwrites the device-reported queue length with this
     // value before validating it (tests of check_lengths; -1 = off)
@@ -739,6 +740,7 @@ int enqueue_tick(fb_ctx *c) {
         if (c->phase != 2 && !(E == 0 && c->xz_ok)) HIPCHK(c, hipMemsetAsync(c->xbuf, 0, xl.c8, c->stream));
     }
     TickArgs a{};
+    a.fault_qlen = -1;
     a.W = W;
     a.E = E;
     a.R = R;
@@ -1055,7 +1057,6 @@ int enqueue_tick(fb_ctx *c) {
     if (c->l_cout) {
         a.rb_slot = c->cout_slot;
         a.rb_c = c->cout_c;
-        a.evicted = c->cout_ev;
     }
     a.arena = (char *)c->arena;
     a.arena32 = c->arena_bytes < ((size_t)1 << 32) ? 1 : 0;
@@ -1067,7 +1068,8 @@ int enqueue_tick(fb_ctx *c) {
 
     a.c_hb = c->c_hb;
     a.orphans = c->orphans;
-    a.evicted = c->evicted;
+    // (registered pinned outputs: the evicted slots straight into the caller's array)
+    a.evicted = c->l_cout ? c->cout_ev : c->evicted;
     a.hout = c->hout_dev;
     if (c->shard) {
         a.shard = c->phase == 2 ? 2 : 1;
@@ -1171,10 +1173,15 @@ int enqueue_tick(fb_ctx *c) {
         a.pos_in = c->pos_of[qc];
         a.tomb = c->tomb;
         a.lstamp = c->lstamp;
+        // (a test's injected length goes to the device, which checks what an eager commit reads)
+        a.fault_qlen = c->fault_qlen;
         const int nch = a.nchB + a.nchF + a.nchW;
-        // few enough chunks to be resident together (k_emit_win holds 6 workgroups per CU):
-        // chunk = workgroup index, no ticket round before the element loads
-        a.win_direct = (c->win_direct && nch <= 4 * c->ncu) ? 1 : 0;
+        // few enough chunks to be resident together: chunk = workgroup index, no ticket round
+        // before the element loads.  A chunk's look-back waits on lower chunks only, so the
+        // direct form needs every lower-indexed workgroup resident or done -- guaranteed while
+        // the whole grid fits at once (the occupancy calculator's workgroups per CU, context
+        // creation), with half of it left to concurrent work on the device
+        a.win_direct = (c->win_direct && 2 * (int64_t)nch <= (int64_t)c->win_occ * c->ncu) ? 1 : 0;
         a.lpart = c->lpart;
         a.died_tag = c->died_tag;
         a.n_lpart = head > 0 ? ls_grid : 0;
@@ -1474,6 +1481,7 @@ int create_ctx(fb_ctx **out, int32_t max_workers, int64_t max_log, int32_t max_e
     if (!rc && (hipDeviceGetAttribute(&c->ncu, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess ||
                 hipDeviceGetAttribute(&c->max_lds, hipDeviceAttributeMaxSharedMemoryPerBlock, device) != hipSuccess))
         rc = FB_EHIP;
+    if (!rc) c->win_occ = emit_win_resident_per_cu();
     if (!rc && hipHostMalloc(&c->h_stage, (size_t)E * 32 * 2, hipHostMallocDefault) != hipSuccess) rc = FB_ENOMEM;
     for (int h = 0; h < 2 && !rc; ++h)
         if (hipEventCreateWithFlags(&c->stage_ev[h], hipEventDisableTiming) != hipSuccess ||
@@ -2301,6 +2309,7 @@ int fb_tick_wait(fb_ctx *c, fb_tick_result *res) {
         if (rc) return rc;
     }
     if (c->fault_qlen >= 0) {
+        // (a window tick reported the injected length from the device already)
         c->hout->new_qlen = c->fault_qlen;
         c->hout->win_qlen = c->fault_qlen;
         c->fault_qlen = -1;

@@ -34,8 +34,8 @@ constexpr int kXGroupBlocks = 16;
 constexpr int kXGroupDigits = 4;
 constexpr int kXGroupR = 32;
 __host__ __device__ constexpr int xg_row(int R) { return (kXGroupDigits * xr_stride(R) + 15) & ~15; }
-constexpr int kXgAccStride = 36;
-constexpr int kXsBlocks = 64;  // k_xscan: queue blocks per workgroup (chunk): a lane per block  // words per group accumulator row (R + 1 = 33 columns)
+constexpr int kXgAccStride = 36;  // words per group accumulator row (R + 1 = 33 columns)
+constexpr int kXsBlocks = 64;      // k_xscan: queue blocks per workgroup (chunk): a lane per block
 // phase 2: the parts (lanes) per 16-byte load column of the digit rows, a power of two
 // with every column's parts in one workgroup; own rows (R / 4 columns) use kBS / (R / 4)
 __host__ __device__ constexpr int xr_parts(int R) {
@@ -326,9 +326,9 @@ struct TickArgs {
     const uint32_t *tbits;  // one GPU, message ticks: touched as a bitmap (L2-resident: 128 KB per 1M slots)
     const PostRec *post;
     const uint8_t *post_rf;
-    int slots_in_apply;
+    int slots_in_apply;  // the slot purge ran in k_ev_apply_ll's launch: k_scan has no W blocks
     int cq_direct;  // idle one-GPU tick on k_emit2: the emit recomputes each position's raw free count
-                    // and heartbeat from the committed per-position arrays; k_scan stores neither  // the slot purge ran in k_ev_apply_ll's launch: k_scan has no W blocks
+                    // and heartbeat from the committed per-position arrays; k_scan stores neither
     int post_lazy;  // 1: the slot purge loads post records only for touched slots (large tables)
     const int32_t *front_list, *back_list;  // slot + 1, 0 = empty
     // intermediates
@@ -359,9 +359,9 @@ struct TickArgs {
     int32_t *wq_buf, *wqf_buf;
     double *wqh_buf;
     int nchB, nchF, nchW;
-    int win_direct;
-    int xself;
-    int wfirst;      // k_scan: log and slot blocks ahead of the queue blocks in the grid (sharded phase 1)       // xplan ticks with <= 64 chunks: k_emit_shard_xp prefixes the chunk totals itself  // k_emit_win: chunk = workgroup index (every chunk resident at once), else a ticket
+    int win_direct;  // k_emit_win: chunk = workgroup index (every chunk resident at once), else a ticket
+    int xself;       // xplan ticks with <= 64 chunks: k_emit_shard_xp prefixes the chunk totals itself
+    int wfirst;      // k_scan: log and slot blocks ahead of the queue blocks in the grid (sharded phase 1)
     unsigned long long *wlb;     // look-back granules: [0, nchB) the back chain, then the front / window chain
     uint32_t *wticket;           // chunk tickets (zeroed by k_ev_link)
     int64_t *cw;                 // commit word {failed, window head, window length} (eager commits)
@@ -374,6 +374,7 @@ struct TickArgs {
     int32_t *tomb;               // per back / front list entry: the committed position of a queued slot
                                  // it moved (-1: none), 2 E entries
     int wseg;                    // k_logscan writes per-tile orphan segments (window ticks)
+    int64_t fault_qlen;          // >= 0: k_emit_win reports this window / queue length (a test's fault)
 
     // the previous tick's commit folded into this k_scan (one-GPU heartbeat contexts, an
     // idle tick after an idle tick): the W role deletes the records that tick evicted
@@ -486,6 +487,8 @@ void launch_emit(const TickArgs &a, Stream st);
 void launch_emit2(const TickArgs &a, Stream st);
 void launch_emit_shard(const TickArgs &a, Stream st);
 void launch_emit_win(const TickArgs &a, int grid, Stream st);
+// k_emit_win workgroups resident per CU at once (the occupancy calculator; 0 on failure)
+int emit_win_resident_per_cu();
 void launch_pos_rebuild(int32_t *pos, const int32_t *queue, const int32_t *qfree, int64_t off, int64_t n, Stream st);
 // evicted slots in ascending order from the per-slot status bytes and per-tile counts (two
 // launches: a one-workgroup scan of the tile counts, then one block per tile)

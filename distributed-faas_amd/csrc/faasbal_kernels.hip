@@ -3482,6 +3482,23 @@ __device__ __forceinline__ void win_fail(const TickArgs &a) {
     a.hout->win_ovf = 1;
     a.cw[0] = a.cw_tag;
 }
+// The window report: the next window [head, head + len) of the queue buffer and the true
+// queue length, into the host results and the commit word.  The device checks them with
+// fb_tick_wait's bounds (check_lengths) before an eager commit can read them: outside, the
+// commit word's failure tag keeps the eager commit from committing, and the host refuses
+// the tick with FB_EHIP -- device and host agree the tick is not committed.  (fault_qlen >=
+// 0: a test overrides both lengths here, fb_set_path("fault_qlen").)
+__device__ __forceinline__ void win_report(const TickArgs &a, int64_t head, int64_t len, int64_t qlen) {
+    if (a.fault_qlen >= 0) len = qlen = a.fault_qlen;
+    a.hout->win_head = head;
+    a.hout->new_qlen = len;
+    a.hout->win_qlen = qlen;
+    a.cw[1] = head;
+    a.cw[2] = len;
+    if (head < a.wq_off || len < 0 || head > a.wq_cap || len > a.wq_cap - head || qlen < 0 || qlen > len ||
+        qlen > a.q_cap)
+        a.cw[0] = a.cw_tag;
+}
 constexpr uint64_t kGrA = (1ull << 22) - 1, kGrM = (1ull << 18) - 1;
 constexpr int kWinStampRow = 8192;  // k_emit_win's diagnostic stamp rows (after k_ev_apply_ll's)
 __device__ __forceinline__ uint64_t gr_pack(uint32_t st, uint32_t lv, uint32_t g1, uint32_t mx) {
@@ -3645,11 +3662,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
                     a.hout->AL = inc + LB;  // at least
                 }
                 if (ci == 0 && N == 0) {
-                    a.hout->win_head = a.wq_off;
-                    a.hout->new_qlen = a.wq_tail + LB - a.wq_off;
-                    a.cw[1] = a.wq_off;
-                    a.cw[2] = a.wq_tail + LB - a.wq_off;
-                    a.hout->win_qlen = nq;
+                    win_report(a, a.wq_off, a.wq_tail + LB - a.wq_off, nq);
                     if (a.wq_tail + LB - a.wq_off > a.q_cap) win_fail(a);
                 }
             }
@@ -3723,11 +3736,7 @@ __global__ __launch_bounds__(kBS) void k_emit_win(TickArgs a) {
         }
         if (k == N - 1) {
             const int64_t head = reg == 2 ? i0 + j * kBS + tid + 1 : a.wq_off;
-            a.hout->win_head = head;
-            a.hout->new_qlen = a.wq_tail + LB + G - head;
-            a.cw[1] = head;
-            a.cw[2] = a.wq_tail + LB + G - head;
-            a.hout->win_qlen = (int64_t)nq - (N - G);
+            win_report(a, head, a.wq_tail + LB + G - head, (int64_t)nq - (N - G));
             // the next window, tombstones included, must fit a general tick's position arrays
             if (a.wq_tail + LB + G - head > a.q_cap) win_fail(a);
         }
@@ -4945,6 +4954,11 @@ __global__ __launch_bounds__(64) void k_gate(uint32_t *flag, uint32_t want, uint
         }
         __builtin_amdgcn_s_sleep(8);
     }
+}
+int emit_win_resident_per_cu() {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_emit_win, kBS, 0) != hipSuccess) return 0;
+    return n;
 }
 void launch_gate(uint32_t *flag, uint32_t want, uint64_t limit, Stream st) {
     hipExtLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st.s, st.e0, st.e1, 0, flag, want, limit);

@@ -24,10 +24,78 @@ _NONE = None
 # fixtures set them (tests/test_gpu_parity.py); production code leaves this empty.
 TEST_PATHS = {}
 # ... or from the environment for same-box A/B runs (tools/ab_stream.sh):
-# FAASBAL_PATHS="spec_purge=0,xplan=1"
-for _kv in filter(None, os.environ.get("FAASBAL_PATHS", "").split(",")):
-    _k, _v = _kv.split("=")
-    TEST_PATHS[_k.strip()] = int(_v)
+# FAASBAL_PATHS="cmix=0,wtiles=2".  Only knobs that leave the sharded exchange layout alone
+# (a per-process value of one that changes it, e.g. xplan, would split a group's ranks);
+# a malformed entry is reported, not fatal to the import.
+_ENV_PATHS_REFUSED = ("xplan",)
+
+
+def _env_paths(spec):
+    out = {}
+    for kv in filter(None, (x.strip() for x in spec.split(","))):
+        k, sep, v = kv.partition("=")
+        k = k.strip()
+        try:
+            val = int(v)
+        except ValueError:
+            val = None
+        if not sep or not k or val is None:
+            import warnings
+            warnings.warn("FAASBAL_PATHS: ignoring %r (expected name=integer)" % kv)
+            continue
+        if k in _ENV_PATHS_REFUSED:
+            import warnings
+            warnings.warn("FAASBAL_PATHS: ignoring %r (it changes the sharded exchange layout; set it with "
+                          "fb_set_path on every rank)" % kv)
+            continue
+        out[k] = val
+    return out
+
+
+TEST_PATHS.update(_env_paths(os.environ.get("FAASBAL_PATHS", "")))
+
+
+def iter_compact(slot, c, n):
+    """The per-task slots of a tick (``assignments()``) from its compact form, one LRU
+    round at a time: round r serves, in LRU order, the positions whose min(c, L + 1) > r
+    (``task_dispatcher.py:393-419`` in closed form), the last round only
+    its first p.  Yields int32 arrays whose concatenation is the first ``n`` tasks' slots;
+    each round filters the one before it, so the whole walk touches every task once."""
+    sl = np.asarray(slot, np.int32)
+    cc = np.asarray(c, np.uint8)
+    r, left = 0, int(n)
+    while left > 0:
+        keep = cc > r
+        sl, cc = sl[keep], cc[keep]
+        if not len(sl):
+            raise ValueError("compact form holds fewer than %d tasks" % n)
+        take = sl[:left]
+        left -= len(take)
+        yield take
+        r += 1
+
+
+class CompactAssignments:
+    """A tick's task -> slot assignments held in compact form (slot and min(c, L + 1) per
+    LRU position, 5 bytes per queued worker instead of 4 per task): iterating yields the
+    slot of task 0, 1, ... expanded round by round as the consumer goes
+    (``GpuPushDispatcher`` sends while it expands); ``array()`` expands it whole."""
+
+    def __init__(self, slot, c, n):
+        self.slot, self.c, self.n = slot, c, int(n)
+
+    def __len__(self):
+        return self.n
+
+    def chunks(self):
+        return iter_compact(self.slot, self.c, self.n)
+
+    def __iter__(self):
+        for ch in self.chunks():
+            yield from ch.tolist()
+
+    def array(self):
+        return np.concatenate(list(self.chunks())) if self.n else np.zeros(0, np.int32)
 
 
 def _p(a):
@@ -395,15 +463,44 @@ class GpuBalancer:
                                zip(old, need, (np.int32, np.int64, np.int32)))
         return self._pout
 
+    def _compact_out(self):
+        """Registered pinned arrays for the compact outputs (set_compact_out), made once:
+        slot / c for the queue plus twice the messages, the orphans for the whole log (up
+        to 1M entries; a tick with a longer log copies into them instead), every worker."""
+        if getattr(self, "_cbufs", None) is None:
+            q = self.max_workers + 2 * self.max_events + 16
+            ocap = min(int(self.max_log), 1 << 20)
+            self._cbufs = (self.pinned(q, np.int32), self.pinned(q, np.uint8), self.pinned(max(ocap, 1), np.int64),
+                           self.pinned(max(self.max_workers, 1), np.int32))
+            self.set_compact(True)
+            self.set_compact_out(*self._cbufs)
+        return self._cbufs
+
     def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0,
-             commit=True, outputs=True, pinned=False):
+             commit=True, outputs=True, pinned=False, compact=False):
         """One full tick.  Returns dict(result, reconnect, assign, orphans, evicted).
-        ``pinned=True`` (the drop-in dispatcher's path): the three lists come back in one
-        readback into reusable pinned arrays -- views valid until the next tick."""
+        ``pinned=True``: the three lists come back in one readback into reusable pinned
+        arrays -- views valid until the next tick.  ``compact=True`` (the drop-in
+        dispatcher's path, heartbeat loop): the tick writes slot + min(c, L + 1) per LRU
+        position into registered pinned arrays and ``assign`` is a ``CompactAssignments``
+        that expands round by round as it is iterated (views valid until the next tick)."""
+        if compact and self.mode == "heartbeat":
+            bufs = self._compact_out()
+        else:
+            compact = False
         self.launch(now, tte, ev_kind, ev_slot, ev_val, ev_ts, ev_seq, n_pending)
         res = self.wait()
         out = dict(result=res)
-        if outputs and pinned:
+        if outputs and compact and res["fill_level"] + 1 > 255:
+            compact, pinned = False, True  # rounds beyond a byte: the per-task readback
+        if outputs and compact:
+            ob = bufs[2]
+            if res["n_orphans_local"] > len(ob):  # more orphans than the registered array holds
+                ob = np.zeros(res["n_orphans_local"], np.int64)
+            sl, cc, o, e = self.outputs_compact(bufs[0], bufs[1], ob, bufs[3])
+            out.update(reconnect=self.event_status(), assign=CompactAssignments(sl, cc, res["n_assigned"]),
+                       orphans=o, evicted=e)
+        elif outputs and pinned:
             a, o, e = self.outputs(*self._pinned_out())
             out.update(reconnect=self.event_status(), assign=a, orphans=o, evicted=e)
         elif outputs:

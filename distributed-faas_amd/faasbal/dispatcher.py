@@ -303,11 +303,13 @@ class GpuPushDispatcher:
                 val[i] = v
             elif k == EV_RESULT:
                 seq[i] = self.task_seq.get(m["data"]["task_id"], -1)
-        # a one-GPU balancer hands the tick's assignments / orphans / evicted slots back in one
-        # readback into pinned arrays, consumed below before the next tick
-        # (exactly a GpuBalancer: a ShardedBalancer subclass has no pinned path; shard groups
-        # are the sharded route)
-        tkw = {"pinned": True} if type(self.balancer) is GpuBalancer else {}
+        # a one-GPU balancer hands the tick's assignments back in compact form -- slot and
+        # min(c, L + 1) per LRU position, written by the tick into registered pinned arrays
+        # (5 B per queued worker instead of 4 B per task) -- expanded round by round while the
+        # task messages go out below; orphans / evicted slots in the same readback, consumed
+        # before the next tick (exactly a GpuBalancer: a ShardedBalancer subclass has no pinned
+        # path; shard groups are the sharded route)
+        tkw = {"compact": True, "pinned": True} if type(self.balancer) is GpuBalancer else {}
         try:
             out = self.balancer.tick(now, float(self.time_to_expire), kind, slot, val, ts, seq,
                                      n_pending=len(self.pending), **tkw)
@@ -381,8 +383,9 @@ class GpuPushDispatcher:
             vals = qpipe.execute()
         wpipe = self._pipe() if n else None
         wdb = wpipe if wpipe is not None else self.redis_client
-        for k, tid in enumerate(tids):
-            s = int(assign[k])
+        # (the per-task slots in LRU rounds: a CompactAssignments expands as it is iterated)
+        for k, (tid, s) in enumerate(zip(tids, assign)):
+            s = int(s)
             if qpipe is None:
                 task_id, fn_payload, param_payload = self.query_redis({"data": tid.encode("utf-8")})
             else:

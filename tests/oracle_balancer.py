@@ -26,8 +26,9 @@ class OracleBalancer:
     def read_state(self, with_log=True):
         return self.o.export()
 
-    def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0, pinned=False):
-        # (pinned: GpuBalancer's single pinned readback -- the oracle's outputs are host arrays)
+    def tick(self, now, tte, ev_kind=(), ev_slot=(), ev_val=(), ev_ts=(), ev_seq=None, n_pending=0, pinned=False,
+             compact=False):
+        # (pinned / compact: GpuBalancer's readback forms -- the oracle's outputs are host arrays)
         if ev_seq is None:
             ev_seq = np.full(len(ev_kind), -1, np.int64)
         # the HIP tick fails with FB_ENOSPC and commits nothing when its dispatches do not

@@ -53,3 +53,38 @@ def _lib_load_fresh(path):
         return _lib.load(path)
     finally:
         _lib._LIB = saved
+
+
+def test_env_paths_parse_defensively():
+    """FAASBAL_PATHS (same-box A/B runs): malformed entries and layout-changing knobs are
+    ignored with a warning, never fatal to the import."""
+    import warnings
+    from faasbal.balancer import _env_paths
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        got = _env_paths("cmix=0, wtiles=2,bogus,xplan=0,n=abc,=3")
+    assert got == {"cmix": 0, "wtiles": 2}
+    assert len(w) == 4
+
+
+def test_iter_compact_matches_round_expansion():
+    """CompactAssignments / iter_compact (the dispatcher's lazy expansion) against a plain
+    round-by-round expansion of the closed form: round r serves, in LRU
+    order, the positions with min(c, L + 1) > r; the last round only its first p."""
+    import numpy as np
+    from faasbal.balancer import CompactAssignments, iter_compact
+    rng = np.random.default_rng(0)
+    for trial in range(50):
+        Q = int(rng.integers(0, 400))
+        L = int(rng.integers(0, 20))
+        slot = rng.integers(-1, 10_000, Q).astype(np.int32)
+        c = rng.integers(0, L + 2, Q).astype(np.uint8)
+        ref = []
+        for r in range(L + 1):
+            ref.extend(int(s) for s, x in zip(slot, c) if x > r)
+        total = len(ref)
+        n = int(rng.integers(0, total + 1))
+        got = np.concatenate(list(iter_compact(slot, c, n))) if n else np.zeros(0, np.int32)
+        assert got.tolist() == ref[:n]
+        ca = CompactAssignments(slot, c, n)
+        assert list(ca) == ref[:n] and len(ca) == n and ca.array().tolist() == ref[:n]

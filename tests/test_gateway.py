@@ -220,3 +220,52 @@ def test_service_end_to_end(dispatcher_cls):
         assert s["status"] == ("FAILED" if v is None else "COMPLETED"), s
         assert codec.deserialize(s["result"]) == v
     assert not d.pending
+
+
+def immediate_function(number):
+    """client_performance.py:19-20, the no-op task of BASELINE configs[0]."""
+    return number
+
+
+@pytest.mark.parametrize("loop", ["heartbeat", "deque"])
+def test_configs0_client_performance_shape(dispatcher_cls, loop):
+    """BASELINE configs[0] as client_performance.py states it (:157-164, :218, :225-226):
+    4 push workers of 4 processes each (``-w 4``, ``-np 4``), ``n_tasks`` 10 per worker ->
+    a problem size of 40 ``immediate_function`` tasks with params ((1,), {})
+    (``params_immediate_function``, :22-24); ``measure_service`` (:98-143) registers the
+    function and the tasks over REST and polls every result until COMPLETED.  Both
+    dispatcher loops: ``--hb`` (start_heartbeat) and the default ``start()``; every result
+    is read back and checked."""
+    r = MemoryRedis()
+    router = _Router()
+    clock = [100.0]
+    d = dispatcher_cls("127.0.0.1", 0, 10, max_workers=64, max_inflight=4096, max_events=512,
+                       redis_client=r, socket=router, poller=router, clock=lambda: clock[0])
+    if loop == "deque":
+        d.use_loop("deque")
+    c = TestClient(create_app(r))
+    number_workers, number_processes, n_tasks = 4, 4, 10
+    workers = [_PushWorker(b"push%d" % i, number_processes, router) for i in range(number_workers)]
+    for w in workers:
+        w.register()
+    fid = c.post("/register_function", json={"name": immediate_function.__name__,
+                                              "payload": codec.serialize(immediate_function)}).json()["function_id"]
+    problem_size = n_tasks * number_workers
+    fn_params = [((1,), {}) for _ in range(problem_size)]
+    tasks = [c.post("/execute_function", json={"function_id": fid, "payload": codec.serialize(p)}).json()["task_id"]
+             for p in fn_params]
+    assert len(set(tasks)) == problem_size
+    for _ in range(200):
+        clock[0] += 0.01
+        d.tick()
+        for w in workers:
+            w.step()
+        if all(c.get("/status/%s" % t).json()["status"] == "COMPLETED" for t in tasks):
+            break
+    for t, p in zip(tasks, fn_params):
+        s = c.get("/result/%s" % t).json()
+        assert s["status"] == "COMPLETED", s
+        assert codec.deserialize(s["result"]) == immediate_function(*p[0], **p[1])
+    assert not d.pending
+    # every worker served: 40 tasks over 4 workers of 4 processes
+    assert d.ticks > 1

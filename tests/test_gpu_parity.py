@@ -188,6 +188,8 @@ def test_compact_outputs_written_during_the_tick(shape):
     W = len(st["reg"])
     g = GpuBalancer(W, 3 * len(st["log"]) + 4 * T + 16, max_events=max(E, 256))
     g.load(st)
+    o = Oracle(W, 3 * len(st["log"]) + 4 * T + 16)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
     cap = W + 2 * g.max_events + 16
     bufs = (g.pinned(cap, np.int32), g.pinned(cap, np.uint8), g.pinned(3 * len(st["log"]) + 4 * T + 16, np.int64),
             g.pinned(W, np.int32))
@@ -196,6 +198,12 @@ def test_compact_outputs_written_during_the_tick(shape):
         g.launch(tk["now"], 10.0, *tk["ev"], tk["n"])
         r = g.wait()
         slot, c, orph, ev = g.outputs_compact(*bufs)
+        # against the oracle (g.orphans() / g.evicted() copy these same registered arrays)
+        b = o.tick(tk["now"], 10.0, *[x if x is not None else [] for x in tk["ev"][:4]],
+                   tk["ev"][4] if tk["ev"][4] is not None else np.full(len(tk["ev"][0]), -1, np.int64), tk["n"])
+        np.testing.assert_array_equal(g.expand(slot, c), b["assign"], err_msg="tick %d assign (oracle)" % t)
+        np.testing.assert_array_equal(orph, b["orphans"], err_msg="tick %d orphans (oracle)" % t)
+        np.testing.assert_array_equal(ev, b["evicted"], err_msg="tick %d evicted (oracle)" % t)
         np.testing.assert_array_equal(g.expand(slot, c), g.assignments(), err_msg="tick %d assign" % t)
         np.testing.assert_array_equal(orph, g.orphans(), err_msg="tick %d orphans" % t)
         np.testing.assert_array_equal(ev, g.evicted(), err_msg="tick %d evicted" % t)
@@ -386,18 +394,21 @@ def test_log_full_is_an_error():
         g.tick(1000.0, 10.0, n_pending=5000)
 
 
-@pytest.mark.parametrize("window", [0, 1])
-def test_device_reported_lengths_are_validated(window):
+@pytest.mark.parametrize("window,eager", [(0, 0), (1, 0), (1, 1)])
+def test_device_reported_lengths_are_validated(window, eager):
     """fb_tick_wait checks every device-reported length against its buffer before any
     copy uses it: a queue length past the buffer (injected into the results) fails the
     tick with FB_EHIP naming the number; the tick is not committed and the next one runs
-    against the oracle as if it never happened."""
+    against the oracle as if it never happened.  Eager window commits (enqueued behind the
+    tick at launch): the device checks the window it reports with the same bounds, so the
+    commit kernel commits nothing either."""
     # nobody dead and a frozen clock: both ticks stay at fill level 0, so with window ticks
     # on the second one is a window tick (a death's orphans would lift it to level 1: a
     # general tick after the window attempt)
     st = synth.zipf_state(W=2048, seed=3, dead_frac=0.0)
     g, o = _pair(st, len(st["log"]) * 2 + 100_000)
     g.set_window(window)
+    g.set_eager_commit(bool(eager))
     args = (1000.0, 10.0, [], [], [], [], [], 500)
     a, b = g.tick(*args), o.tick(*args)
     _cmp_out(a, b, 0)

@@ -327,3 +327,31 @@ def test_sharded_exchanged_rows_shapes(world, nbq, cap):
         b = o.tick(*args)
         _cmp(bals, o, a, b, t)
         carried = carried + n_new + len(b["orphans"]) - len(b["assign"])
+
+
+def test_sharded_length_check_failure_aborts_the_group():
+    """A device-reported length that fails fb_tick_wait's check on ONE rank (injected
+    there) fails the group's tick: LocalShardGroup commits no rank, so the shards stay in
+    step and the same tick then runs against the oracle as if the failure never happened
+    (DistShardGroup settles the same way: commit only when every rank succeeded)."""
+    import torch  # noqa: F401
+    from faasbal import FaasbalError
+    from faasbal.sharded import LocalShardGroup
+
+    st = synth.zipf_state(W=4096, seed=4)
+    T = 30_000
+    grp = LocalShardGroup(3, 4096, len(st["log"]) + 4 * T + 16, max_events=64)
+    grp.load(st)
+    o = Oracle(4096, len(st["log"]) + 4 * T + 16)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    grp.bals[1].set_path("fault_qlen", 1 << 30)
+    args = (1000.0, 10.0, [synth.EV_HEARTBEAT], [7], [0], [999.0], [-1], T)
+    with pytest.raises(FaasbalError, match="queue length"):
+        grp.tick(*args)
+    for t in range(2):
+        a = grp.tick(*args)
+        b = o.tick(*args)
+        for k in ("reconnect", "assign", "orphans", "evicted"):
+            np.testing.assert_array_equal(a[k], b[k], err_msg="tick %d: %s" % (t, k))
+        args = (1001.0, 10.0, [], [], [], [], [], T // 3)
+    np.testing.assert_array_equal(grp.read_state()["queue"], o.export()["queue"])
