@@ -5046,7 +5046,7 @@ void launch_emit_shard(const TickArgs &a, Stream st) {
     }
     const dim3 g(a.nbq + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
     if (a.xplan) {
-        // two queue blocks per workgroup (k_emit_shard_xp)
+        // two queue blocks per workgroup (k_emit_shard_xp; four measured no faster, r06f_probe_*)
         const dim3 g2((a.nbq + 1) / 2 + (a.nbf + 3) / 4 + (a.nbw + 3) / 4);
         hipExtLaunchKernelGGL(k_emit_shard_xp<2>, g2, dim3(kBS), 0, st.s, st.e0, st.e1, 0, a);
         return;

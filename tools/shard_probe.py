@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--scaling", default="strong", choices=("strong", "weak"))
     ap.add_argument("--workload", default="tick", choices=("tick", "cfg3"),
                     help="tick: configs[2] (64K workers, 1M tasks); cfg3: configs[3] (1M workers, 16M tasks)")
+    ap.add_argument("--gated", action="store_true",
+                    help="per rank: phase 1, exchange copy and phase 2 back to back behind the timing gate")
     args = ap.parse_args()
     for world in args.world:
         k = world if args.scaling == "weak" else 1
@@ -52,22 +54,43 @@ def main():
             for b in bals:
                 b.cont()
                 b.wait()
+            return tot
 
         for _ in range(5):
             tick()
+        # the summed exchange of two consecutive ticks: the records alternate between two
+        # copies by exchange parity, so the contents repeat with period 2
+        tots = [tick(), tick()]  # phase 2's input (the summed exchange) of two consecutive ticks
+        rep = [0]
+
+        def tick_gated():
+            # each rank alone, its phases back to back on the device behind the timing gate:
+            # phase 1, the exchange's summed contents (this idle tick's, identical every other
+            # repetition) copied in on the rank's stream, phase 2 -- no host pacing between
+            tot = tots[rep[0] % 2]
+            rep[0] += 1
+            for b in bals:
+                b.timing_gate(True)
+                b.launch(1000.0, 10.0, n_pending=T)
+                with torch.cuda.stream(b.stream):
+                    b.exchange().copy_(tot)
+                b.cont()
+                b.timing_gate(False)
+                b.wait()
+
         for b in bals:
             b.timing_enable(True)
         t0 = time.perf_counter()
         for _ in range(args.reps):
-            tick()
+            (tick_gated if args.gated else tick)()
         dt = (time.perf_counter() - t0) / args.reps
         pers = []
         for b in bals:
             kt = b.timing_read()
             pers.append({k: round(ms / args.reps * 1e3, 2) for k, (ms, n) in kt.items()})
         slow = max(range(world), key=lambda r: sum(pers[r].values()))
-        print("%s %s world %d: rank-0 device us per tick %s (sum %.1f); slowest rank %d: sum %.1f; exchange %d B, "
-              "serial wall %.0f us" % (args.workload, args.scaling, world, pers[0], sum(pers[0].values()), slow,
+        print("%s%s %s world %d: rank-0 device us per tick %s (sum %.1f); slowest rank %d: sum %.1f; exchange %d B, "
+              "serial wall %.0f us" % (args.workload, " gated" if args.gated else "", args.scaling, world, pers[0], sum(pers[0].values()), slow,
                                        sum(pers[slow].values()), bals[0].exchange().numel(), dt * 1e6), flush=True)
         for b in bals:
             b.timing_enable(False)
