@@ -302,6 +302,7 @@ struct fb_ctx {
     int gpcheck = 0;                                  // fb_set_path("gpcheck", 1): diagnostic (stamps builds)
     int cmix_on = 1;                                  // fb_set_path("cmix"): k_emit2 role interleave
     int wtiles = 0;                                   // fb_set_path("wtiles"): slot tiles per k_scan W workgroup (0 auto)
+    int qtiles = 0;                                   // fb_set_path("qtiles"): 1 = one queue block per k_scan Q workgroup (0 auto: 4)
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
     bool l_full = false;                              // ... and the last launch did
@@ -1274,6 +1275,11 @@ int enqueue_tick(fb_ctx *c) {
     // slot tiles per k_scan W-role workgroup: unfused (large) tables 4 -- fewer, longer
     // workgroups (configs[3]: scan 16.3 -> 14.8 us with 2, tick 55.4 -> 53.4 us with 4)
     a.wtiles = c->wtiles ? c->wtiles : (a.fused ? 1 : 4);
+    // queue blocks per k_scan Q-role workgroup in the same (4-tile) instance: one-GPU unfused
+    // tables with ride-along queue records
+    a.qtiles = (c->qtiles != 1 && a.wtiles == 4 && !a.fused && !c->shard && !c->deque && a.qaos && a.R <= kRFused)
+                   ? 4
+                   : 1;
     if (!a.slots_in_scan && !a.slots_in_apply) {
         Timer t(c, "slots");
         launch_slots(a, t.st());
@@ -2912,6 +2918,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "gpcheck" && (value == 0 || value == 1)) c->gpcheck = value;
     else if (n == "cmix" && (value == 0 || value == 1)) c->cmix_on = value;
     else if (n == "wtiles" && (value == 0 || value == 1 || value == 2 || value == 4)) c->wtiles = value;
+    else if (n == "qtiles" && (value == 0 || value == 1 || value == 4)) c->qtiles = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }

@@ -1518,6 +1518,131 @@ __device__ __forceinline__ bool died_touched(const TickArgs &a, int s) {
     return (rf & 1) && ((a.now - a.post[s].hb) > a.tte);
 }
 
+// k_scan's Q role for a position that is not a committed entry with ride-along records (a
+// front / back insertion, or no qaos): its slot from the lists, the free count and heartbeat
+// from the slot's record.  raw stays INT32_MIN without a live record (or not mine).
+__device__ __forceinline__ void q_raw_slow(const TickArgs &a, int64_t pos, bool inq, int32_t &raw, double &hbq) {
+    const int s = lq_slot(a, pos);
+    const int ls = s >= 0 ? own_slot(a, s) : -1;
+    if (ls >= 0) {
+        if (a.slots_in_scan) {
+            const Cur cu = cur_slot(a, ls);
+            raw = (cu.reg && !is_dead(a, cu)) ? cu.fr : INT32_MIN;
+            hbq = cu.hb;
+        } else {
+            raw = a.free_out[ls].x;
+            // the heartbeat after this tick's messages rides along into the next queue
+            const double h0 = a.hb[ls], h1 = a.post[ls].hb;
+            hbq = (a.E > 0 && got_msg(a, ls)) ? h1 : h0;
+        }
+    }
+    // an old queue entry moved to the front, re-appended or removed by this tick's messages
+    if (raw != INT32_MIN && a.E > 0 && inq && got_msg(a, ls) && ((a.post_rf[ls] >> 2) & 3) != kQsKeep)
+        raw = INT32_MIN;
+}
+
+// k_scan's Q role, QT queue blocks per workgroup (one GPU, unfused tables with ride-along
+// queue records, R <= kRFused): every block's position loads in one round, the touched
+// tests in a second, then per block the wave histograms of min(c, R), one barrier for all
+// blocks, and the blocks' round counts, capacity and max c -- the values the one-block form
+// writes (configs[3]: 3 547 one-block workgroups of ~2 us of dependent phases each).
+template <int QT>
+__device__ __forceinline__ void queue_tiles(const TickArgs &a, int b0) {
+    __shared__ uint32_t qh[kWaves][kRFused + 1];
+    __shared__ uint32_t qwc[QT][kWaves][kRFused];
+    __shared__ uint32_t qm[QT][kWaves], qsum[QT][kWaves];
+    const int t = threadIdx.x, lane = lane_id(), w = wave_id(), R = a.R;
+    int sqv[QT];
+    double hqv[QT];
+    int32_t fqv[QT];
+    bool tqv[QT];
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+        const int64_t q = (int64_t)(b0 + j) * kBS + t - a.E;
+        const int64_t qc = q < 0 ? 0 : (q < a.Qn ? q : (a.Qn > 0 ? a.Qn - 1 : 0));
+        sqv[j] = a.queue_in[qc];
+        hqv[j] = a.qhb_in[qc];
+        fqv[j] = a.qfree_in[qc];
+    }
+#pragma unroll
+    for (int j = 0; j < QT; ++j) tqv[j] = a.E > 0 && got_msg(a, sqv[j]);
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+        const int64_t pos = (int64_t)(b0 + j) * kBS + t;
+        int c = 0;
+        if (pos < a.Qlog) {
+            int32_t raw = INT32_MIN;
+            double hbq = 0.0;
+            const int64_t q = pos - a.E;
+            if (q >= 0 && q < a.Qn) {
+                // a committed entry (as the one-block form)
+                const int sq = sqv[j];
+                if (!tqv[j]) {
+                    hbq = hqv[j];
+                    raw = ((a.now - hqv[j]) > a.tte) ? INT32_MIN : fqv[j];
+                } else {
+                    const uint8_t rf = a.post_rf[sq];
+                    const PostRec pr = a.post[sq];
+                    hbq = pr.hb;
+                    raw = ((rf & 1) && !((a.now - pr.hb) > a.tte)) ? pr.free : INT32_MIN;
+                    if (((rf >> 2) & 3) != kQsKeep || fqv[j] == kTomb) raw = INT32_MIN;
+                }
+            } else {
+                q_raw_slow(a, pos, false, raw, hbq);
+            }
+            if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
+            if (!a.cq_direct) {
+                a.c_arr[pos] = raw;
+                a.c_hb[pos] = hbq;
+            }
+        }
+        // the wave's counts of c > r for every round r < R from a histogram of min(c, R)
+        uint32_t *h = qh[w];
+        for (int i = lane; i <= R; i += 64) h[i] = 0;
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        atomicAdd(&h[c < R ? c : R], 1u);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t carry = 0;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const int r = 64 * k + lane;
+            const uint32_t hv = h[r < R ? r : R];
+            const uint32_t P = carry + wave_incl_scan_u32(r < R ? hv : 0u);
+            if (r < R) qwc[j][w][r] = 64u - P;
+            carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
+        }
+        // capacity sum_r count(c > r) over r < R = sum of min(c, R); max c
+        const uint32_t ws = wave_sum_u32((uint32_t)(c < R ? c : R)), wm = wave_max_u32((uint32_t)c);
+        if (lane == 0) {
+            qsum[j][w] = ws;
+            qm[j][w] = wm;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+    }
+    lds_barrier();
+#pragma unroll
+    for (int j = 0; j < QT; ++j) {
+        const int b = b0 + j;
+        if (b >= a.nbq) break;  // (uniform)
+        if (t < R) {
+            const uint32_t n = qwc[j][0][t] + qwc[j][1][t] + qwc[j][2][t] + qwc[j][3][t];
+            a.qcnt[(size_t)b * R + t] = n;
+            // the group's row of round totals (memory-side atomics, no return)
+            if (a.grp_on && n) atomicAdd(&a.grp[(b >> a.gshift) * a.gstride + t], n);
+        }
+    }
+    if (t < QT && b0 + t < a.nbq) {
+        const int b = b0 + t;
+        const uint32_t bm = max(max(qm[t][0], qm[t][1]), max(qm[t][2], qm[t][3]));
+        a.qbm_raw[b] = (int32_t)bm;
+        a.csum[b] = (unsigned long long)qsum[t][0] + qsum[t][1] + qsum[t][2] + qsum[t][3];
+        if (a.grp_on && bm > 0) atomicMax(&a.grp[(b >> a.gshift) * a.gstride + R], bm);
+    }
+}
+
 // ------------------------------------------------------------ k_scan
 // F-blocks flag orphaned log entries (died bitmap in LDS); Q-blocks compute the
 // effective free count c of every LRU position and the block's count of c > r
@@ -1533,21 +1658,23 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     __shared__ unsigned long long s4[kWaves];
     __shared__ uint32_t wc[kWaves][kBS];
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;  // phase 2 re-derives only the queue counts
+    // Q-role workgroups (a.qtiles queue blocks each in the 4-tile instance)
+    const int nqb = (WT == 4 && a.qtiles == 4) ? (a.nbq + 3) >> 2 : a.nbq;
     // grid: queue blocks first (the critical path: their loads go out before the log
     // role's gathers fill the memory queues), then log blocks, then slot blocks.  Sharded
     // phase 1 (a.wfirst): the log and slot blocks first -- there they are the longer ones
     // (4-5 us against the queue blocks' 3 at configs[3], N = 8) and nothing waits on the
     // queue role before the exchange
-    const int nfw = (int)gridDim.x - a.nbq - (a.cm_fold ? a.cm_blocks : 0);
+    const int nfw = (int)gridDim.x - nqb - (a.cm_fold ? a.cm_blocks : 0);
     const int bid = !a.wfirst ? (int)blockIdx.x
-                              : ((int)blockIdx.x < nfw ? a.nbq + (int)blockIdx.x
-                                                       : ((int)blockIdx.x < nfw + a.nbq ? (int)blockIdx.x - nfw
-                                                                                         : (int)blockIdx.x));
+                              : ((int)blockIdx.x < nfw ? nqb + (int)blockIdx.x
+                                                       : ((int)blockIdx.x < nfw + nqb ? (int)blockIdx.x - nfw
+                                                                                       : (int)blockIdx.x));
     const int SO = a.nbw;
     STAMP(a, SO, 0);
-    if (bid >= a.nbq && bid - a.nbq < nbf) {
+    if (bid >= nqb && bid - nqb < nbf) {
         // ---- F-role: orphan flags of log entries [b*2048 + t*8, +8)
-        const int b = bid - a.nbq;
+        const int b = bid - nqb;
         const int64_t nlog = a.shard ? a.head_local : a.head_in;
         const int64_t base = (int64_t)b * kFTile + (int64_t)threadIdx.x * kFItems;
         int32_t v[kFItems];
@@ -1635,12 +1762,12 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         if (i < a.cm_n_orph) a.log_slot[a.orphans[i]] = -1;
         return;
     }
-    if (bid >= a.nbq) {
+    if (bid >= nqb) {
         // ---- W-role: heartbeat purge of slots [b*256, +256)
         // WT tiles per workgroup (a.wtiles; its own instance, so the one-tile form -- fused
         // ticks -- keeps its registers and occupancy)
         __shared__ uint32_t l4w[WT][kWaves];
-        slots_body<WT>(a, WT * (bid - a.nbq - nbf), l4w);
+        slots_body<WT>(a, WT * (bid - nqb - nbf), l4w);
         STAMP(a, SO, 15);
         return;
     }
@@ -1648,6 +1775,11 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
     const int b = bid;
     const int64_t pos = (int64_t)b * kBS + threadIdx.x;
     int c = 0, oc = 0;
+    if (a.qtiles == 4 && WT == 4) {
+        queue_tiles<4>(a, 4 * b);
+        STAMP(a, SO, 15);
+        return;
+    }
     if (a.shard == 2) {
         // phase 2 of a sharded tick: every rank's effective free counts arrived in the exchange
         // both loads issued together (a guarded slot load would wait for the c byte first)
@@ -1696,7 +1828,6 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
         }
         c = cc != INT32_MIN ? cc : 0;
     } else if (pos < a.Qlog) {
-        int s = -1, ls = -1;
         int32_t raw = INT32_MIN;  // INT32_MIN: no live record (or not mine)
         double hbq = 0.0;
         const int64_t q = pos - a.E;  // committed queue position (fronts come first)
@@ -1726,24 +1857,7 @@ __global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
                 if (((rf >> 2) & 3) != kQsKeep || fq == kTomb) raw = INT32_MIN;
             }
         } else {
-            s = lq_slot(a, pos);
-            ls = s >= 0 ? own_slot(a, s) : -1;
-            if (ls >= 0) {
-                if (a.slots_in_scan) {
-                    const Cur cu = cur_slot(a, ls);
-                    raw = (cu.reg && !is_dead(a, cu)) ? cu.fr : INT32_MIN;
-                    hbq = cu.hb;
-                } else {
-                    raw = a.free_out[ls].x;
-                    // the heartbeat after this tick's messages rides along into the next queue
-                    const double h0 = a.hb[ls], h1 = a.post[ls].hb;
-                    hbq = (a.E > 0 && got_msg(a, ls)) ? h1 : h0;
-                }
-            }
-            // an old queue entry moved to the front, re-appended or removed by this tick's messages
-            if (raw != INT32_MIN && a.E > 0 && inq && got_msg(a, ls) &&
-                ((a.post_rf[ls] >> 2) & 3) != kQsKeep)
-                raw = INT32_MIN;
+            q_raw_slow(a, pos, inq, raw, hbq);
         }
         if (raw != INT32_MIN) c = raw > 1 ? raw : 1;  // free <= 0 still takes one task (:409-419)
         if (!a.cq_direct) {
@@ -4990,8 +5104,9 @@ void launch_scan(const TickArgs &a, Stream st) {
     const size_t lds = (a.lds_bitmap && !a.slots_in_scan) ? (size_t)((a.W + 63) / 64) * 8 : 0;
     const int nbw = (a.shard == 2 || !a.slots_in_scan || a.slots_in_apply) ? 0 : (a.wtiles > 1 ? (a.nbw + a.wtiles - 1) / a.wtiles : a.nbw);
     const int nbf = (a.shard == 2 || a.f_sep || a.f_emit) ? 0 : a.nbf;
-    const dim3 g(nbf + nbw + a.nbq + (a.cm_fold ? a.cm_blocks : 0));
     const int wt = nbw ? a.wtiles : 1;
+    const int nqb = (wt == 4 && a.qtiles == 4) ? (a.nbq + 3) / 4 : a.nbq;  // (k_scan's own count)
+    const dim3 g(nbf + nbw + nqb + (a.cm_fold ? a.cm_blocks : 0));
     if (wt == 4) launch_scan_t<4>(a, g, nbf ? lds : 0, st);
     else if (wt == 2) launch_scan_t<2>(a, g, nbf ? lds : 0, st);
     else launch_scan_t<1>(a, g, nbf ? lds : 0, st);

@@ -550,6 +550,14 @@ def test_random_multitick_logscan_plan_wtiles(logscan, force_plan, monkeypatch, 
 
 
 @pytest.mark.parametrize("seed", range(3))
+def test_random_multitick_logscan_plan_qtiles1(logscan, force_plan, monkeypatch, seed):
+    """k_scan's queue role with one queue block per workgroup (fb_set_path("qtiles", 1));
+    unfused one-GPU tables default to four per workgroup."""
+    monkeypatch.setitem(TEST_PATHS, "qtiles", 1)
+    test_random_multitick_vs_oracle(seed + 20)
+
+
+@pytest.mark.parametrize("seed", range(3))
 def test_random_multitick_logscan_plan_no_cmix(logscan, force_plan, monkeypatch, seed):
     """k_emit2's grid in role order (fb_set_path("cmix", 0)): queue blocks, then the
     compaction workgroups -- the default interleaves their rows."""
