@@ -4687,19 +4687,32 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_xp(TickArgs a) {
 // ---- compaction roles of k_emit_shard*, as in k_emit2: one wave per tile (a phase-1
 // k_scan block's 2048 log entries or 256 slots), four tiles per workgroup
 __device__ __forceinline__ void shard_compact(const TickArgs &a, int bid) {
+    __shared__ uint32_t cred[kWaves];
     const int lane = lane_id(), w = wave_id();
     const int nbf4 = (a.nbf + 3) >> 2;
     const bool frole = bid < a.nbq + nbf4;
-    const int t = 4 * (frole ? bid - a.nbq : bid - a.nbq - nbf4) + w;
-    if (t >= (frole ? a.nbf : a.nbw)) return;
+    const int t0 = 4 * (frole ? bid - a.nbq : bid - a.nbq - nbf4);
+    const int t = t0 + w;
+    const int ntile = frole ? a.nbf : a.nbw;
     // the tile's offset: k_plan's scan of the tile counts, or (no k_plan: group rows) the
-    // wave's own sum of the earlier tiles' counts
-    auto tile_pre = [&](const uint32_t *cnt, const int64_t *pre) -> int64_t {
-        if (!a.grp_on && !a.xrows && !a.xplan) return pre[t];
-        uint32_t v = 0;
-        for (int i = lane; i < t; i += 64) v += cnt[i];
-        return (int64_t)wave_sum_u32(v);
-    };
+    // workgroup's sum of the counts before its first tile -- every load in flight at once
+    // (16 per thread up to 4 096 tiles; a wave-serial loop over them put ~t/128 dependent
+    // load rounds on the kernel's last workgroups) -- plus its earlier waves' tiles
+    int64_t toff = 0;
+    if (!a.grp_on && !a.xrows && !a.xplan) {
+        if (t < ntile) toff = (frole ? a.fpre : a.wpre)[t];
+    } else {
+        const uint32_t *cnt = frole ? a.fcnt : a.wcnt;
+        unsigned long long tot, pre;
+        peeled_sum<16>(cnt, t0 < ntile ? t0 : ntile, t0, tot, pre);
+        const uint32_t ws = wave_sum_u32((uint32_t)pre);
+        if (lane == 0) cred[w] = ws;
+        __syncthreads();
+        toff = (int64_t)cred[0] + cred[1] + cred[2] + cred[3];
+        for (int q = 0; q < w; ++q) toff += t0 + q < ntile ? cnt[t0 + q] : 0u;
+    }
+    if (t >= ntile) return;
+    auto tile_pre = [&](const uint32_t *, const int64_t *) -> int64_t { return toff; };
     if (frole) {
         // own orphans (global sequence numbers, ascending): lane l holds flag bytes
         // 4l .. 4l+3 of tile t, i.e. local entries t*2048 + 32l .. +32
