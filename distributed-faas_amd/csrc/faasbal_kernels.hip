@@ -2235,7 +2235,9 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
                 int sj = v[k][j];
                 if (a.shard && sj >= 0) sj -= a.slot_base;  // log slots are global ids
                 const int sc = sj < 0 ? 0 : sj;
-                flags |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << j) : 0u;
+                // (32-bit LDS reads: one bank per lane instead of two)
+                const uint32_t *bm32 = reinterpret_cast<const uint32_t *>(bm);
+                flags |= (sj >= 0 && ((bm32[sc >> 5] >> (sc & 31)) & 1u)) ? (1u << j) : 0u;
             }
             flags = drop_completed(a, flags, v[k], (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems);
             if (a.wseg) {
