@@ -303,6 +303,7 @@ struct fb_ctx {
     int cmix_on = 1;                                  // fb_set_path("cmix"): k_emit2 role interleave
     int wtiles = 0;                                   // fb_set_path("wtiles"): slot tiles per k_scan W workgroup (0 auto)
     int qtiles = 0;                                   // fb_set_path("qtiles"): 1 = one queue block per k_scan Q workgroup (0 auto: 4)
+    int xcfirst_on = 1;                               // fb_set_path("xcfirst", 0): k_emit_shard_xp's compaction workgroups last
     int xplan_on = 1;                                 // fb_set_path("xplan", 0): large queues take the phase-2 k_scan path
     int full_assign = 0;                              // fb_set_full_assign: phase 2 writes the whole task -> slot array
     bool l_full = false;                              // ... and the last launch did
@@ -1095,6 +1096,10 @@ int enqueue_tick(fb_ctx *c) {
         a.xplan = (c->xplan_on && xrows_mode(c->world, R, Qlog) == 2) ? 1 : 0;
         // (<= 64 chunks of kXsBlocks queue blocks: 16 loads per k_emit_shard_xp thread)
         a.xself = (a.xplan && c->xself_on && cdiv(Qlog, kBS) <= 64 * kXsBlocks) ? 1 : 0;
+        // k_emit_shard_xp's compaction workgroups first when they are many (configs[3], N = 2:
+        // 975 beside 1 774 queue workgroups, emit 30.3 -> 26.9 us; N = 8: 244, no gain)
+        a.xcfirst = (a.xplan && c->xcfirst_on &&
+                     4 * ((a.nbf + 3) / 4 + (a.nbw + 3) / 4) > (nbq + 1) / 2) ? 1 : 0;
         c->l_full = c->full_assign != 0;
         if (c->l_full && c->phase == 2) {
             // the whole tick's assignments: at most its pending tasks plus every in-flight entry
@@ -2919,6 +2924,7 @@ int fb_set_path(fb_ctx *c, const char *name, int value) {
     else if (n == "cmix" && (value == 0 || value == 1)) c->cmix_on = value;
     else if (n == "wtiles" && (value == 0 || value == 1 || value == 2 || value == 4)) c->wtiles = value;
     else if (n == "qtiles" && (value == 0 || value == 1 || value == 4)) c->qtiles = value;
+    else if (n == "xcfirst" && (value == 0 || value == 1)) c->xcfirst_on = value;
     else return fail(c, FB_EINVAL, "fb_set_path(\"%s\", %d): unknown path or value", name, value);
     return FB_OK;
 }

@@ -426,6 +426,7 @@ struct TickArgs {
     int cmix;     // k_emit2: compaction workgroups interleaved with the queue blocks
     int wtiles;   // k_scan: slot tiles per W-role workgroup (1, 2 or 4)
     int qtiles;   // k_scan (one GPU, unfused, 4-tile instance): queue blocks per Q-role workgroup (1 or 4)
+    int xcfirst;  // k_emit_shard_xp: the compaction workgroups first in the grid
     // sharded phase 2 (fb_set_full_assign): this rank also writes the whole tick's task -> slot
     // array (every rank computes the global water-filling; one rank's copy serves the host)
     int32_t *assign_all;

@@ -4431,12 +4431,18 @@ __global__ __launch_bounds__(kBS) void k_emit_shard_xp(TickArgs a) {
     prefetch_args(a);
     constexpr int R = kXGroupR;
     static_assert(R < 64, "one 64-round chunk");
-    const int bid = blockIdx.x, t = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int t = threadIdx.x, lane = lane_id(), w = wave_id();
+    const int nqw = (a.nbq + NSB - 1) / NSB;
+    // the compaction workgroups first in the grid (a.xcfirst): they are short, and behind the
+    // queue workgroups -- more than fit on the device at once -- they started only as the first
+    // queue workgroups left, ~10 us in, and ended the kernel (profiles/r06bb_stamps_shard_*)
+    const int ncw = (int)gridDim.x - nqw;
+    const int bid = !a.xcfirst ? (int)blockIdx.x
+                               : ((int)blockIdx.x < ncw ? nqw + (int)blockIdx.x : (int)blockIdx.x - ncw);
     const int SO = 3 * (a.nbw + a.nbf + a.nbq);  // diagnostic stamp rows (stamps builds)
     STAMP(a, SO, 0);
     // the other parity's exchange records, for the next tick's phase 1
     for (int i = bid * kBS + t; i < a.xz_words; i += (int)gridDim.x * kBS) a.xz[i] = 0ull;
-    const int nqw = (a.nbq + NSB - 1) / NSB;
     if (bid >= nqw) {
         shard_compact(a, a.nbq + (bid - nqw));
         return;

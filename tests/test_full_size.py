@@ -128,15 +128,17 @@ def test_gpu_stream_1m_workers_matches_oracle(window, eager, resident):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world,xself", [(2, 1), (4, 1), (8, 1), (4, 0)])
-def test_gpu_sharded_16m_x_1m_matches_oracle(world, xself, monkeypatch):
+@pytest.mark.parametrize("world,xself,xcfirst", [(2, 1, 1), (4, 1, 1), (8, 1, 1), (4, 0, 1), (2, 1, 0)])
+def test_gpu_sharded_16m_x_1m_matches_oracle(world, xself, xcfirst, monkeypatch):
     """configs[3]: 16M pending tasks x 1M workers, the worker table sharded by
     slot range over `world` rank contexts on one GPU; the exchange buffers are
     summed on the device (what the RCCL all-reduce computes).  xself 0: k_xscan's last
     workgroup prefixes the chunk totals (fb_set_path("xself", 0)) instead of phase 2's
-    emission workgroups."""
+    emission workgroups; xcfirst 0: phase 2's compaction workgroups after its queue
+    workgroups in the grid (fb_set_path("xcfirst", 0))."""
     from faasbal.balancer import TEST_PATHS
     monkeypatch.setitem(TEST_PATHS, "xself", xself)
+    monkeypatch.setitem(TEST_PATHS, "xcfirst", xcfirst)
     from test_gpu_sharded import _cmp as _cmp_sharded, _group, _group_tick
     W, T = 1 << 20, 16_000_000
     st = synth.zipf_state(W=W, seed=0)
