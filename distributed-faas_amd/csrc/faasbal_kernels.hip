@@ -1549,7 +1549,7 @@ __device__ __forceinline__ void q_raw_slow(const TickArgs &a, int64_t pos, bool 
 template <int QT>
 __device__ __forceinline__ void queue_tiles(const TickArgs &a, int b0) {
     __shared__ uint32_t qh[kWaves][kRFused + 1];
-    __shared__ uint32_t qwc[QT][kWaves][kRFused];
+    __shared__ uint8_t qwc[QT][kWaves][kRFused];  // per-wave counts (<= 64): bytes keep k_scan at 8 workgroups per CU
     __shared__ uint32_t qm[QT][kWaves], qsum[QT][kWaves];
     const int t = threadIdx.x, lane = lane_id(), w = wave_id(), R = a.R;
     int sqv[QT];
@@ -1610,7 +1610,7 @@ __device__ __forceinline__ void queue_tiles(const TickArgs &a, int b0) {
             const int r = 64 * k + lane;
             const uint32_t hv = h[r < R ? r : R];
             const uint32_t P = carry + wave_incl_scan_u32(r < R ? hv : 0u);
-            if (r < R) qwc[j][w][r] = 64u - P;
+            if (r < R) qwc[j][w][r] = (uint8_t)(64u - P);
             carry = (uint32_t)__builtin_amdgcn_readlane((int)P, 63);
         }
         // capacity sum_r count(c > r) over r < R = sum of min(c, R); max c
@@ -1628,7 +1628,7 @@ __device__ __forceinline__ void queue_tiles(const TickArgs &a, int b0) {
         const int b = b0 + j;
         if (b >= a.nbq) break;  // (uniform)
         if (t < R) {
-            const uint32_t n = qwc[j][0][t] + qwc[j][1][t] + qwc[j][2][t] + qwc[j][3][t];
+            const uint32_t n = (uint32_t)qwc[j][0][t] + qwc[j][1][t] + qwc[j][2][t] + qwc[j][3][t];
             a.qcnt[(size_t)b * R + t] = n;
             // the group's row of round totals (memory-side atomics, no return)
             if (a.grp_on && n) atomicAdd(&a.grp[(b >> a.gshift) * a.gstride + t], n);
@@ -1648,7 +1648,7 @@ __device__ __forceinline__ void queue_tiles(const TickArgs &a, int b0) {
 // effective free count c of every LRU position and the block's count of c > r
 // for every round r (table laid out [block][round]).
 template <int MODE, int WT>
-__global__ __launch_bounds__(kBS) void k_scan(TickArgs a_) {
+__global__ __launch_bounds__(kBS, (WT == 4 ? 8 : 1)) void k_scan(TickArgs a_) {
     STAMP_TOP(a_, a_.nbw);
     prefetch_args(a_);
     const TickArgs a = specialise<MODE>(a_);
