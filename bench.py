@@ -852,14 +852,14 @@ def main():
         line["value"] = cm["value_with_commit"]
         line["ms_per_step"] = cm["ms_per_step_with_commit"]
         line["roofline"]["tick_frac"] = B / (cm["ms_per_step_with_commit"] * 1e-3) / 1e9 / HBM_PEAK_GBS
-        cm["note"] = ("the configs[2] tick's commit (its 3277-ish evicted records' deletion and its orphaned log "
-                      "entries) folded into the NEXT tick (folded): the records in k_scan's W role, the log entries "
+        cm["note"] = ("the tick's commit (its %d evicted records' deletion and its %d orphaned log entries) "
+                      "folded into the NEXT tick (folded): the records in k_scan's W role, the log entries "
                       "by k_emit2's log workgroup of each tile (fused ticks) or extra k_scan blocks. That next tick "
                       "runs on the committed, depleted state (kernels_ms: fewer queued positions and tasks than the "
                       "timed step's tick.kernels_avg_ms), so only the delta carries over: commit_in_tick_ms = its "
                       "kernels with the fold pending - the same tick relaunched without it (same state); "
                       "ms_per_step_with_commit = the timed region's ms_per_step + that delta (the line's value and "
-                      "ms_per_step)")
+                      "ms_per_step)" % (n_evicted, O))
         line["committed"] = cm
     if world == 1 and not args.no_host_observed:
         line["host_observed"] = host_observed(g, st, T, min(args.steps, 50), n_assigned)

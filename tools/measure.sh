@@ -12,5 +12,5 @@ timeout -k 10 300 python -u bench.py --workload stream --no-cpu-baseline > gpuru
 cat gpurun_out/${T}_stream.json
 timeout -k 10 300 python -u bench.py --workload cfg3 --no-cpu-baseline > gpurun_out/${T}_cfg3.json 2> gpurun_out/${T}_cfg3.err || { tail -20 gpurun_out/${T}_cfg3.err; exit 5; }
 cat gpurun_out/${T}_cfg3.json
-timeout -k 10 400 python -u tools/shard_probe.py --workload cfg3 --reps 20 > gpurun_out/${T}_shard_cfg3.log 2>&1 || { tail -20 gpurun_out/${T}_shard_cfg3.log; exit 6; }
+timeout -k 10 400 python -u tools/shard_probe.py --workload cfg3 --reps 20 --gated > gpurun_out/${T}_shard_cfg3.log 2>&1 || { tail -20 gpurun_out/${T}_shard_cfg3.log; exit 6; }
 cat gpurun_out/${T}_shard_cfg3.log
