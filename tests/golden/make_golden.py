@@ -20,7 +20,7 @@ registrations that died during the tick are put, in ascending original dispatch
 sequence, ahead of the pending tasks.
 
 Only data leaves this script: ``tests/golden/*.npz`` (inputs + expected outputs).
-No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque|cfg2full]
+No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque|cfg2full|cfg3full]
 
 The same harness drives the loop without heartbeats, ``PushDispatcher.start``
 (``task_dispatcher.py:251-322``, a deque of ids instead of the OrderedDict) for
@@ -413,12 +413,13 @@ def digests(assign, orphans, evicted, post_reg, post_free, post_hb, post_queue):
 # BASELINE.json configs[2] at its stated size: the headline tick pinned against the
 # reference itself (digests only: the outputs are MBs; tests recompute them)
 CFG2_FULL = dict(W=65536, seed=0, T=1_000_000, now=1000.0, tte=10.0)
+# ... and configs[3]'s one-GPU tick (16 M pending tasks x 1 M workers), the same way
+CFG3_FULL = dict(W=1 << 20, seed=0, T=16_000_000, now=1000.0, tte=10.0)
 
 
-def cfg2_full_fixture(td):
+def cfg2_full_fixture(td, p=CFG2_FULL, name="cfg2_full_digests.json"):
     import json
     import time
-    p = CFG2_FULL
     st = synth.zipf_state(W=p["W"], seed=p["seed"])
     scen = synth.state_to_scenario(st, [synth.empty_tick(p["now"], p["T"])], tte=p["tte"])
     t0 = time.perf_counter()
@@ -431,7 +432,7 @@ def cfg2_full_fixture(td):
                n_evicted=int(len(o["evicted"])), n_pending=int(o["n_pending"]),
                digests=digests(o["assign"], o["orphans"], o["evicted"], o["post_reg"], o["post_free"], o["post_hb"],
                                o["post_queue"]))
-    path = os.path.join(HERE, "cfg2_full_digests.json")
+    path = os.path.join(HERE, name)
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
     return [path]
@@ -446,6 +447,8 @@ def main(which="all"):
         made += deque_fixtures(td)
     if which in ("all", "cfg2full"):
         made += cfg2_full_fixture(td)
+    if which == "cfg3full":  # (about an hour of reference loop; not part of "all")
+        made += cfg2_full_fixture(td, CFG3_FULL, "cfg3_full_digests.json")
     for p in made:
         print(p, os.path.getsize(p))
 
