@@ -220,8 +220,10 @@ class RefHarness:
                 orph.append(seq)
                 rec[2] = "orphaned"
         self.orphans = orph
-        self.pending = [("orphan", seq) for seq in orph] + self.carried + \
-            [("new", tid) for tid in self.new_ids]
+        # (a deque: taken from the front one task per loop iteration -- a list's pop(0)
+        # made the 1M-task capture O(T^2) and a 16M-task one a matter of hours)
+        self.pending = collections.deque([("orphan", seq) for seq in orph] + list(self.carried) +
+                                         [("new", tid) for tid in self.new_ids])
         self.n_pending = len(self.pending)
 
     def _finish_iteration(self):
@@ -338,7 +340,7 @@ class RefHarness:
         if not self.pending:
             self.gm_task = False
             return None
-        kind, ref = self.pending.pop(0)
+        kind, ref = self.pending.popleft()
         tid = self.records[ref][3] if kind == "orphan" else ref
         self._cur_task_id = tid
         self.gm_task = True

@@ -6,8 +6,10 @@
   unmodified ``task_dispatcher.py:324-419`` with a purge once per unchanged clock).
 * configs[4] (64K new tasks per tick against 1M workers with churn): committed
   ticks, the HIP path against the oracle, bit-exact on every output.
-* configs[3] (16M tasks x 1M workers) sharded over world 2 and 4: one tick of the
-  rank contexts (single process, exchange summed on the device) against the oracle.
+* configs[3] (16M tasks x 1M workers): the oracle and the one-GPU HIP tick against
+  digests captured from the reference loop the same way (``cfg3_full_digests.json``,
+  ``make_golden.py cfg3full``); sharded over world 2 / 4 / 8: one tick of the rank
+  contexts (single process, exchange summed on the device) against the oracle.
 """
 import json
 import os
@@ -26,15 +28,16 @@ from faasbal import synth  # noqa: E402
 from make_golden import digests  # noqa: E402  (pure numpy: no reference code is loaded)
 
 CFG2 = json.load(open(os.path.join(HERE, "golden", "cfg2_full_digests.json")))
+CFG3 = json.load(open(os.path.join(HERE, "golden", "cfg3_full_digests.json")))
 
 
-def _cfg2_state():
-    p = CFG2["params"]
+def _cfg2_state(fx=CFG2):
+    p = fx["params"]
     return p, synth.zipf_state(W=p["W"], seed=p["seed"])
 
 
-def _check(d, where):
-    for k, v in CFG2["digests"].items():
+def _check(d, where, fx=CFG2):
+    for k, v in fx["digests"].items():
         assert d[k] == v, "%s: %s differs from the reference capture (%s)" % (where, k, d[k])
 
 
@@ -60,6 +63,34 @@ def test_gpu_cfg2_full_matches_reference():
     assert out["result"]["n_assigned"] == CFG2["n_assigned"]
     _check(digests(out["assign"], out["orphans"], out["evicted"], sg["reg"], sg["free"], sg["hb"], sg["queue"]),
            "HIP tick")
+    g.close()
+
+
+def test_oracle_cfg3_full_matches_reference():
+    """The oracle at configs[3]'s size (16M tasks x 1M workers, one tick) against the
+    reference loop's own outputs (digests)."""
+    from oracle import Oracle
+    p, st = _cfg2_state(CFG3)
+    o = Oracle(p["W"], len(st["log"]) + p["T"] + len(st["log"]) + 16, purge_mode=1)
+    o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
+    out = o.tick(p["now"], p["tte"], [], [], [], [], [], p["T"])
+    so = o.export()
+    _check(digests(out["assign"], out["orphans"], out["evicted"], so["reg"], so["free"], so["hb"], so["queue"]),
+           "oracle", CFG3)
+
+
+@pytest.mark.gpu
+def test_gpu_cfg3_full_matches_reference():
+    """The one-GPU HIP tick at configs[3]'s size against the reference capture."""
+    from faasbal import GpuBalancer
+    p, st = _cfg2_state(CFG3)
+    g = GpuBalancer(p["W"], 2 * len(st["log"]) + p["T"] + 16, max_events=1, device=0)
+    g.load(st)
+    out = g.tick(p["now"], p["tte"], n_pending=p["T"])
+    sg = g.read_state(with_log=False)
+    assert out["result"]["n_assigned"] == CFG3["n_assigned"]
+    _check(digests(out["assign"], out["orphans"], out["evicted"], sg["reg"], sg["free"], sg["hb"], sg["queue"]),
+           "HIP tick", CFG3)
     g.close()
 
 
