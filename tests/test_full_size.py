@@ -178,6 +178,12 @@ def test_gpu_sharded_16m_x_1m_matches_oracle(world, xself, xcfirst, monkeypatch)
     b = o.tick(1000.0, 10.0, [], [], [], [], [], T)
     assert len(b["assign"]) == res["n_assigned"] > 0 and len(b["orphans"]) > 0
     _cmp_sharded(bals, o, merged, b, 0)
+    # ... and the merged decisions against the reference loop's own (cfg3_full_digests.json)
+    import hashlib
+    assert CFG3["params"]["W"] == W and CFG3["params"]["T"] == T
+    for k, dt in (("assign", "<i4"), ("orphans", "<i8"), ("evicted", "<i4")):
+        h = hashlib.sha256(np.asarray(merged[k], dt).tobytes()).hexdigest()
+        assert h == CFG3["digests"][k]["sha256"], "sharded world %d: %s differs from the reference capture" % (world, k)
     for x in bals:
         x.close()
 
