@@ -20,7 +20,7 @@ registrations that died during the tick are put, in ascending original dispatch
 sequence, ahead of the pending tasks.
 
 Only data leaves this script: ``tests/golden/*.npz`` (inputs + expected outputs).
-No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque|cfg2full|cfg3full]
+No reference source is copied.  Usage:  python tests/golden/make_golden.py [all|heartbeat|deque|cfg1full|cfg2full|cfg3full]
 
 The same harness drives the loop without heartbeats, ``PushDispatcher.start``
 (``task_dispatcher.py:251-322``, a deque of ids instead of the OrderedDict) for
@@ -417,17 +417,21 @@ def digests(assign, orphans, evicted, post_reg, post_free, post_hb, post_queue):
 CFG2_FULL = dict(W=65536, seed=0, T=1_000_000, now=1000.0, tte=10.0)
 # ... and configs[3]'s one-GPU tick (16 M pending tasks x 1 M workers), the same way
 CFG3_FULL = dict(W=1 << 20, seed=0, T=16_000_000, now=1000.0, tte=10.0)
+# ... and configs[1] (100K tasks x 1K workers, uniform loads)
+CFG1_FULL = dict(W=1000, seed=0, T=100_000, now=1000.0, tte=10.0, loads="uniform")
 
 
 def cfg2_full_fixture(td, p=CFG2_FULL, name="cfg2_full_digests.json"):
     import json
     import time
-    st = synth.zipf_state(W=p["W"], seed=p["seed"])
+    uniform = p.get("loads") == "uniform"
+    st = (synth.uniform_state if uniform else synth.zipf_state)(W=p["W"], seed=p["seed"])
     scen = synth.state_to_scenario(st, [synth.empty_tick(p["now"], p["T"])], tte=p["tte"])
     t0 = time.perf_counter()
     o = capture(td, scen, purge_once=True)[0]
     dt = time.perf_counter() - t0
-    out = dict(params=p, generator="faasbal.synth.zipf_state(W, seed) + one tick of T pending tasks at now",
+    out = dict(params=p, generator="faasbal.synth.%s(W, seed) + one tick of T pending tasks at now" % (
+                   "uniform_state" if uniform else "zipf_state"),
                reference="task_dispatcher.py:324-419 via tests/golden/make_golden.py (purge once per unchanged "
                          "clock, SURVEY.md App. B), %.1f s in the capture container" % dt,
                n_assigned=int(len(o["assign"])), n_orphans=int(len(o["orphans"])),
@@ -449,6 +453,8 @@ def main(which="all"):
         made += deque_fixtures(td)
     if which in ("all", "cfg2full"):
         made += cfg2_full_fixture(td)
+    if which in ("all", "cfg1full"):
+        made += cfg2_full_fixture(td, CFG1_FULL, "cfg1_full_digests.json")
     if which == "cfg3full":  # (about an hour of reference loop; not part of "all")
         made += cfg2_full_fixture(td, CFG3_FULL, "cfg3_full_digests.json")
     for p in made:

@@ -29,11 +29,13 @@ from make_golden import digests  # noqa: E402  (pure numpy: no reference code is
 
 CFG2 = json.load(open(os.path.join(HERE, "golden", "cfg2_full_digests.json")))
 CFG3 = json.load(open(os.path.join(HERE, "golden", "cfg3_full_digests.json")))
+CFG1 = json.load(open(os.path.join(HERE, "golden", "cfg1_full_digests.json")))
 
 
 def _cfg2_state(fx=CFG2):
     p = fx["params"]
-    return p, synth.zipf_state(W=p["W"], seed=p["seed"])
+    gen = synth.uniform_state if p.get("loads") == "uniform" else synth.zipf_state
+    return p, gen(W=p["W"], seed=p["seed"])
 
 
 def _check(d, where, fx=CFG2):
@@ -66,31 +68,36 @@ def test_gpu_cfg2_full_matches_reference():
     g.close()
 
 
-def test_oracle_cfg3_full_matches_reference():
-    """The oracle at configs[3]'s size (16M tasks x 1M workers, one tick) against the
-    reference loop's own outputs (digests)."""
+@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
+def test_oracle_full_matches_reference(name):
+    """The oracle at configs[1]'s (100K tasks x 1K workers, uniform loads) and configs[3]'s
+    (16M tasks x 1M workers) sizes, one tick, against the reference loop's own outputs."""
+    fx = dict(cfg1=CFG1, cfg3=CFG3)[name]
     from oracle import Oracle
-    p, st = _cfg2_state(CFG3)
+    p, st = _cfg2_state(fx)
     o = Oracle(p["W"], len(st["log"]) + p["T"] + len(st["log"]) + 16, purge_mode=1)
     o.load(st["reg"], st["free"], st["hb"], st["epoch"], st["queue"], st["log"])
     out = o.tick(p["now"], p["tte"], [], [], [], [], [], p["T"])
     so = o.export()
     _check(digests(out["assign"], out["orphans"], out["evicted"], so["reg"], so["free"], so["hb"], so["queue"]),
-           "oracle", CFG3)
+           "oracle", fx)
 
 
 @pytest.mark.gpu
-def test_gpu_cfg3_full_matches_reference():
-    """The one-GPU HIP tick at configs[3]'s size against the reference capture."""
+@pytest.mark.parametrize("name", ["cfg1", "cfg3"])
+def test_gpu_full_matches_reference(name):
+    """The one-GPU HIP tick at configs[1]'s and configs[3]'s sizes against the reference
+    captures."""
     from faasbal import GpuBalancer
-    p, st = _cfg2_state(CFG3)
+    CFG = dict(cfg1=CFG1, cfg3=CFG3)[name]
+    p, st = _cfg2_state(CFG)
     g = GpuBalancer(p["W"], 2 * len(st["log"]) + p["T"] + 16, max_events=1, device=0)
     g.load(st)
     out = g.tick(p["now"], p["tte"], n_pending=p["T"])
     sg = g.read_state(with_log=False)
-    assert out["result"]["n_assigned"] == CFG3["n_assigned"]
+    assert out["result"]["n_assigned"] == CFG["n_assigned"]
     _check(digests(out["assign"], out["orphans"], out["evicted"], sg["reg"], sg["free"], sg["hb"], sg["queue"]),
-           "HIP tick", CFG3)
+           "HIP tick", CFG)
     g.close()
 
 
