@@ -94,9 +94,12 @@ constexpr uint8_t kStQ0 = 8;
 // Committed per-slot heartbeat: last_heartbeat, NaN when the slot holds no record
 // (so the log scan's one 8-byte gather per in-flight entry decides liveness
 // without a registered flag); the first log sequence of the current registration
-// lives in its own array (epoch) that no scan reads.  Log entries of a dead
-// registration are cleared (-1) when the tick that redistributed them commits,
-// so every live entry belongs to its slot's current registration.
+// lives in its own array (epoch).  Log entries of a dead registration are cleared (-1)
+// when the tick that redistributed them commits -- except on one-GPU heartbeat contexts
+// (round 6, lazy clears): there the commit leaves them, and an entry q naming slot s is
+// live only if s holds a record and q >= epoch[s] (entries of a registration that died
+// are older than any later registration of the slot).  Kernels test that (live_chk) only
+// once such entries may exist; state reads clear them first (k_log_normalize).
 
 // Post-message record of a slot that got messages this tick (k_ev_apply*): one
 // 16-byte store per slot; its registered flag and queue flags ride in post_rf
@@ -208,6 +211,7 @@ struct EvArgs {
     uint32_t *post_infl;
     int32_t *bud_next;
     int orph_grp;         // the slot purge adds the orphans of dead registrations to column R + 1
+    int live_chk;         // lazy clears: a result completes entry q only if it is live (reg at tick start, q >= epoch)
     int32_t *front_rank, *back_rank;   // deque: rank of a new token among its slot's tokens
     int32_t *post_tok, *post_nf;       // deque: tokens per slot after the messages; new front tokens
     int shard;          // 0: one GPU; else this rank owns global slots [slot_base, slot_base + W)
@@ -426,6 +430,10 @@ struct TickArgs {
     int cmix;     // k_emit2: compaction workgroups interleaved with the queue blocks
     int wtiles;   // k_scan: slot tiles per W-role workgroup (1, 2 or 4)
     int qtiles;   // k_scan (one GPU, unfused, 4-tile instance): queue blocks per Q-role workgroup (1 or 4)
+    // lazy clears (one-GPU heartbeat contexts): entries of dead registrations may remain in
+    // the log; an orphan flag needs q >= epoch[s] (the committed epoch of its died slot)
+    int live_chk;
+    const uint32_t *epoch;
     int xcfirst;  // k_emit_shard_xp: the compaction workgroups first in the grid
     // sharded phase 2 (fb_set_full_assign): this rank also writes the whole tick's task -> slot
     // array (every rank computes the global water-filling; one rank's copy serves the host)
@@ -480,6 +488,7 @@ void launch_selftest(uint32_t *err, uint32_t seed, Stream st);
 // a one-lane kernel that holds the stream until flag[0] == want (host-mapped word) or
 // `limit` ticks of the 100 MHz realtime counter pass (then flag[1] = 1)
 void launch_gate(uint32_t *flag, uint32_t want, uint64_t limit, Stream st);
+void launch_log_normalize(int32_t *log, int64_t n, const uint8_t *reg, const uint32_t *epoch, Stream st);
 void launch_slots(const TickArgs &a, Stream st);
 void launch_scan(const TickArgs &a, Stream st);
 void launch_logscan(const TickArgs &a, int grid, Stream st);

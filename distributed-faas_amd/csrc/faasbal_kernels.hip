@@ -639,6 +639,8 @@ __device__ void ev_apply_deque(const EvArgs &a, int j, uint32_t s) {
 // iteration at the message's own clock first).  s: local slot, gs: global slot.
 struct SlotRun {
     int reg, inq, q0, qstat, qidx, cur_is_start, died_start;
+    int reg_s;       // registered at tick start (lazy clears: its entries >= ep_s are in flight)
+    uint32_t ep_s;
     int32_t fr;
     double hb;
     uint32_t epoch;
@@ -650,6 +652,8 @@ struct SlotRun {
         fr = fq.x;
         hb = a.hb[s];
         epoch = a.epoch[s];
+        reg_s = reg;
+        ep_s = epoch;
         // a slot without a record has no in-flight entries (its budget is stale)
         infl0 = (a.defer_clr && reg) ? (uint32_t)(a.bud[s] - fq.x) : 0u;
         ncl = 0;
@@ -693,7 +697,10 @@ struct SlotRun {
             fr += 1;
             hb = ts;
             const int64_t q = seq;
-            if (q >= 0 && q < a.head_in) {
+            // lazy clears: an entry of a registration that died before this tick is still in
+            // the log naming the slot, but not in flight
+            const bool live = !a.live_chk || (reg_s && (uint64_t)q >= (uint64_t)ep_s);
+            if (q >= 0 && q < a.head_in && live) {
                 if (PF) {
                     // one GPU: the entry's slot loaded ahead.  defer_clr: the log stays as
                     // committed (the commit clears the entry), ctag names the entry for this
@@ -1508,6 +1515,21 @@ __device__ __forceinline__ uint32_t drop_completed(const A &a, uint32_t flags, c
     return flags;
 }
 
+// Lazy clears (one-GPU heartbeat contexts): drop from a row's orphan flags the entries older
+// than their died slot's registration -- entries of an earlier, dead registration that its
+// commit left in the log (bit j: entry base + j, slot v[j]).  Only once such entries may exist.
+template <int N, class A>
+__device__ __forceinline__ uint32_t drop_stale(const A &a, uint32_t flags, const int32_t *v, int64_t base) {
+    if (!a.live_chk || !flags) return flags;
+    uint32_t e[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) e[j] = a.epoch[((flags >> j) & 1u) ? v[j] : 0];  // (every gather in flight)
+#pragma unroll
+    for (int j = 0; j < N; ++j)
+        if (((flags >> j) & 1u) && (uint64_t)(base + j) < (uint64_t)e[j]) flags &= ~(1u << j);
+    return flags;
+}
+
 // The registration of slot s alive at tick start died during this tick (read
 // straight from the record: used by k_scan's log role when no bitmap exists).
 // Committed hb is NaN for unregistered slots, so the untouched case is one load.
@@ -1739,7 +1761,7 @@ __global__ __launch_bounds__(kBS, (WT == 4 ? 8 : 1)) void k_scan(TickArgs a_) {
             died |= (v[j] >= 0 && ((wd >> (sj & 63)) & 1ull)) ? (1u << j) : 0u;
         }
         }
-        const uint32_t flags = drop_completed(a, died, v, base);
+        const uint32_t flags = drop_completed(a, drop_stale<kFItems>(a, died, v, base), v, base);
         a.ofl[(size_t)b * kBS + threadIdx.x] = (uint8_t)flags;
         const uint32_t wv = wave_sum_u32((uint32_t)__popc(flags));
         if (lane_id() == 0) l4[wave_id()] = wv;
@@ -2239,7 +2261,8 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
                 const uint32_t *bm32 = reinterpret_cast<const uint32_t *>(bm);
                 flags |= (sj >= 0 && ((bm32[sc >> 5] >> (sc & 31)) & 1u)) ? (1u << j) : 0u;
             }
-            flags = drop_completed(a, flags, v[k], (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems);
+            const int64_t fb0 = (int64_t)b * kFTile + (int64_t)(k * 64 + lane) * kFItems;
+            flags = drop_completed(a, drop_stale<kFItems>(a, flags, v[k], fb0), v[k], fb0);
             if (a.wseg) {
                 // the tile's orphans, ascending, into its own segment (orphans[b*2048 + i]):
                 // entry order is k, then lane, then j
@@ -3019,7 +3042,7 @@ __device__ __forceinline__ void emit_log_tile(const TickArgs &a, int t, unsigned
             m |= (sj >= 0 && ((bm[sc >> 6] >> (sc & 63)) & 1ull)) ? (1u << q) : 0u;
         }
         const int64_t e0 = tbase + k * 1024 + 4 * tid;
-        m = drop_completed(a, m, v[k], e0);
+        m = drop_completed(a, drop_stale<4>(a, m, v[k], e0), v[k], e0);
         uint32_t tot;
         const uint32_t ex = block_excl_scan_u32((uint32_t)__popc(m), l4, tot);
         int64_t oo = o + ex;
@@ -5078,6 +5101,18 @@ void launch_copy_words(uint32_t *dst, const uint32_t *src, int64_t n, Stream st)
 // `want` into it, so the launches queued behind this kernel run back to back, free of
 // the host's enqueue pace.  Every exit path is bounded: after `limit` ticks of the
 // 100 MHz realtime counter the gate opens by itself and reports it in flag[1].
+// Lazy clears: the deferred clears of every entry whose registration died (no record, or
+// older than the slot's epoch) -- before a state read, so the log reads as it would had
+// every commit cleared its orphans
+__global__ __launch_bounds__(kBS) void k_log_normalize(int32_t *__restrict__ log, int64_t n,
+                                                       const uint8_t *__restrict__ reg,
+                                                       const uint32_t *__restrict__ epoch) {
+    for (int64_t q = (int64_t)blockIdx.x * kBS + threadIdx.x; q < n; q += (int64_t)gridDim.x * kBS) {
+        const int32_t s = log[q];
+        if (s >= 0 && (!reg[s] || (uint64_t)q < (uint64_t)epoch[s])) log[q] = -1;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_gate(uint32_t *flag, uint32_t want, uint64_t limit) {
     if (threadIdx.x != 0) return;
     const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
@@ -5094,6 +5129,11 @@ int emit_win_resident_per_cu() {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_emit_win, kBS, 0) != hipSuccess) return 0;
     return n;
+}
+void launch_log_normalize(int32_t *log, int64_t n, const uint8_t *reg, const uint32_t *epoch, Stream st) {
+    if (n <= 0) return;
+    const int grid = (int)std::min<int64_t>(cdiv(n, kBS), 8192);
+    hipExtLaunchKernelGGL(k_log_normalize, dim3(grid), dim3(kBS), 0, st.s, st.e0, st.e1, 0, log, n, reg, epoch);
 }
 void launch_gate(uint32_t *flag, uint32_t want, uint64_t limit, Stream st) {
     hipExtLaunchKernelGGL(k_gate, dim3(1), dim3(64), 0, st.s, st.e0, st.e1, 0, flag, want, limit);
