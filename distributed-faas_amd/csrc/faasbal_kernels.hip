@@ -1714,7 +1714,8 @@ __global__ __launch_bounds__(kBS, (WT == 4 ? 8 : 1)) void k_scan(TickArgs a_) {
             for (int j = 0; j < kFItems; ++j) v[j] = v[j] < 0 ? -1 : v[j] - a.slot_base;
         }
         // an entry is an orphan iff its slot's registration alive at tick start died this
-        // tick (entries of earlier registrations were cleared when their tick committed)
+        // tick (entries of earlier registrations were cleared when their tick committed, or --
+        // lazy clears -- are older than the slot's epoch: drop_stale)
         uint32_t died = 0;
         if (a.slots_in_scan) {
             // died-at-start straight from the heartbeats: 8 independent 8-byte gathers per
@@ -2247,7 +2248,8 @@ __global__ __launch_bounds__(kLsBS) void k_logscan(TickArgs a) {
             }
         }
         // died bits from LDS: an entry is an orphan iff its slot's registration alive at
-        // tick start died (entries of earlier registrations are cleared at commit)
+        // tick start died (entries of earlier registrations: cleared at commit, or older than
+        // the slot's epoch under lazy clears -- drop_stale)
         uint32_t cnt = 0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
