@@ -294,6 +294,13 @@ int fb_debug_read(fb_ctx *ctx, unsigned long long *dst, int64_t n, int64_t *n_to
  *   "wtiles"      slot tiles (256 slots each) per slot-purge workgroup: 0 auto (k_scan: 4 on
  *                 unfused tables, 1 fused; k_ev_apply_ll: 4 from 1024 tiles), or 1, 2, 4
  *                 (k_ev_apply_ll: 2 runs as 1);
+ *   "qtiles"      k_scan's queue role on unfused one-GPU tables: 0 auto (four queue blocks
+ *                 per workgroup), 1 one;
+ *   "xcfirst"     sharded xplan phase 2: 1 k_emit_shard_xp's compaction workgroups first in
+ *                 its grid when they are many (default), 0 after the queue workgroups;
+ *   "lazy"        one-GPU heartbeat contexts: 1 commits leave the log entries they
+ *                 redistributed, every later reader tests liveness (default), 0 commits clear
+ *                 them (the entries left so far are cleared first);
  *   "gpcheck"     diagnostic (stamps builds): k_plan2 runs beside a gp tick for comparison.
  * Between ticks only; FB_EINVAL for an unknown name or value. */
 int fb_set_path(fb_ctx *ctx, const char *name, int value);
